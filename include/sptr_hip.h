@@ -1,0 +1,203 @@
+/* sptr_hip.h — C ABI of libsptr_hip.so, the MI355X (gfx950) wavefront path-tracing backend.
+ *
+ * Drop-in boundary: these entry points are what a binding for the reference's GPU backend slot
+ * needs.  The reference has no abstract backend interface; GLRenderer::renderLoop drives the
+ * concrete OptixBackend class (/root/reference/src/GLRenderer.cpp:116-176) through the surface in
+ * /root/reference/include/backends/OptixBackend.h:39-71.  Mapping (each entry cites what it replaces):
+ *
+ *   sptr_create / sptr_destroy   <- OptixBackend::OptixBackend / destroy()        (OptixBackend.h:41-66)
+ *   sptr_upload_scene            <- OptixBackend::build(const SceneDesc&)         (OptixBackend.h:46;
+ *                                   GAS/IAS builds at src/backends/OptixBackend.cpp:916-1308), fed the
+ *                                   world-space flattening of EmbreeBackend::build
+ *                                   (src/backends/EmbreeBackend.cpp:18-193) so geomIDs match the CPU path
+ *   sptr_set_materials           <- OptixBackend::setMaterialManager              (OptixBackend.h:59)
+ *   sptr_set_lights              <- OptixBackend::setLightManager                 (OptixBackend.h:63)
+ *   sptr_set_environment         <- OptixBackend::setEnvironment                  (OptixBackend.h:55)
+ *   sptr_render + sptr_read_rgb8 <- OptixBackend::render(uint8_t* rgb,w,h,Camera) (OptixBackend.h:51;
+ *                                   src/backends/OptixBackend.cpp:1506-1850)
+ *   sptr_set_debug_mode          <- OptixBackend::setDebugMode                    (OptixBackend.h:71)
+ *
+ * Semantics are those of the CPU Embree wavefront integrator (src/wavefront/wf_pt_cpu.cpp:61-255
+ * driven by src/GLRenderer.cpp:353-435), not of the OptiX device programs.
+ *
+ * Conventions: 0 = OK, negative = error (sptr_last_error has the text); no exceptions, no exit()
+ * across the ABI.  The caller owns every host buffer; upload calls copy.  One context per GPU, used
+ * from one host thread at a time; contexts are independent.  Device pointers handed out stay valid
+ * until the next render call with a different size, or sptr_destroy.
+ */
+#ifndef SPTR_HIP_H
+#define SPTR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPTR_ABI_VERSION 1
+
+enum sptr_status {
+  SPTR_OK = 0,
+  SPTR_ERR_INVALID = -1,   /* bad argument / shape */
+  SPTR_ERR_HIP = -2,       /* HIP runtime error */
+  SPTR_ERR_NO_SCENE = -3,  /* render before upload / materials */
+  SPTR_ERR_OOM = -4,
+  SPTR_ERR_NO_DEVICE = -5
+};
+
+typedef struct sptr_ctx sptr_ctx;
+
+/* World-space flattened scene, geomID order of EmbreeBackend::build: one triangle geometry per
+ * SceneDesc instance (geomIDs 0..num_tri_geoms-1), then one geometry per analytic sphere. */
+typedef struct sptr_scene {
+  const float* positions; /* 3 floats per vertex, world space */
+  uint32_t num_verts;
+  const uint32_t* indices; /* 3 global vertex indices per triangle */
+  uint32_t num_tris;
+  const uint32_t* tri_geom_first; /* num_tri_geoms+1 prefix offsets into the triangle list */
+  uint32_t num_tri_geoms;
+  const float* spheres; /* cx, cy, cz, radius per sphere */
+  uint32_t num_spheres;
+  const uint32_t* geom_material; /* geomID -> material index (EmbreeBackend::geomMaterialId_) */
+} sptr_scene;
+
+/* One entry of MaterialManager's table (include/Material.h:19-39, values after the ctor clamps). */
+typedef struct sptr_material {
+  float albedo[3];
+  float metallic;
+  float roughness;
+  float emission[3];
+  float ior;
+  int32_t type; /* 0 PBR, 1 DIELECTRIC (informational; shading follows metallic/ior) */
+  float pad[2];
+} sptr_material;
+
+/* LightManager entry (include/Light.h:43-81): type 0 = directional (v = direction of the light's
+ * rays, as passed to addDirectionalLight), 1 = point (v = position). */
+typedef struct sptr_light {
+  int32_t type;
+  float v[3];
+  float color[3];
+  float intensity;
+} sptr_light;
+
+/* EnvironmentManager state: faces == NULL selects the procedural sky
+ * (src/EnvironmentManager.cpp:35-61); otherwise 6 cube faces (+X,-X,+Y,-Y,+Z,-Z) of size*size RGB
+ * floats, sampled bilinearly as Cubemap::sample (src/Cubemap.cpp:82-180). */
+typedef struct sptr_environment {
+  const float* faces;
+  int32_t size;
+  float intensity; /* 0.8 in the reference (EnvironmentManager.h:12) */
+  float max_clamp; /* 5.0 */
+} sptr_environment;
+
+/* Camera basis as Camera::updateCameraVectors leaves it (src/Camera.cpp:33-50). */
+typedef struct sptr_camera {
+  float pos[3];
+  float forward[3];
+  float right[3];
+  float up[3];
+  float half_width;
+  float half_height;
+} sptr_camera;
+
+enum sptr_frame_flags {
+  SPTR_FRAME_TIMING = 1u,     /* record per-stage HIP events (adds sync at the end of the call) */
+  SPTR_FRAME_NO_RESOLVE = 2u, /* skip the tonemap/resolve pass */
+  SPTR_FRAME_COUNT_VISITS = 4u /* one instrumented trace pass: count BVH node / primitive fetches */
+};
+
+/* One render call = `spp` progressive frames (samples per pixel) starting at accumulation index
+ * frame_begin (1-based, as GLRenderer::m_accumulated_samples; frame_begin == 1 clears the
+ * accumulation).  Pixels are rendered in 32x32 tiles (GLRenderer.h:36); with shard_count > 1 only
+ * tiles t with t % shard_count == shard_rank are rendered (interleaved multi-GPU sharding). */
+typedef struct sptr_frame {
+  int32_t width, height;
+  sptr_camera camera;
+  uint32_t frame_begin;
+  uint32_t spp;
+  uint32_t max_depth;
+  int32_t shard_rank, shard_count;
+  uint32_t flags;
+} sptr_frame;
+
+typedef struct sptr_stats {
+  uint64_t rays_closest; /* closest-hit queries (primary + extension) = rtcIntersect1 calls */
+  uint64_t rays_shadow;  /* any-hit queries = rtcOccluded1 calls */
+  uint64_t samples;      /* pixel samples completed */
+  uint64_t waves;        /* wavefront batches launched */
+  double ms_total;       /* wall time of the call on the device stream */
+  double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_accum; /* SPTR_FRAME_TIMING only */
+  uint64_t trace_launches;
+  uint64_t node_visits, tri_tests, sphere_tests; /* SPTR_FRAME_COUNT_VISITS only */
+  uint64_t shadow_node_visits, shadow_prim_tests;
+} sptr_stats;
+
+/* ---- context ---------------------------------------------------------------------------------- */
+int sptr_abi_version(void);
+int sptr_create(int device, sptr_ctx** out);
+int sptr_destroy(sptr_ctx* ctx);
+const char* sptr_last_error(const sptr_ctx* ctx);
+int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
+/* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default). */
+int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
+
+/* ---- scene / state (OptixBackend::build and setters) -------------------------------------------- */
+int sptr_upload_scene(sptr_ctx* ctx, const sptr_scene* scene); /* builds the LBVH on the device */
+int sptr_set_materials(sptr_ctx* ctx, const sptr_material* mats, uint32_t count);
+int sptr_set_lights(sptr_ctx* ctx, const sptr_light* lights, uint32_t count);
+int sptr_set_environment(sptr_ctx* ctx, const sptr_environment* env);
+int sptr_scene_info(const sptr_ctx* ctx, uint32_t* num_prims, uint32_t* num_nodes, uint32_t* bvh_depth,
+                    double* build_ms);
+
+/* ---- rendering ---------------------------------------------------------------------------------- */
+/* Renders on the context's stream, or on `stream` (a hipStream_t) when not NULL; returns after the
+ * work completes. */
+int sptr_render(sptr_ctx* ctx, const sptr_frame* frame, void* stream, sptr_stats* stats);
+/* Full image RGB8 (width*height*3; only this shard's tiles are written) and the linear accumulation
+ * sums (width*height*3 floats: sum of samples, divide by the sample count for the mean). */
+int sptr_read_rgb8(sptr_ctx* ctx, uint8_t* rgb);
+int sptr_read_accum(sptr_ctx* ctx, float* accum);
+/* Device view of this shard's resolved tiles: RGBA8, [local tile][32][32] uint32, for the
+ * multi-GPU gather.  *bytes = local_tiles * 4096. */
+int sptr_tiles_device(sptr_ctx* ctx, void** dptr, size_t* bytes);
+/* Scatter gathered tile buffers (rank-major: rank r's local tiles at offset r*tiles_per_rank*4096
+ * bytes) into an RGB8 device image width*height*3. */
+int sptr_unpack_tiles(sptr_ctx* ctx, const void* gathered, int32_t shard_count, uint32_t tiles_per_rank,
+                      int32_t width, int32_t height, void* rgb8_out, void* stream);
+
+/* ---- query entry points (tests / tooling) -------------------------------------------------------- */
+/* Closest-hit / any-hit queries on the device BVH: rays = n*8 floats (o3, d3, tnear, tfar).
+ * Outputs as rtcIntersect1 reports them: geomID (0xFFFFFFFF on miss), primID, t, unnormalised Ng. */
+int sptr_intersect(sptr_ctx* ctx, const float* rays, uint32_t n, uint32_t* geom, uint32_t* prim, float* t,
+                   float* ng);
+int sptr_occluded(sptr_ctx* ctx, const float* rays, uint32_t n, uint8_t* occluded);
+/* Primary rays of the wavefront raygen for a W x H image at accumulation index acc: directions
+ * (W*H*3) and initial path RNG states (W*H), computed by the device kernel. */
+int sptr_primary_rays(sptr_ctx* ctx, const sptr_camera* cam, int32_t width, int32_t height, uint32_t acc,
+                      float* dirs, uint32_t* rng);
+
+/* ---- host-side scene layer (the C++ SceneDesc / Camera / MaterialManager / LightManager mirror) ---- */
+typedef struct sptr_host_scene sptr_host_scene;
+/* name: "default", "default_emitter", "sphere_mesh" (p0 = stacks, p1 = slices), "test_triangle",
+ * or "gltf:<path>" (p0 = material id for the mesh). */
+int sptr_host_builtin_scene(const char* name, uint32_t p0, uint32_t p1, sptr_host_scene** out);
+int sptr_host_scene_view(const sptr_host_scene* s, sptr_scene* view);
+void sptr_host_scene_free(sptr_host_scene* s);
+int sptr_host_camera_lookat(const float pos[3], const float target[3], float fov_deg, float aspect,
+                            sptr_camera* out);
+/* MaterialManager::setupDefaultMaterials presets; with_light appends Materials::Light() as index 9. */
+int sptr_host_preset_materials(int with_light, sptr_material* out, int capacity);
+/* setupLights in src/main.cpp:85-94: one directional sun. */
+int sptr_host_default_lights(sptr_light* out, int capacity);
+/* Cubemap::loadEquirectangular: RGB float equirect (w x h) -> 6 faces of size x size. */
+int sptr_host_equirect_to_faces(const float* rgb, int32_t w, int32_t h, int32_t size, float* faces);
+/* Radiance .hdr reader (RGBE, RLE) -> RGB float; caller frees with sptr_host_free. */
+int sptr_host_load_hdr(const char* path, float** rgb, int32_t* w, int32_t* h);
+void sptr_host_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPTR_HIP_H */

@@ -1,0 +1,406 @@
+// kernels_lbvh.hip — on-device LBVH build replacing Embree's BVH build / OptiX GAS+IAS builds
+// (src/backends/EmbreeBackend.cpp:82-181, src/backends/OptixBackend.cpp:916-1308).
+//
+// One flat BVH2 over every world-space triangle and analytic sphere (typed leaf links):
+//   k_prim_bounds : per-primitive AABB + centroid bounds (ordered-int atomics)
+//   k_morton      : 63-bit Morton code (21 bits/axis) of the centroid, value = primitive id
+//   radix sort    : rocPRIM radix_sort_pairs on the codes
+//   k_leaves      : scatter triangles (v0, e1, e2, Ng precomputed as Embree's TriangleM does) and
+//                   spheres into sorted slots; typed leaf links
+//   k_karras      : Karras 2012 binary radix tree over the sorted codes (ties broken by index)
+//   k_refit       : bottom-up box propagation; the second child to arrive at a node finishes it
+//                   (agent-scope release/acquire, write-through box stores — the hand-off recipe of
+//                   the gfx950 guide, Guideline 16)
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "sptr_internal.h"
+
+namespace sptr {
+
+namespace {
+
+#define LB_CHECK(x)                                                   \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      c.err = std::string("lbvh: ") + #x + ": " + hipGetErrorString(e_); \
+      return SPTR_ERR_HIP;                                            \
+    }                                                                 \
+  } while (0)
+
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+__device__ __forceinline__ uint64_t expand21(uint32_t v) {
+  uint64_t x = v & 0x1FFFFFu;
+  x = (x | x << 32) & 0x1F00000000FFFFull;
+  x = (x | x << 16) & 0x1F0000FF0000FFull;
+  x = (x | x << 8) & 0x100F00F00F00F00Full;
+  x = (x | x << 4) & 0x10C30C30C30C30C3ull;
+  x = (x | x << 2) & 0x1249249249249249ull;
+  return x;
+}
+
+struct BuildIn {
+  const float* pos;
+  const uint32_t* idx;
+  const float4* sph;
+  const uint32_t* tri_geom;
+  uint32_t ntri, nsph, sph_geom_base;
+};
+
+__device__ __forceinline__ void prim_box(const BuildIn& in, uint32_t i, vec3& lo, vec3& hi) {
+  if (i < in.ntri) {
+    const uint32_t a = in.idx[3 * i], b = in.idx[3 * i + 1], c = in.idx[3 * i + 2];
+    const vec3 p0 = v3(in.pos[3 * a], in.pos[3 * a + 1], in.pos[3 * a + 2]);
+    const vec3 p1 = v3(in.pos[3 * b], in.pos[3 * b + 1], in.pos[3 * b + 2]);
+    const vec3 p2 = v3(in.pos[3 * c], in.pos[3 * c + 1], in.pos[3 * c + 2]);
+    lo = v3(fminf(p0.x, fminf(p1.x, p2.x)), fminf(p0.y, fminf(p1.y, p2.y)), fminf(p0.z, fminf(p1.z, p2.z)));
+    hi = v3(fmaxf(p0.x, fmaxf(p1.x, p2.x)), fmaxf(p0.y, fmaxf(p1.y, p2.y)), fmaxf(p0.z, fmaxf(p1.z, p2.z)));
+  } else {
+    const float4 s = in.sph[i - in.ntri];
+    lo = v3(s.x - s.w, s.y - s.w, s.z - s.w);
+    hi = v3(s.x + s.w, s.y + s.w, s.z + s.w);
+  }
+}
+
+__global__ void k_prim_bounds(BuildIn in, float4* blo, float4* bhi, uint32_t* cb) {
+  const uint32_t N = in.ntri + in.nsph;
+  uint32_t mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u};
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    vec3 lo, hi;
+    prim_box(in, i, lo, hi);
+    blo[i] = make_float4(lo.x, lo.y, lo.z, 0.0f);
+    bhi[i] = make_float4(hi.x, hi.y, hi.z, 0.0f);
+    const float c[3] = {0.5f * (lo.x + hi.x), 0.5f * (lo.y + hi.y), 0.5f * (lo.z + hi.z)};
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t o = f2ord(c[k]);
+      mn[k] = min(mn[k], o);
+      mx[k] = max(mx[k], o);
+    }
+  }
+  for (int k = 0; k < 3; ++k) {
+    for (int off = 32; off > 0; off >>= 1) {
+      mn[k] = min(mn[k], (uint32_t)__shfl_xor((int)mn[k], off));
+      mx[k] = max(mx[k], (uint32_t)__shfl_xor((int)mx[k], off));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    for (int k = 0; k < 3; ++k) {
+      atomicMin(&cb[k], mn[k]);
+      atomicMax(&cb[3 + k], mx[k]);
+    }
+  }
+}
+
+__global__ void k_morton(uint32_t N, const float4* blo, const float4* bhi, const uint32_t* cb, uint64_t* keys,
+                         uint32_t* vals) {
+  float lo[3], ext[3];
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = ord2f(cb[k]);
+    ext[k] = ord2f(cb[3 + k]) - lo[k];
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    const float4 a = blo[i], b = bhi[i];
+    const float c[3] = {0.5f * (a.x + b.x), 0.5f * (a.y + b.y), 0.5f * (a.z + b.z)};
+    uint64_t code = 0;
+    for (int k = 0; k < 3; ++k) {
+      const float t = ext[k] > 0.0f ? (c[k] - lo[k]) / ext[k] : 0.5f;
+      const float q = fminf(fmaxf(t * 2097152.0f, 0.0f), 2097151.0f);
+      code |= expand21((uint32_t)q) << (2 - k);
+    }
+    keys[i] = code;
+    vals[i] = i;
+  }
+}
+
+__global__ void k_is_tri(uint32_t N, uint32_t ntri, const uint32_t* vals, uint32_t* flag) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    flag[i] = vals[i] < ntri ? 1u : 0u;
+}
+
+__global__ void k_leaves(BuildIn in, const uint32_t* vals, const uint32_t* tri_slot, float4* tris, uint32_t* tri_geom,
+                         uint32_t* tri_orig, float4* sph, uint32_t* sph_geom, uint32_t* sph_orig, uint32_t* leaf_link) {
+  const uint32_t N = in.ntri + in.nsph;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    const uint32_t prim = vals[i];
+    if (prim < in.ntri) {
+      const uint32_t slot = tri_slot[i];
+      const uint32_t a = in.idx[3 * prim], b = in.idx[3 * prim + 1], c = in.idx[3 * prim + 2];
+      const vec3 v0 = v3(in.pos[3 * a], in.pos[3 * a + 1], in.pos[3 * a + 2]);
+      const vec3 v1 = v3(in.pos[3 * b], in.pos[3 * b + 1], in.pos[3 * b + 2]);
+      const vec3 v2 = v3(in.pos[3 * c], in.pos[3 * c + 1], in.pos[3 * c + 2]);
+      const vec3 e1 = v0 - v1, e2 = v2 - v0;
+      // Ng = cross(e2, e1) with Embree's msub (fma) evaluation
+      const vec3 ng = v3(__builtin_fmaf(e2.y, e1.z, -(e2.z * e1.y)), __builtin_fmaf(e2.z, e1.x, -(e2.x * e1.z)),
+                         __builtin_fmaf(e2.x, e1.y, -(e2.y * e1.x)));
+      tris[3 * slot + 0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+      tris[3 * slot + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+      tris[3 * slot + 2] = make_float4(e2.z, ng.x, ng.y, ng.z);
+      tri_geom[slot] = in.tri_geom[prim];
+      tri_orig[slot] = prim;
+      leaf_link[i] = kLeafBit | slot;
+    } else {
+      const uint32_t slot = i - tri_slot[i];
+      const uint32_t s = prim - in.ntri;
+      sph[slot] = in.sph[s];
+      sph_geom[slot] = in.sph_geom_base + s;
+      sph_orig[slot] = s;
+      leaf_link[i] = kLeafBit | kSphereBit | slot;
+    }
+  }
+}
+
+__device__ __forceinline__ int delta(const uint64_t* keys, int N, int i, int j) {
+  if (j < 0 || j >= N) return -1;
+  const uint64_t a = keys[i], b = keys[j];
+  if (a == b) return 64 + __clz((uint32_t)(i ^ j));
+  return __clzll((long long)(a ^ b));
+}
+
+__global__ void k_karras(int N, const uint64_t* keys, const uint32_t* leaf_link, BvhNode* nodes, uint32_t* leaf_parent) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
+    const int d = (delta(keys, N, i, i + 1) - delta(keys, N, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta(keys, N, i, i - d);
+    int lmax = 2;
+    while (delta(keys, N, i, i + lmax * d) > dmin) lmax *= 2;
+    int l = 0;
+    for (int t = lmax / 2; t >= 1; t /= 2)
+      if (delta(keys, N, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = delta(keys, N, i, j);
+    int s = 0;
+    for (int div = 2;; div *= 2) {
+      const int t = (l + div - 1) / div;
+      if (delta(keys, N, i, i + (s + t) * d) > dnode) s += t;
+      if (t <= 1) break;
+    }
+    const int gamma = i + s * d + min(d, 0);
+    const int lo = min(i, j), hi = max(i, j);
+    uint32_t left, right;
+    if (lo == gamma) {
+      left = leaf_link[gamma];
+      leaf_parent[gamma] = (uint32_t)i;
+    } else {
+      left = (uint32_t)gamma;
+      nodes[gamma].link.z = (uint32_t)i;
+    }
+    if (hi == gamma + 1) {
+      right = leaf_link[gamma + 1];
+      leaf_parent[gamma + 1] = (uint32_t)i;
+    } else {
+      right = (uint32_t)(gamma + 1);
+      nodes[gamma + 1].link.z = (uint32_t)i;
+    }
+    nodes[i].link.x = left;
+    nodes[i].link.y = right;
+    nodes[i].link.w = 0u;
+  }
+}
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Each leaf walks up; at each node the first arriving child stops, the second merges both child
+// boxes (read back through agent-scope loads) and continues.  Also records the leaf depth.
+__global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const float4* bhi, const uint32_t* leaf_link,
+                        const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* max_depth) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    const uint32_t prim = vals[i];
+    const float4 a = blo[prim], b = bhi[prim];
+    float lo[3] = {a.x, a.y, a.z}, hi[3] = {b.x, b.y, b.z};
+    uint32_t child = leaf_link[i];
+    uint32_t par = leaf_parent[i];
+    // depth of this leaf (walk the parent chain)
+    {
+      uint32_t dep = 1, q = par;
+      while (q != 0u) {
+        q = nodes[q].link.z;
+        ++dep;
+      }
+      atomicMax(max_depth, dep);
+    }
+    for (;;) {
+      BvhNode* nd = nodes + par;
+      const bool left = (nd->link.x == child);
+      float* f = reinterpret_cast<float*>(nd);
+      // lxy = f[0..3], rxy = f[4..7], z = f[8..11]
+      if (left) {
+        st_agent(f + 0, lo[0]); st_agent(f + 1, hi[0]); st_agent(f + 2, lo[1]); st_agent(f + 3, hi[1]);
+        st_agent(f + 8, lo[2]); st_agent(f + 9, hi[2]);
+      } else {
+        st_agent(f + 4, lo[0]); st_agent(f + 5, hi[0]); st_agent(f + 6, lo[1]); st_agent(f + 7, hi[1]);
+        st_agent(f + 10, lo[2]); st_agent(f + 11, hi[2]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t old = __hip_atomic_fetch_add(flags + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == 0u) break;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const float l0 = ld_agent(f + 0), l1 = ld_agent(f + 1), l2 = ld_agent(f + 2), l3 = ld_agent(f + 3);
+      const float r0 = ld_agent(f + 4), r1 = ld_agent(f + 5), r2 = ld_agent(f + 6), r3 = ld_agent(f + 7);
+      const float z0 = ld_agent(f + 8), z1 = ld_agent(f + 9), z2 = ld_agent(f + 10), z3 = ld_agent(f + 11);
+      lo[0] = fminf(l0, r0); hi[0] = fmaxf(l1, r1);
+      lo[1] = fminf(l2, r2); hi[1] = fmaxf(l3, r3);
+      lo[2] = fminf(z0, z2); hi[2] = fmaxf(z1, z3);
+      if (par == 0u) break;
+      child = par;
+      par = nd->link.z;
+    }
+  }
+}
+
+struct Tmp {
+  std::vector<void*> ptrs;
+  ~Tmp() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <class T>
+  hipError_t alloc(T** p, size_t n) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, n ? n * sizeof(T) : 16);
+    if (e == hipSuccess) ptrs.push_back(q);
+    *p = static_cast<T*>(q);
+    return e;
+  }
+};
+
+hipError_t realloc_buf(DevBuf& b, size_t bytes) {
+  if (b.p && b.bytes >= bytes) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  hipError_t e = hipMalloc(&b.p, bytes ? bytes : 16);
+  if (e == hipSuccess) b.bytes = bytes ? bytes : 16;
+  return e;
+}
+
+unsigned blocks_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* h_idx, uint32_t ntris,
+               const float* h_sph, uint32_t nsph, const uint32_t* h_tri_geom, uint32_t sph_geom_base) {
+  const auto t0 = std::chrono::steady_clock::now();
+  hipStream_t s = c.stream;
+  const uint32_t N = ntris + nsph;
+  c.num_tris = ntris;
+  c.num_sph = nsph;
+  c.num_nodes = N > 1 ? N - 1 : 0;
+  c.bvh_depth = 0;
+  LB_CHECK(realloc_buf(c.tris, (size_t)ntris * 48));
+  LB_CHECK(realloc_buf(c.tri_geom, (size_t)ntris * 4));
+  LB_CHECK(realloc_buf(c.tri_orig, (size_t)ntris * 4));
+  LB_CHECK(realloc_buf(c.sph, (size_t)nsph * 16));
+  LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
+  LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
+  LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));
+  if (N == 0) {
+    c.root = kNoHit;
+    return SPTR_OK;
+  }
+  Tmp tmp;
+  float* d_pos = nullptr;
+  uint32_t *d_idx = nullptr, *d_tg = nullptr;
+  float4* d_sph = nullptr;
+  LB_CHECK(tmp.alloc(&d_pos, (size_t)nverts * 3));
+  LB_CHECK(tmp.alloc(&d_idx, (size_t)ntris * 3));
+  LB_CHECK(tmp.alloc(&d_tg, (size_t)ntris));
+  LB_CHECK(tmp.alloc(&d_sph, (size_t)nsph));
+  if (nverts) LB_CHECK(hipMemcpyAsync(d_pos, h_pos, (size_t)nverts * 12, hipMemcpyHostToDevice, s));
+  if (ntris) {
+    LB_CHECK(hipMemcpyAsync(d_idx, h_idx, (size_t)ntris * 12, hipMemcpyHostToDevice, s));
+    LB_CHECK(hipMemcpyAsync(d_tg, h_tri_geom, (size_t)ntris * 4, hipMemcpyHostToDevice, s));
+  }
+  if (nsph) LB_CHECK(hipMemcpyAsync(d_sph, h_sph, (size_t)nsph * 16, hipMemcpyHostToDevice, s));
+  BuildIn in{d_pos, d_idx, d_sph, d_tg, ntris, nsph, sph_geom_base};
+
+  float4 *blo = nullptr, *bhi = nullptr;
+  uint32_t* cb = nullptr;
+  uint64_t *keys = nullptr, *keys_s = nullptr;
+  uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_link = nullptr,
+           *leaf_parent = nullptr, *rflags = nullptr, *dmax = nullptr;
+  LB_CHECK(tmp.alloc(&blo, N));
+  LB_CHECK(tmp.alloc(&bhi, N));
+  LB_CHECK(tmp.alloc(&cb, 8));
+  LB_CHECK(tmp.alloc(&keys, N));
+  LB_CHECK(tmp.alloc(&keys_s, N));
+  LB_CHECK(tmp.alloc(&vals, N));
+  LB_CHECK(tmp.alloc(&vals_s, N));
+  LB_CHECK(tmp.alloc(&flag, N));
+  LB_CHECK(tmp.alloc(&slot, N));
+  LB_CHECK(tmp.alloc(&leaf_link, N));
+  LB_CHECK(tmp.alloc(&leaf_parent, N));
+  LB_CHECK(tmp.alloc(&rflags, N));
+  LB_CHECK(tmp.alloc(&dmax, 1));
+  const uint32_t cb_init[8] = {~0u, ~0u, ~0u, 0u, 0u, 0u, 0u, 0u};
+  LB_CHECK(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
+  LB_CHECK(hipMemsetAsync(dmax, 0, 4, s));
+  hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(N)), dim3(256), 0, s, in, blo, bhi, cb);
+  hipLaunchKernelGGL(k_morton, dim3(blocks_for(N)), dim3(256), 0, s, N, blo, bhi, cb, keys, vals);
+  LB_CHECK(hipGetLastError());
+  size_t tbytes = 0;
+  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, N, 0, 63, s));
+  void* tstore = nullptr;
+  LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
+  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, N, 0, 63, s));
+  hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(N)), dim3(256), 0, s, N, ntris, vals_s, flag);
+  size_t sbytes = 0;
+  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, N, rocprim::plus<uint32_t>(), s));
+  void* sstore = nullptr;
+  LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&sstore), sbytes));
+  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, N, rocprim::plus<uint32_t>(), s));
+  hipLaunchKernelGGL(k_leaves, dim3(blocks_for(N)), dim3(256), 0, s, in, vals_s, slot,
+                     static_cast<float4*>(c.tris.p), static_cast<uint32_t*>(c.tri_geom.p),
+                     static_cast<uint32_t*>(c.tri_orig.p), static_cast<float4*>(c.sph.p),
+                     static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p), leaf_link);
+  LB_CHECK(hipGetLastError());
+  if (N == 1) {
+    uint32_t link = 0;
+    LB_CHECK(hipMemcpyAsync(&link, leaf_link, 4, hipMemcpyDeviceToHost, s));
+    LB_CHECK(hipStreamSynchronize(s));
+    c.root = link;
+    c.bvh_depth = 0;
+  } else {
+    BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
+    LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
+    LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
+    hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_link, nodes, leaf_parent);
+    hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, leaf_link,
+                       leaf_parent, nodes, rflags, dmax);
+    LB_CHECK(hipGetLastError());
+    uint32_t dep = 0;
+    LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
+    LB_CHECK(hipStreamSynchronize(s));
+    c.root = 0;
+    c.bvh_depth = dep;
+    if (dep >= (uint32_t)kStack) {
+      c.err = "lbvh: tree depth " + std::to_string(dep) + " exceeds the traversal stack";
+      return SPTR_ERR_INVALID;
+    }
+  }
+  LB_CHECK(hipStreamSynchronize(s));
+  c.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SPTR_OK;
+}
+
+}  // namespace sptr

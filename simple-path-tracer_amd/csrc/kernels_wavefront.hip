@@ -1,0 +1,810 @@
+// kernels_wavefront.hip — the wavefront stages of the MI355X (gfx950) path tracer.
+//
+//   k_raygen  : path init for every (sample slot, tile-packed pixel) of a wave; wave64 ballot append
+//               into the depth-0 queue.                  (GLRenderer.cpp:384-408, Camera.cpp:95-106)
+//   k_trace   : closest-hit BVH2 traversal + Embree-style Moeller-Trumbore triangles + the
+//               reference's quadratic spheres, one thread per queued path.   (wf_pt_cpu.cpp:28-56)
+//   k_shade   : miss/env, emission, direct-light shadow tasks, metal/glass/diffuse continuation with
+//               ballot-compacted next queue and shadow queue.           (wf_pt_cpu.cpp:94-248)
+//   k_shadow  : any-hit traversal of the shadow tasks, adds unoccluded light. (Light.cpp:16-40)
+//   k_accum   : per-pixel sum of the wave's samples in accumulation order.  (GLRenderer.cpp:411-413)
+//   k_resolve : mean -> ACES -> gamma 1/2.2 -> clamp -> 8-bit truncation.   (GLRenderer.cpp:416-431)
+//
+// Kernels run a fixed grid (<= 8 blocks per CU) and grid-stride over a device-side queue count, so a
+// wave needs no host round trip between stages.  Arithmetic order follows the CPU reference line
+// for line (see sptr_math.h); the file is compiled with -ffp-contract=off.  Box tests are the one
+// place that uses fma: they only prune traversal and are padded to stay conservative.
+#include <hip/hip_runtime.h>
+
+#include "sptr_internal.h"
+
+namespace sptr {
+
+// --------------------------------------------------------------------------------- small helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-aggregated queue append: one atomic per wave; lanes keep their relative order.
+// Must be reached by all active lanes of the wave together.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0ull) return 0u;
+  const uint32_t lane = lane_id();
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0u;
+  if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ vec3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
+__device__ __forceinline__ float4 f4(vec3 a, float w) { return make_float4(a.x, a.y, a.z, w); }
+__device__ __forceinline__ float clamp_std(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+
+__device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim.x; }
+
+// tile-packed local pixel -> image coordinates (interleaved 32x32 tile sharding)
+__device__ __forceinline__ bool local_pixel(const FrameView& f, uint32_t l, int& x, int& y) {
+  const uint32_t lt = l >> 10, w = l & 1023u;
+  const uint32_t t = lt * (uint32_t)f.G + (uint32_t)f.R;
+  const int tx = (int)(t % (uint32_t)f.ntx), ty = (int)(t / (uint32_t)f.ntx);
+  x = tx * kTile + (int)(w & 31u);
+  y = ty * kTile + (int)(w >> 5);
+  return x < f.W && y < f.H;
+}
+
+// Camera::getRayDirection
+__device__ __forceinline__ vec3 camera_dir(const FrameView& f, float u, float v) {
+  const float nx = (u - 0.5f) * 2.0f;
+  const float ny = -(v - 0.5f) * 2.0f;
+  const vec3 d = f.cam_f + nx * f.half_w * f.cam_r + ny * f.half_h * f.cam_u;
+  return normalize(d);
+}
+
+// --------------------------------------------------------------------------------- intersection
+struct Ray {
+  vec3 o, d, inv, oinv;
+};
+__device__ __forceinline__ Ray make_ray(vec3 o, vec3 d) {
+  Ray r;
+  r.o = o;
+  r.d = d;
+  const float eps = 1e-20f;
+  const float ix = 1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x));
+  const float iy = 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y));
+  const float iz = 1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z));
+  r.inv = v3(ix, iy, iz);
+  r.oinv = v3(o.x * ix, o.y * iy, o.z * iz);
+  return r;
+}
+
+// Slab test of one child box; conservative by a few ulps (only prunes, never decides a hit).
+__device__ __forceinline__ bool slab(float xlo, float xhi, float ylo, float yhi, float zlo, float zhi, const Ray& r,
+                                     float tnear, float tfar, float& tent) {
+  const float tx0 = __builtin_fmaf(xlo, r.inv.x, -r.oinv.x), tx1 = __builtin_fmaf(xhi, r.inv.x, -r.oinv.x);
+  const float ty0 = __builtin_fmaf(ylo, r.inv.y, -r.oinv.y), ty1 = __builtin_fmaf(yhi, r.inv.y, -r.oinv.y);
+  const float tz0 = __builtin_fmaf(zlo, r.inv.z, -r.oinv.z), tz1 = __builtin_fmaf(zhi, r.inv.z, -r.oinv.z);
+  const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tnear));
+  const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tfar));
+  tent = tmin;
+  return tmin <= tmax * 1.0000003f;
+}
+
+__device__ __forceinline__ float e_dot(vec3 a, vec3 b) {
+  return __builtin_fmaf(a.x, b.x, __builtin_fmaf(a.y, b.y, a.z * b.z));
+}
+__device__ __forceinline__ vec3 e_cross(vec3 a, vec3 b) {
+  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+}
+__device__ __forceinline__ float xorsign(float x, float s) {
+  return __uint_as_float(__float_as_uint(x) ^ (__float_as_uint(s) & 0x80000000u));
+}
+
+// Embree default Moeller-Trumbore (restated; see oracle/wf_oracle.cpp tri_hit): accepts
+// tnear*|den| < T <= tfar*|den|.  Triangle record: v0, e1 = v0-v1, e2 = v2-v0, Ng = cross(e2,e1).
+__device__ __forceinline__ bool tri_hit(const float4* tris, uint32_t i, const Ray& r, float tnear, float tfar, float& t) {
+  const float4 a = tris[3 * i + 0], b = tris[3 * i + 1], c = tris[3 * i + 2];
+  const vec3 v0 = v3(a.x, a.y, a.z), e1 = v3(a.w, b.x, b.y), e2 = v3(b.z, b.w, c.x), ng = v3(c.y, c.z, c.w);
+  const vec3 C = v0 - r.o;
+  const vec3 R = e_cross(C, r.d);
+  const float den = e_dot(ng, r.d);
+  const float aden = fabsf(den);
+  const float U = xorsign(e_dot(R, e2), den);
+  const float V = xorsign(e_dot(R, e1), den);
+  if (!(den != 0.0f && U >= 0.0f && V >= 0.0f && U + V <= aden)) return false;
+  const float T = xorsign(e_dot(ng, C), den);
+  if (!(aden * tnear < T && T <= aden * tfar)) return false;
+  t = T / aden;
+  return true;
+}
+
+// EmbreeBackend.cpp:223-314 sphere callbacks, same evaluation order.
+__device__ __forceinline__ bool sphere_roots(float4 s, const Ray& r, float& t1, float& t2) {
+  const vec3 D = r.d;
+  const float ox = r.o.x - s.x, oy = r.o.y - s.y, oz = r.o.z - s.z;
+  const float a = D.x * D.x + D.y * D.y + D.z * D.z;
+  const float b = 2.0f * (ox * D.x + oy * D.y + oz * D.z);
+  const float c = ox * ox + oy * oy + oz * oz - s.w * s.w;
+  const float disc = b * b - 4.0f * a * c;
+  if (!(disc >= 0.0f)) return false;
+  const float sq = sqrtf(disc);
+  t1 = (-b - sq) / (2.0f * a);
+  t2 = (-b + sq) / (2.0f * a);
+  return true;
+}
+__device__ __forceinline__ bool sphere_hit(float4 s, const Ray& r, float tnear, float tfar, float& t) {
+  float t1, t2;
+  if (!sphere_roots(s, r, t1, t2)) return false;
+  float tt = -1.0f;
+  if (t1 > tnear && t1 < tfar) tt = t1;
+  else if (t2 > tnear && t2 < tfar) tt = t2;
+  if (!(tt > 0.0f && tt < tfar)) return false;
+  t = tt;
+  return true;
+}
+__device__ __forceinline__ bool sphere_occ(float4 s, const Ray& r, float tnear, float tfar) {
+  float t1, t2;
+  if (!sphere_roots(s, r, t1, t2)) return false;
+  return (t1 > tnear && t1 < tfar) || (t2 > tnear && t2 < tfar);
+}
+
+struct Visits {
+  uint32_t nodes = 0, tris = 0, sph = 0;
+};
+
+// Leaf primitive test.  Closest: updates tfar/ref, returns hit.  Any-hit: returns occlusion.
+template <bool kAny, bool kCount>
+__device__ __forceinline__ bool leaf_test(uint32_t link, const float4* tris, const float4* sph, const Ray& r,
+                                          float tnear, float& tfar, uint32_t& ref, Visits& vc) {
+  const uint32_t idx = link & kIndexMask;
+  float t;
+  if (link & kSphereBit) {
+    if (kCount) ++vc.sph;
+    const float4 s = sph[idx];
+    if (kAny) return sphere_occ(s, r, tnear, tfar);
+    if (sphere_hit(s, r, tnear, tfar, t)) {
+      tfar = t;
+      ref = link & ~kLeafBit;
+      return true;
+    }
+    return false;
+  }
+  if (kCount) ++vc.tris;
+  if (tri_hit(tris, idx, r, tnear, tfar, t)) {
+    if (kAny) return true;
+    tfar = t;
+    ref = link & ~kLeafBit;
+    return true;
+  }
+  return false;
+}
+
+// BVH2 stack traversal: nearest child first; leaf children are tested as soon as their box is hit.
+template <bool kAny, bool kCount>
+__device__ __forceinline__ bool traverse(const BvhNode* nodes, const float4* tris, const float4* sph, uint32_t root,
+                                         const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc) {
+  if (root == kNoHit) return false;
+  if (root & kLeafBit) {
+    const bool h = leaf_test<kAny, kCount>(root, tris, sph, r, tnear, tfar, ref, vc);
+    return h;
+  }
+  uint32_t stack[kStack];
+  int sp = 0;
+  uint32_t cur = root;
+  bool hit = false;
+  for (;;) {
+    const BvhNode* nd = nodes + cur;
+    const float4 lxy = nd->lxy, rxy = nd->rxy, z = nd->z;
+    const uint4 ln = nd->link;
+    if (kCount) ++vc.nodes;
+    float tl, tr;
+    bool hl = slab(lxy.x, lxy.y, lxy.z, lxy.w, z.x, z.y, r, tnear, tfar, tl);
+    bool hr = slab(rxy.x, rxy.y, rxy.z, rxy.w, z.z, z.w, r, tnear, tfar, tr);
+    uint32_t L = ln.x, R = ln.y;
+    if (hl && (L & kLeafBit)) {
+      if (leaf_test<kAny, kCount>(L, tris, sph, r, tnear, tfar, ref, vc)) {
+        hit = true;
+        if (kAny) return true;
+      }
+      hl = false;
+    }
+    if (hr && (R & kLeafBit)) {
+      if (leaf_test<kAny, kCount>(R, tris, sph, r, tnear, tfar, ref, vc)) {
+        hit = true;
+        if (kAny) return true;
+      }
+      hr = false;
+    }
+    if (hl && hr) {
+      if (tr < tl) {
+        const uint32_t s = L;
+        L = R;
+        R = s;
+      }
+      if (sp < kStack) stack[sp++] = R;
+      cur = L;
+    } else if (hl) {
+      cur = L;
+    } else if (hr) {
+      cur = R;
+    } else {
+      if (sp == 0) break;
+      cur = stack[--sp];
+    }
+  }
+  return hit;
+}
+
+// Stage the whole scene (nodes, triangles, spheres) into LDS when it fits (SceneView::lds_bytes).
+struct Staged {
+  const BvhNode* nodes;
+  const float4* tris;
+  const float4* sph;
+};
+template <bool kLds>
+__device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) {
+  Staged s{sv.nodes, sv.tris, sv.sph};
+  if (kLds) {
+    const uint32_t nn = sv.num_nodes * 4u, nt = sv.num_tris * 3u, ns = sv.num_sph;
+    const float4* gn = reinterpret_cast<const float4*>(sv.nodes);
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = gn[i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = sv.tris[i];
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + i] = sv.sph[i];
+    __syncthreads();
+    s.nodes = reinterpret_cast<const BvhNode*>(lds);
+    s.tris = lds + nn;
+    s.sph = lds + nn + nt;
+  }
+  return s;
+}
+
+__device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long long* tot, int base) {
+  unsigned long long a = vc.nodes, b = vc.tris, c = vc.sph;
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+    c += __shfl_xor(c, off);
+  }
+  if (lane_id() == 0) {
+    atomicAdd(&tot[base + 0], a);
+    atomicAdd(&tot[base + 1], b);
+    if (base == kTotNodes) atomicAdd(&tot[base + 2], c);
+  }
+}
+
+// --------------------------------------------------------------------------------- k_raygen
+__global__ void __launch_bounds__(kBlock) k_raygen(FrameView f, WaveView w) {
+  const uint32_t C = f.P * f.k;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < C; base += grid_threads()) {
+    const uint32_t p = base + threadIdx.x;
+    bool live = false;
+    if (p < C) {
+      const uint32_t s = p / f.P, l = p - s * f.P;
+      int x, y;
+      live = local_pixel(f, l, x, y);
+      w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (live) {
+        const uint32_t acc = f.acc0 + s;
+        const uint32_t ps = (uint32_t)(y * f.W + x);
+        uint32_t r = wang_hash(ps ^ acc * 9781u);
+        const float jx = rand01(r);
+        const float jy = rand01(r);
+        const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
+        const vec3 d = safe_normalize(dir);
+        const uint32_t rng = wang_hash((ps ^ acc) ^ 1u);
+        w.o[p] = f4(f.cam_pos, __uint_as_float(rng));
+        w.d[p] = f4(d, 0.0f);
+        w.thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      }
+    }
+    const uint32_t slot = wave_append(&w.cnt[kCntLive], live);
+    if (live) w.q[0][slot] = p;
+  }
+}
+
+// --------------------------------------------------------------------------------- k_trace
+template <bool kLds, bool kCount>
+__global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, WaveView w, int depth) {
+  extern __shared__ float4 lds[];
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  const uint32_t n = w.cnt[kCntLive + depth];
+  const uint32_t* q = w.q[depth & 1];
+  Visits vc;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
+    const uint32_t p = q[i];
+    const float4 o4 = w.o[p], d4 = w.d[p];
+    const Ray r = make_ray(xyz(o4), xyz(d4));
+    float tfar = __builtin_huge_valf();
+    uint32_t ref = kNoHit;
+    traverse<false, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
+    w.hit[p] = make_uint2(__float_as_uint(tfar), ref);
+  }
+  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+}
+
+// --------------------------------------------------------------------------------- shading math
+// EnvironmentManager::getSkyColor
+__device__ __forceinline__ vec3 sky_color(vec3 d) {
+  float t = 0.5f * (d.y + 1.0f);
+  {
+    const float u = clamp_g((t - 0.0f) / (1.0f - 0.0f), 0.0f, 1.0f);
+    t = u * u * (3.0f - 2.0f * u);
+  }
+  vec3 c = mix(v3(0.7f, 0.8f, 0.9f), v3(0.2f, 0.4f, 0.8f), t);
+  const vec3 sd = normalize(v3(0.3f, 0.6f, -0.8f));
+  const float sdot = fmax_g(dot(d, sd), 0.0f);
+  const float si = powf(sdot, 64.0f);
+  const float sg = powf(sdot, 8.0f) * 0.3f;
+  c = c + v3(1.0f, 0.9f, 0.7f) * (si + sg);
+  return c * 0.8f;
+}
+
+// Cubemap::sample + EnvironmentManager::getCubemapColor
+__device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, int x, int y) {
+  const float4 t = env[((size_t)face * S + y) * S + x];
+  return v3(t.x, t.y, t.z);
+}
+__device__ vec3 env_color(const ShadeView& sh, vec3 dir) {
+  if (!sh.env) return sky_color(dir);
+  const vec3 d = normalize(dir);
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  float ma, uc, vc;
+  int face;
+  if (ax >= ay && ax >= az) {
+    ma = ax;
+    if (d.x > 0) { face = 0; uc = -d.z; vc = -d.y; }
+    else         { face = 1; uc = d.z;  vc = -d.y; }
+  } else if (ay >= ax && ay >= az) {
+    ma = ay;
+    if (d.y > 0) { face = 2; uc = d.x; vc = d.z; }
+    else         { face = 3; uc = d.x; vc = -d.z; }
+  } else {
+    ma = az;
+    if (d.z > 0) { face = 4; uc = d.x;  vc = -d.y; }
+    else         { face = 5; uc = -d.x; vc = -d.y; }
+  }
+  const float u = clamp_g((uc / ma + 1.0f) * 0.5f, 0.0f, 1.0f);
+  const float v = clamp_g((vc / ma + 1.0f) * 0.5f, 0.0f, 1.0f);
+  const int S = sh.env_size;
+  const float fx_ = u * float(S - 1), fy_ = v * float(S - 1);
+  const int x0 = (int)floorf(fx_), y0 = (int)floorf(fy_);
+  const int x1 = min(x0 + 1, S - 1), y1 = min(y0 + 1, S - 1);
+  const float fx = fx_ - float(x0), fy = fy_ - float(y0);
+  const vec3 c0 = mix(cube_texel(sh.env, S, face, x0, y0), cube_texel(sh.env, S, face, x1, y0), fx);
+  const vec3 c1 = mix(cube_texel(sh.env, S, face, x0, y1), cube_texel(sh.env, S, face, x1, y1), fx);
+  vec3 c = mix(c0, c1, fy);
+  c = v3(fmin_g(c.x, sh.env_clamp), fmin_g(c.y, sh.env_clamp), fmin_g(c.z, sh.env_clamp));
+  return c * sh.env_intensity;
+}
+
+// Material::evaluateBRDF (Material.cpp:84-117).  The GGX denominator is double as in the reference
+// (M_PI is a double literal there).
+__device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, vec3 L) {
+  const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  const vec3 H = normalize(V + L);
+  const float NdotV = fmax_g(dot(N, V), 0.0f);
+  const float NdotL = fmax_g(dot(N, L), 0.0f);
+  const float HdotV = fmax_g(dot(H, V), 0.0f);
+  const float r = clamp_g(m.roughness, 0.02f, 1.0f);
+  const float alpha = r * r;
+  const float a2 = alpha * alpha;
+  const float NdotH = fmax_g(dot(N, H), 0.0f);
+  const float NdotH2 = NdotH * NdotH;
+  float dden = (NdotH2 * (a2 - 1.0f) + 1.0f);
+  dden = (float)(3.14159265358979323846 * (double)dden * (double)dden);
+  const float D = a2 / dden;
+  const float rr = clamp_g(sqrtf(fmax_g(alpha, 0.0f)), 0.02f, 1.0f);
+  const float kq = (rr + 1.0f);
+  const float k = (kq * kq) / 8.0f;
+  const float g_v = NdotV / (NdotV * (1.0f - k) + k);
+  const float g_l = NdotL / (NdotL * (1.0f - k) + k);
+  const float G = g_l * g_v;
+  float f0d = (m.ior - 1.0f) / (m.ior + 1.0f);
+  f0d *= f0d;
+  const vec3 F0 = mix(v3(f0d, f0d, f0d), albedo, m.metallic);
+  const float pw = powf(clamp_g(1.0f - HdotV, 0.0f, 1.0f), 5.0f);
+  const vec3 F = F0 + (1.0f - F0) * pw;
+  const vec3 numer = (D * G) * F;
+  const float denom = 4.0f * NdotV * NdotL + 0.0001f;
+  const vec3 spec = numer / denom;
+  const vec3 kD = 1.0f - F;
+  const vec3 diffuse = (albedo * (1.0f - m.metallic)) / float(3.14159265358979323846);
+  return (kD * diffuse + spec) * NdotL;
+}
+
+// --------------------------------------------------------------------------------- k_shade
+__global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
+  __shared__ DevMaterial smat[64];
+  const uint32_t nm = sh.num_mats < 64u ? sh.num_mats : 64u;
+  for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
+    reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
+  __syncthreads();
+
+  const uint32_t n = w.cnt[kCntLive + depth];
+  const uint32_t* q = w.q[depth & 1];
+  uint32_t* qn = w.q[(depth + 1) & 1];
+  const bool last = (uint32_t)(depth + 1) >= f.max_depth;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += grid_threads()) {
+    const uint32_t i = base + threadIdx.x;
+    bool cont = false, shadow = false;
+    uint32_t p = 0;
+    if (i < n) {
+      p = q[i];
+      const uint2 h = w.hit[p];
+      const float4 o4 = w.o[p], d4 = w.d[p], t4 = w.thr[p];
+      const vec3 ro = xyz(o4), rd = xyz(d4);
+      vec3 thr = xyz(t4);
+      uint32_t rng = __float_as_uint(o4.w);
+      if (h.y == kNoHit) {  // miss -> environment, path ends
+        if (sh.debug_mode == 1) {
+          w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+          const vec3 e = env_color(sh, safe_normalize(rd));
+          const vec3 rv = xyz(w.rad[p]) + thr * e;
+          w.rad[p] = f4(rv, 0.0f);
+        }
+      } else if (sh.debug_mode == 1) {
+        w.rad[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      } else {
+        const float t = __uint_as_float(h.x);
+        const vec3 P = ro + t * rd;
+        const uint32_t idx = h.y & kIndexMask;
+        vec3 ng;
+        uint32_t mid;
+        if (h.y & kSphereBit) {
+          const float4 s = sv.sph[idx];
+          ng = v3((P.x - s.x) / s.w, (P.y - s.y) / s.w, (P.z - s.z) / s.w);
+          mid = sh.geom_mat[sv.sph_geom[idx]];
+        } else {
+          const float4 c = sv.tris[3 * idx + 2];
+          ng = v3(c.y, c.z, c.w);
+          mid = sh.geom_mat[sv.tri_geom[idx]];
+        }
+        vec3 nrm = safe_normalize(ng);
+        if (dot(nrm, rd) > 0.0f) nrm = -nrm;
+        const DevMaterial m = (mid < nm) ? smat[mid] : sh.mats[mid];
+        const vec3 emission = v3(m.emission[0], m.emission[1], m.emission[2]);
+        if (dot(emission, emission) > 0.0f) {
+          const vec3 rv = xyz(w.rad[p]) + thr * emission;
+          w.rad[p] = f4(rv, 0.0f);
+        }
+        // direct light: build shadow tasks (contribution precomputed; added if unoccluded)
+        {
+          const vec3 view = -rd;
+          for (uint32_t li = 0; li < sh.num_lights; ++li) {
+            const DevLight& L = sh.lights[li];
+            vec3 ldir, Li;
+            float ldist;
+            if (L.type == 0) {
+              ldir = v3(L.v[0], L.v[1], L.v[2]);
+              ldist = __builtin_huge_valf();
+              Li = v3(L.radiance[0], L.radiance[1], L.radiance[2]);
+            } else {
+              const vec3 lv = v3(L.v[0], L.v[1], L.v[2]) - P;
+              ldist = sqrtf(dot(lv, lv));
+              ldir = lv / ldist;
+              const float att = 1.0f + 0.09f * ldist + 0.032f * ldist * ldist;
+              Li = v3(L.radiance[0], L.radiance[1], L.radiance[2]) / att;
+            }
+            const float cs = fmax_g(dot(nrm, ldir), 0.0f);
+            float4* task = w.stask + ((size_t)p * w.L + li) * 3;
+            if (cs <= 0.0f) {
+              task[2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              continue;
+            }
+            const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
+            const vec3 so = P + nrm * eps;
+            const vec3 fr = eval_brdf(m, nrm, view, ldir);
+            const vec3 contrib = thr * (fr * Li * cs);
+            task[0] = f4(so, ldist - 1e-4f);
+            task[1] = f4(ldir, 0.0f);
+            task[2] = f4(contrib, 1.0f);
+            shadow = true;
+          }
+        }
+        // continuation
+        vec3 no, nd;
+        const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+        if (m.metallic > 0.5f) {
+          no = P + nrm * 1e-4f;
+          nd = safe_normalize(reflect(rd, nrm));
+          thr = thr * (albedo * m.metallic);
+          cont = true;
+        } else if (m.metallic < 0.1f && m.ior > 1.3f) {
+          const float ior = m.ior;
+          const float cosine = -dot(rd, nrm);
+          const float eta = (cosine >= 0.0f) ? (1.0f / ior) : ior;
+          const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
+          float r0 = (1.0f - ior) / (1.0f + ior);
+          r0 = r0 * r0;
+          const float xc = 1.0f - clamp_std(fabsf(cosine), 0.0f, 1.0f);
+          const float F = r0 + (1.0f - r0) * xc * xc * xc * xc * xc;
+          const float xi = rand01(rng);
+          if (xi < F) {
+            no = P + nrm * 1e-4f;
+            nd = safe_normalize(reflect(rd, nrm));
+            thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
+          } else {
+            const float ci = -dot(nrm, rd);
+            const float kk = 1.0f - eta * eta * (1.0f - ci * ci);
+            vec3 refr = v3(0.0f, 0.0f, 0.0f);
+            if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
+            if (dot(refr, refr) > 0.0f) {
+              no = P - nrm * 1e-4f;
+              nd = safe_normalize(refr);
+              thr = thr * v3(tr, tr, tr);
+            } else {
+              no = P + nrm * 1e-4f;
+              nd = safe_normalize(reflect(rd, nrm));
+            }
+          }
+          cont = true;
+        } else {
+          const float r1 = rand01(rng);
+          const float r2 = rand01(rng);
+          const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
+          const float rr = sqrtf(r2);
+          const float lx = rr * cosf(phi), ly = rr * sinf(phi);
+          const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
+          const vec3 nn = safe_normalize(nrm);
+          const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
+                                                 : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
+          const vec3 bt = cross(tg, nn);
+          const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
+          no = P + nrm * 1e-4f;
+          const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
+          const float xi = rand01(rng);
+          cont = true;
+          if ((uint32_t)depth > 2u) {
+            if (xi >= surv) cont = false;
+            else thr = thr * (albedo / fmax_g(surv, 1e-6f));
+          } else {
+            thr = thr * albedo;
+          }
+          nd = safe_normalize(sdir);
+        }
+        cont = cont && !last;
+        if (cont) {
+          w.o[p] = f4(no, __uint_as_float(rng));
+          w.d[p] = f4(nd, 0.0f);
+          w.thr[p] = f4(thr, 0.0f);
+        }
+      }
+    }
+    const uint32_t slot = wave_append(&w.cnt[kCntLive + depth + 1], cont);
+    if (cont) qn[slot] = p;
+    const uint32_t sslot = wave_append(&w.cnt[kCntShadow + depth], shadow);
+    if (shadow) w.sq[sslot] = p;
+  }
+}
+
+// --------------------------------------------------------------------------------- k_shadow
+template <bool kLds, bool kCount>
+__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, WaveView w, int depth) {
+  extern __shared__ float4 lds[];
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  const uint32_t n = w.cnt[kCntShadow + depth];
+  Visits vc;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
+    const uint32_t p = w.sq[i];
+    vec3 add = v3(0.0f, 0.0f, 0.0f);
+    bool any = false;
+    vec3 rv = v3(0.0f, 0.0f, 0.0f);
+    for (uint32_t li = 0; li < w.L; ++li) {
+      const float4* task = w.stask + ((size_t)p * w.L + li) * 3;
+      const float4 c = task[2];
+      if (c.w == 0.0f) continue;
+      const float4 a = task[0], b = task[1];
+      const Ray r = make_ray(xyz(a), xyz(b));
+      float tfar = a.w;
+      uint32_t ref = kNoHit;
+      const bool occ = traverse<true, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
+      if (!occ) {
+        if (!any) rv = xyz(w.rad[p]);
+        any = true;
+        rv = rv + xyz(c);
+      }
+    }
+    (void)add;
+    if (any) w.rad[p] = f4(rv, 0.0f);
+  }
+  if (kCount) flush_visits(vc, w.tot, kTotShNodes);
+}
+
+// --------------------------------------------------------------------------------- k_accum / resolve
+__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset, int max_depth) {
+  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
+    vec3 a = reset ? v3(0.0f, 0.0f, 0.0f) : xyz(accum[l]);
+    for (uint32_t s = 0; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
+    accum[l] = f4(a, 0.0f);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned long long live = 0, sh = 0;
+    for (int d = 0; d < max_depth; ++d) {
+      live += w.cnt[kCntLive + d];
+      sh += w.cnt[kCntShadow + d];
+    }
+    w.tot[kTotClosest] += live;
+    w.tot[kTotShadow] += sh;
+  }
+}
+
+__device__ __forceinline__ uint32_t resolve_rgba(vec3 acc, uint32_t n) {
+  vec3 c = acc / float(n);
+  c = clamp_g((c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f), 0.0f, 1.0f);
+  const float g = 1.0f / 2.2f;
+  c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
+  c = clamp_g(c, 0.0f, 1.0f);
+  const uint32_t r = (uint32_t)(unsigned char)(c.x * 255.0f);
+  const uint32_t gg = (uint32_t)(unsigned char)(c.y * 255.0f);
+  const uint32_t b = (uint32_t)(unsigned char)(c.z * 255.0f);
+  return r | (gg << 8) | (b << 16) | 0xFF000000u;
+}
+
+__global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n, uint32_t* tiles,
+                                                    uint8_t* image) {
+  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
+    int x, y;
+    const bool valid = local_pixel(f, l, x, y);
+    const uint32_t px = valid ? resolve_rgba(xyz(accum[l]), n) : 0u;
+    tiles[l] = px;
+    if (valid && image) {
+      uint8_t* o = image + ((size_t)y * f.W + x) * 3;
+      o[0] = (uint8_t)(px & 0xFF);
+      o[1] = (uint8_t)((px >> 8) & 0xFF);
+      o[2] = (uint8_t)((px >> 16) & 0xFF);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_unpack(const uint32_t* g, int G, uint32_t tpr, int W, int H, int ntx,
+                                                   uint8_t* rgb) {
+  const uint32_t N = (uint32_t)W * (uint32_t)H;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += grid_threads()) {
+    const int x = (int)(i % (uint32_t)W), y = (int)(i / (uint32_t)W);
+    const uint32_t t = (uint32_t)(y / kTile) * (uint32_t)ntx + (uint32_t)(x / kTile);
+    const uint32_t r = t % (uint32_t)G, lt = t / (uint32_t)G;
+    const uint32_t px = g[((size_t)r * tpr + lt) * kTilePixels + (uint32_t)(y % kTile) * kTile + (uint32_t)(x % kTile)];
+    rgb[(size_t)i * 3 + 0] = (uint8_t)(px & 0xFF);
+    rgb[(size_t)i * 3 + 1] = (uint8_t)((px >> 8) & 0xFF);
+    rgb[(size_t)i * 3 + 2] = (uint8_t)((px >> 16) & 0xFF);
+  }
+}
+
+// --------------------------------------------------------------------------------- query kernels
+__global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* tri_orig, const uint32_t* sph_orig,
+                                                  const float* rays, uint32_t n, int anyhit, uint32_t* ref_out,
+                                                  float* t_out, float* ng_out, uint8_t* occ) {
+  Visits vc;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
+    const float* rr = rays + (size_t)i * 8;
+    const Ray r = make_ray(v3(rr[0], rr[1], rr[2]), v3(rr[3], rr[4], rr[5]));
+    float tfar = rr[7];
+    uint32_t ref = kNoHit;
+    if (anyhit) {
+      occ[i] = traverse<true, false>(sv.nodes, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc) ? 1 : 0;
+      continue;
+    }
+    const bool hit = traverse<false, false>(sv.nodes, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc);
+    // report (type bit | original primitive index) so the host can map to (geomID, primID)
+    ref_out[i] = hit ? ((ref & kSphereBit) | ((ref & kSphereBit) ? sph_orig[ref & kIndexMask] : tri_orig[ref & kIndexMask]))
+                     : kNoHit;
+    t_out[i] = hit ? tfar : __builtin_huge_valf();
+    vec3 ng = v3(0.0f, 0.0f, 0.0f);
+    if (hit) {
+      const uint32_t idx = ref & kIndexMask;
+      if (ref & kSphereBit) {
+        const float4 s = sv.sph[idx];
+        const vec3 P = r.o + tfar * r.d;
+        ng = v3((P.x - s.x) / s.w, (P.y - s.y) / s.w, (P.z - s.z) / s.w);
+      } else {
+        const float4 c = sv.tris[3 * idx + 2];
+        ng = v3(c.y, c.z, c.w);
+      }
+    }
+    ng_out[(size_t)i * 3 + 0] = ng.x;
+    ng_out[(size_t)i * 3 + 1] = ng.y;
+    ng_out[(size_t)i * 3 + 2] = ng.z;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, uint32_t* rng) {
+  const uint32_t N = (uint32_t)f.W * (uint32_t)f.H;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += grid_threads()) {
+    const int x = (int)(i % (uint32_t)f.W), y = (int)(i / (uint32_t)f.W);
+    const uint32_t acc = f.acc0;
+    const uint32_t ps = (uint32_t)(y * f.W + x);
+    uint32_t r = wang_hash(ps ^ acc * 9781u);
+    const float jx = rand01(r);
+    const float jy = rand01(r);
+    const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
+    const vec3 d = safe_normalize(dir);
+    dirs[(size_t)i * 3 + 0] = d.x;
+    dirs[(size_t)i * 3 + 1] = d.y;
+    dirs[(size_t)i * 3 + 2] = d.z;
+    rng[i] = wang_hash((ps ^ acc) ^ 1u);
+  }
+}
+
+// --------------------------------------------------------------------------------- launchers
+static inline unsigned grid_for(uint64_t work) {
+  const uint64_t blocks = (work + kBlock - 1) / kBlock;
+  const uint64_t cap = 256ull * 8ull;  // 256 CUs x 8 resident blocks
+  return (unsigned)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
+}
+
+SceneView scene_view(const Context& c) {
+  SceneView s;
+  s.nodes = static_cast<const BvhNode*>(c.nodes.p);
+  s.tris = static_cast<const float4*>(c.tris.p);
+  s.sph = static_cast<const float4*>(c.sph.p);
+  s.tri_geom = static_cast<const uint32_t*>(c.tri_geom.p);
+  s.sph_geom = static_cast<const uint32_t*>(c.sph_geom.p);
+  s.num_nodes = c.num_nodes;
+  s.num_tris = c.num_tris;
+  s.num_sph = c.num_sph;
+  s.root = c.root;
+  const uint64_t bytes = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16;
+  s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
+  return s;
+}
+
+void launch_raygen(const FrameView& f, const WaveView& w, hipStream_t s) {
+  hipLaunchKernelGGL(k_raygen, dim3(grid_for((uint64_t)f.P * f.k)), dim3(kBlock), 0, s, f, w);
+}
+
+void launch_trace(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s) {
+  const dim3 g(grid_for(1ull << 22)), b(kBlock);
+  if (sv.lds_bytes) {
+    if (count) hipLaunchKernelGGL((k_trace<true, true>), g, b, sv.lds_bytes, s, sv, w, depth);
+    else hipLaunchKernelGGL((k_trace<true, false>), g, b, sv.lds_bytes, s, sv, w, depth);
+  } else {
+    if (count) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, s, sv, w, depth);
+    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, s, sv, w, depth);
+  }
+}
+
+void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_shade, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+}
+
+void launch_shadow(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s) {
+  const dim3 g(grid_for(1ull << 22)), b(kBlock);
+  if (sv.lds_bytes) {
+    if (count) hipLaunchKernelGGL((k_shadow<true, true>), g, b, sv.lds_bytes, s, sv, w, depth);
+    else hipLaunchKernelGGL((k_shadow<true, false>), g, b, sv.lds_bytes, s, sv, w, depth);
+  } else {
+    if (count) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, s, sv, w, depth);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, s, sv, w, depth);
+  }
+}
+
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, reset ? 1 : 0, max_depth);
+}
+
+void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_resolve, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, accum, n, tiles, image);
+}
+
+void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
+                   hipStream_t s) {
+  const int ntx = (W + kTile - 1) / kTile;
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for((uint64_t)W * H)), dim3(kBlock), 0, s, gathered, G, tiles_per_rank, W,
+                     H, ntx, rgb);
+}
+
+void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
+                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, hipStream_t s) {
+  hipLaunchKernelGGL(k_query, dim3(grid_for(n)), dim3(kBlock), 0, s, sv, tri_orig, sph_orig, rays, n, anyhit ? 1 : 0,
+                     ref, t, ng, occ);
+}
+
+void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s) {
+  hipLaunchKernelGGL(k_primary, dim3(grid_for((uint64_t)f.W * f.H)), dim3(kBlock), 0, s, f, dirs, rng);
+}
+
+}  // namespace sptr

@@ -1,0 +1,621 @@
+// sptr_api.cpp — C ABI of libsptr_hip (include/sptr_hip.h): context, uploads, and the per-call
+// wavefront schedule.  This is the replacement for OptixBackend::render's orchestration
+// (src/backends/OptixBackend.cpp:1506-1850): where the reference does three blocking host round
+// trips per bounce (queue counter readbacks + a LaunchParams upload), here every stage reads its
+// queue length from device memory, so a whole render call is enqueued without a host sync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sptr_internal.h"
+
+struct sptr_ctx {
+  sptr::Context c;
+};
+
+namespace sptr {
+namespace {
+
+int fail(Context& c, int code, const std::string& msg) {
+  c.err = msg;
+  return code;
+}
+
+#define API_HIP(x)                                                                          \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+hipError_t ensure_buf(DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.p && b.bytes >= bytes) return hipSuccess;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e == hipSuccess) b.bytes = bytes;
+  return e;
+}
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+constexpr uint64_t kDefaultWavePaths = 1ull << 24;
+
+// MaterialManager::getMaterialFromHit (src/MaterialManager.cpp:91-103): the geomID's mapped
+// material when it is in range, else MaterialManager::getMaterialByID(geomID) (:79-89).
+int resolve_geom_materials(Context& c) {
+  const uint32_t nm = (uint32_t)c.mats_host.size();
+  const uint32_t ng = c.num_tri_geoms + c.num_sph;
+  if (!c.have_scene || nm == 0) return SPTR_OK;
+  std::vector<uint32_t> t(ng ? ng : 1, 0u);
+  for (uint32_t g = 0; g < ng; ++g) {
+    uint32_t m = ~0u;
+    if (g < c.geom_material.size() && c.geom_material[g] < nm) m = c.geom_material[g];
+    else m = (g < nm) ? g : g % nm;
+    t[g] = m;
+  }
+  API_HIP(ensure_buf(c.geom_mat, t.size() * 4));
+  API_HIP(hipMemcpy(c.geom_mat.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  return SPTR_OK;
+}
+
+// tile-packed local pixel -> image coordinates (host twin of the kernels' local_pixel)
+inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
+  const int ntx = (c.W + kTile - 1) / kTile;
+  const uint32_t lt = l >> 10, w = l & 1023u;
+  const uint32_t t = lt * (uint32_t)c.G + (uint32_t)c.R;
+  x = (int)(t % (uint32_t)ntx) * kTile + (int)(w & 31u);
+  y = (int)(t / (uint32_t)ntx) * kTile + (int)(w >> 5);
+  return x < c.W && y < c.H;
+}
+
+int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
+  resized = false;
+  if (c.W == W && c.H == H && c.G == G && c.R == R && c.accum.p) return SPTR_OK;
+  const int ntx = (W + kTile - 1) / kTile, nty = (H + kTile - 1) / kTile;
+  const int ntiles = ntx * nty;
+  const uint32_t local_tiles = (uint32_t)((ntiles - R + G - 1) / G);
+  c.W = W;
+  c.H = H;
+  c.G = G;
+  c.R = R;
+  c.local_tiles = local_tiles;
+  c.P = local_tiles * (uint32_t)kTilePixels;
+  API_HIP(ensure_buf(c.accum, (size_t)c.P * 16));
+  API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
+  API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
+  API_HIP(hipMemset(c.accum.p, 0, (size_t)c.P * 16));
+  API_HIP(hipMemset(c.tiles.p, 0, (size_t)c.P * 4));
+  API_HIP(hipMemset(c.image.p, 0, (size_t)W * H * 3));
+  c.last_samples = 0;
+  resized = true;
+  return SPTR_OK;
+}
+
+int ensure_wave(Context& c, uint64_t cap, uint32_t L) {
+  if (c.wave_cap >= cap && c.wave_L >= L && c.w_o.p) return SPTR_OK;
+  const size_t n = (size_t)cap;
+  API_HIP(ensure_buf(c.w_o, n * 16));
+  API_HIP(ensure_buf(c.w_d, n * 16));
+  API_HIP(ensure_buf(c.w_thr, n * 16));
+  API_HIP(ensure_buf(c.w_rad, n * 16));
+  API_HIP(ensure_buf(c.w_hit, n * 8));
+  API_HIP(ensure_buf(c.w_q0, n * 4));
+  API_HIP(ensure_buf(c.w_q1, n * 4));
+  API_HIP(ensure_buf(c.w_sq, n * 4));
+  API_HIP(ensure_buf(c.w_stask, n * (L ? L : 1) * 48));
+  c.wave_cap = cap;
+  c.wave_L = L ? L : 1;
+  return SPTR_OK;
+}
+
+WaveView wave_view(Context& c) {
+  WaveView w;
+  w.o = static_cast<float4*>(c.w_o.p);
+  w.d = static_cast<float4*>(c.w_d.p);
+  w.thr = static_cast<float4*>(c.w_thr.p);
+  w.rad = static_cast<float4*>(c.w_rad.p);
+  w.hit = static_cast<uint2*>(c.w_hit.p);
+  w.q[0] = static_cast<uint32_t*>(c.w_q0.p);
+  w.q[1] = static_cast<uint32_t*>(c.w_q1.p);
+  w.sq = static_cast<uint32_t*>(c.w_sq.p);
+  w.stask = static_cast<float4*>(c.w_stask.p);
+  w.cnt = static_cast<uint32_t*>(c.w_cnt.p);
+  w.tot = static_cast<unsigned long long*>(c.w_tot.p);
+  w.L = (uint32_t)c.lights_host.size();
+  return w;
+}
+
+FrameView frame_view(const Context& c, const sptr_frame& f) {
+  FrameView v;
+  v.W = f.width;
+  v.H = f.height;
+  v.ntx = (f.width + kTile - 1) / kTile;
+  v.G = c.G;
+  v.R = c.R;
+  v.P = c.P;
+  v.k = 1;
+  v.acc0 = f.frame_begin;
+  v.max_depth = f.max_depth;
+  const sptr_camera& k = f.camera;
+  v.cam_pos = v3(k.pos[0], k.pos[1], k.pos[2]);
+  v.cam_f = v3(k.forward[0], k.forward[1], k.forward[2]);
+  v.cam_r = v3(k.right[0], k.right[1], k.right[2]);
+  v.cam_u = v3(k.up[0], k.up[1], k.up[2]);
+  v.half_w = k.half_width;
+  v.half_h = k.half_height;
+  return v;
+}
+
+ShadeView shade_view(const Context& c) {
+  ShadeView s{};
+  s.mats = static_cast<const DevMaterial*>(c.mats.p);
+  s.num_mats = (uint32_t)c.mats_host.size();
+  s.geom_mat = static_cast<const uint32_t*>(c.geom_mat.p);
+  s.num_lights = (uint32_t)c.lights_host.size();
+  for (uint32_t i = 0; i < s.num_lights; ++i) s.lights[i] = c.lights_host[i];
+  s.env = static_cast<const float4*>(c.env.p);
+  s.env_size = c.env_size;
+  s.env_intensity = c.env_intensity;
+  s.env_clamp = c.env_clamp;
+  s.debug_mode = c.debug_mode;
+  return s;
+}
+
+struct StageTimer {
+  bool on = false;
+  hipStream_t s = nullptr;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  void begin(int stage, hipEvent_t* e0) {
+    if (!on) return;
+    (void)hipEventCreate(e0);
+    (void)hipEventRecord(*e0, s);
+    ev.push_back({stage, {*e0, nullptr}});
+  }
+  void end() {
+    if (!on) return;
+    hipEvent_t e1;
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e1, s);
+    ev.back().second.second = e1;
+  }
+  void collect(double ms[5], uint64_t& trace_launches) {
+    for (auto& x : ev) {
+      float t = 0.0f;
+      (void)hipEventElapsedTime(&t, x.second.first, x.second.second);
+      ms[x.first] += t;
+      if (x.first == 1) ++trace_launches;
+      (void)hipEventDestroy(x.second.first);
+      (void)hipEventDestroy(x.second.second);
+    }
+    ev.clear();
+  }
+};
+
+}  // namespace
+}  // namespace sptr
+
+using namespace sptr;
+
+extern "C" {
+
+int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
+
+int sptr_create(int device, sptr_ctx** out) {
+  if (!out) return SPTR_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SPTR_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return SPTR_ERR_INVALID;
+  sptr_ctx* x = new sptr_ctx();
+  Context& c = x->c;
+  c.device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) {
+    delete x;
+    return SPTR_ERR_HIP;
+  }
+  if (ensure_buf(c.w_cnt, kCntWords * 4) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess) {
+    delete x;
+    return SPTR_ERR_OOM;
+  }
+  *out = x;
+  return SPTR_OK;
+}
+
+int sptr_destroy(sptr_ctx* x) {
+  if (!x) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  (void)hipSetDevice(c.device);
+  (void)hipStreamSynchronize(c.stream);
+  DevBuf* bufs[] = {&c.nodes, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig, &c.sph_orig, &c.geom_mat,
+                    &c.mats,  &c.env,   &c.w_o,   &c.w_d,      &c.w_thr,    &c.w_rad,    &c.w_hit,    &c.w_q0,
+                    &c.w_q1,  &c.w_sq,  &c.w_stask, &c.w_cnt,  &c.w_tot,    &c.accum,    &c.tiles,    &c.image,
+                    &c.qbuf};
+  for (DevBuf* b : bufs) free_buf(*b);
+  if (c.stream) (void)hipStreamDestroy(c.stream);
+  delete x;
+  return SPTR_OK;
+}
+
+const char* sptr_last_error(const sptr_ctx* x) { return x ? x->c.err.c_str() : "null context"; }
+
+int sptr_set_debug_mode(sptr_ctx* x, int mode) {
+  if (!x) return SPTR_ERR_INVALID;
+  x->c.debug_mode = mode;
+  return SPTR_OK;
+}
+
+int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (max_paths > (1ull << 31)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^31");
+  x->c.wave_paths = max_paths;
+  return SPTR_OK;
+}
+
+int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
+  if (!x || !s) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  if ((s->num_tris && (!s->indices || !s->positions || !s->tri_geom_first)) || (s->num_spheres && !s->spheres) ||
+      ((s->num_tri_geoms + s->num_spheres) && !s->geom_material))
+    return fail(c, SPTR_ERR_INVALID, "scene: null array with nonzero count");
+  if ((uint64_t)s->num_tris + s->num_spheres >= (1ull << 30)) return fail(c, SPTR_ERR_INVALID, "scene too large");
+  if (s->num_tri_geoms && s->tri_geom_first[s->num_tri_geoms] != s->num_tris)
+    return fail(c, SPTR_ERR_INVALID, "scene: tri_geom_first must end at num_tris");
+  for (uint64_t i = 0; i < (uint64_t)s->num_tris * 3; ++i)
+    if (s->indices[i] >= s->num_verts) return fail(c, SPTR_ERR_INVALID, "scene: vertex index out of range");
+  std::vector<uint32_t> tg(s->num_tris);
+  for (uint32_t g = 0; g < s->num_tri_geoms; ++g) {
+    if (s->tri_geom_first[g] > s->tri_geom_first[g + 1]) return fail(c, SPTR_ERR_INVALID, "scene: geom offsets");
+    for (uint32_t i = s->tri_geom_first[g]; i < s->tri_geom_first[g + 1]; ++i) tg[i] = g;
+  }
+  c.have_scene = false;
+  c.num_tri_geoms = s->num_tri_geoms;
+  c.geom_first.assign(s->tri_geom_first, s->tri_geom_first + (s->num_tri_geoms ? s->num_tri_geoms + 1 : 0));
+  c.geom_material.assign(s->geom_material, s->geom_material + s->num_tri_geoms + s->num_spheres);
+  const int rc = build_lbvh(c, s->positions, s->num_verts, s->indices, s->num_tris, s->spheres, s->num_spheres, tg.data(),
+                            s->num_tri_geoms);
+  if (rc != SPTR_OK) return rc;
+  c.have_scene = true;
+  return resolve_geom_materials(c);
+}
+
+int sptr_scene_info(const sptr_ctx* x, uint32_t* num_prims, uint32_t* num_nodes, uint32_t* depth, double* build_ms) {
+  if (!x) return SPTR_ERR_INVALID;
+  const Context& c = x->c;
+  if (num_prims) *num_prims = c.num_tris + c.num_sph;
+  if (num_nodes) *num_nodes = c.num_nodes;
+  if (depth) *depth = c.bvh_depth;
+  if (build_ms) *build_ms = c.build_ms;
+  return SPTR_OK;
+}
+
+int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
+  if (!x || (n && !m)) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (n == 0) return fail(c, SPTR_ERR_INVALID, "at least one material is required");
+  API_HIP(hipSetDevice(c.device));
+  c.mats_host.resize(n);
+  std::memcpy(c.mats_host.data(), m, sizeof(DevMaterial) * n);
+  API_HIP(ensure_buf(c.mats, sizeof(DevMaterial) * n));
+  API_HIP(hipMemcpy(c.mats.p, c.mats_host.data(), sizeof(DevMaterial) * n, hipMemcpyHostToDevice));
+  return resolve_geom_materials(c);
+}
+
+int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
+  if (!x || (n && !l)) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (n > (uint32_t)kMaxLights) return fail(c, SPTR_ERR_INVALID, "too many lights");
+  c.lights_host.resize(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    DevLight& d = c.lights_host[i];
+    d.type = l[i].type;
+    if (l[i].type == 0) {  // DirectionalLight stores normalize(-direction) (Light.cpp:43-46)
+      const vec3 v = normalize(-v3(l[i].v[0], l[i].v[1], l[i].v[2]));
+      d.v[0] = v.x; d.v[1] = v.y; d.v[2] = v.z;
+    } else if (l[i].type == 1) {
+      d.v[0] = l[i].v[0]; d.v[1] = l[i].v[1]; d.v[2] = l[i].v[2];
+    } else {
+      return fail(c, SPTR_ERR_INVALID, "unknown light type");
+    }
+    const vec3 r = v3(l[i].color[0], l[i].color[1], l[i].color[2]) * l[i].intensity;
+    d.radiance[0] = r.x; d.radiance[1] = r.y; d.radiance[2] = r.z;
+    d.pad = 0.0f;
+  }
+  return SPTR_OK;
+}
+
+int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
+  if (!x) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  if (!e || !e->faces) {
+    free_buf(c.env);
+    c.env_size = 0;
+    if (e) {
+      c.env_intensity = e->intensity;
+      c.env_clamp = e->max_clamp;
+    }
+    return SPTR_OK;
+  }
+  if (e->size < 2) return fail(c, SPTR_ERR_INVALID, "environment face size must be >= 2");
+  const size_t texels = (size_t)6 * e->size * e->size;
+  std::vector<float> tmp(texels * 4);
+  for (size_t i = 0; i < texels; ++i) {
+    tmp[i * 4 + 0] = e->faces[i * 3 + 0];
+    tmp[i * 4 + 1] = e->faces[i * 3 + 1];
+    tmp[i * 4 + 2] = e->faces[i * 3 + 2];
+    tmp[i * 4 + 3] = 0.0f;
+  }
+  API_HIP(ensure_buf(c.env, texels * 16));
+  API_HIP(hipMemcpy(c.env.p, tmp.data(), texels * 16, hipMemcpyHostToDevice));
+  c.env_size = e->size;
+  c.env_intensity = e->intensity;
+  c.env_clamp = e->max_clamp;
+  return SPTR_OK;
+}
+
+int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
+  if (!x || !f) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "render: no scene uploaded");
+  if (c.mats_host.empty()) return fail(c, SPTR_ERR_NO_SCENE, "render: no materials set");
+  if (f->width <= 0 || f->height <= 0 || f->spp == 0 || f->max_depth == 0 || f->max_depth > (uint32_t)kMaxDepth ||
+      f->frame_begin == 0)
+    return fail(c, SPTR_ERR_INVALID, "render: bad frame parameters");
+  const int G = f->shard_count > 0 ? f->shard_count : 1, R = f->shard_count > 0 ? f->shard_rank : 0;
+  if (R < 0 || R >= G) return fail(c, SPTR_ERR_INVALID, "render: shard_rank out of range");
+  const int ntiles = ((f->width + kTile - 1) / kTile) * ((f->height + kTile - 1) / kTile);
+  if (R >= ntiles) return fail(c, SPTR_ERR_INVALID, "render: more shards than tiles");
+  if ((uint64_t)f->width * f->height > (1ull << 28)) return fail(c, SPTR_ERR_INVALID, "render: image too large");
+  bool resized = false;
+  int rc = ensure_pixels(c, f->width, f->height, G, R, resized);
+  if (rc != SPTR_OK) return rc;
+  const bool reset = f->frame_begin == 1;
+  if (!reset && f->frame_begin != c.last_samples + 1)
+    return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
+  const uint64_t wave_paths = c.wave_paths ? c.wave_paths : kDefaultWavePaths;
+  uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
+  k = std::min<uint32_t>(k, f->spp);
+  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size());
+  if (rc != SPTR_OK) return rc;
+
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  const SceneView sv = scene_view(c);
+  const ShadeView sh = shade_view(c);
+  const WaveView w = wave_view(c);
+  FrameView fv = frame_view(c, *f);
+  const bool timing = (f->flags & SPTR_FRAME_TIMING) != 0;
+  const bool count = (f->flags & SPTR_FRAME_COUNT_VISITS) != 0;
+  StageTimer tm;
+  tm.on = timing;
+  tm.s = s;
+  hipEvent_t e_begin, e_end, ev;
+  API_HIP(hipEventCreate(&e_begin));
+  API_HIP(hipEventCreate(&e_end));
+  API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+  API_HIP(hipEventRecord(e_begin, s));
+  uint32_t done = 0, waves = 0;
+  const int D = (int)f->max_depth;
+  while (done < f->spp) {
+    const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
+    fv.k = kk;
+    fv.acc0 = f->frame_begin + done;
+    API_HIP(hipMemsetAsync(c.w_cnt.p, 0, kCntWords * 4, s));
+    tm.begin(0, &ev);
+    launch_raygen(fv, w, s);
+    tm.end();
+    for (int d = 0; d < D; ++d) {
+      tm.begin(1, &ev);
+      launch_trace(sv, w, d, count, s);
+      tm.end();
+      tm.begin(2, &ev);
+      launch_shade(sv, sh, fv, w, d, s);
+      tm.end();
+      tm.begin(3, &ev);
+      launch_shadow(sv, w, d, count, s);
+      tm.end();
+    }
+    tm.begin(4, &ev);
+    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), reset && done == 0, D, s);
+    tm.end();
+    API_HIP(hipGetLastError());
+    done += kk;
+    ++waves;
+  }
+  const uint32_t total = f->frame_begin + f->spp - 1;
+  if (!(f->flags & SPTR_FRAME_NO_RESOLVE)) {
+    tm.begin(4, &ev);
+    launch_resolve(fv, static_cast<const float4*>(c.accum.p), total, static_cast<uint32_t*>(c.tiles.p),
+                   static_cast<uint8_t*>(c.image.p), s);
+    tm.end();
+  }
+  API_HIP(hipGetLastError());
+  API_HIP(hipEventRecord(e_end, s));
+  API_HIP(hipEventSynchronize(e_end));
+  c.last_samples = total;
+  unsigned long long tot[kTotWords];
+  API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e_begin, e_end);
+    stats->ms_total = ms;
+    double st[5] = {0, 0, 0, 0, 0};
+    tm.collect(st, stats->trace_launches);
+    stats->ms_raygen = st[0];
+    stats->ms_trace = st[1];
+    stats->ms_shade = st[2];
+    stats->ms_shadow = st[3];
+    stats->ms_accum = st[4];
+    stats->rays_closest = tot[kTotClosest];
+    stats->rays_shadow = tot[kTotShadow];
+    uint64_t valid = 0;
+    {
+      // pixels of this shard inside the image
+      const int ntx = (c.W + kTile - 1) / kTile;
+      for (uint32_t lt = 0; lt < c.local_tiles; ++lt) {
+        const uint32_t t = lt * (uint32_t)c.G + (uint32_t)c.R;
+        const int x0 = (int)(t % (uint32_t)ntx) * kTile, y0 = (int)(t / (uint32_t)ntx) * kTile;
+        valid += (uint64_t)std::min(kTile, c.W - x0) * (uint64_t)std::min(kTile, c.H - y0);
+      }
+    }
+    stats->samples = valid * f->spp;
+    stats->waves = waves;
+    stats->node_visits = tot[kTotNodes];
+    stats->tri_tests = tot[kTotTris];
+    stats->sphere_tests = tot[kTotSph];
+    stats->shadow_node_visits = tot[kTotShNodes];
+    stats->shadow_prim_tests = tot[kTotShPrims];
+  } else {
+    double st[5] = {0, 0, 0, 0, 0};
+    uint64_t tl = 0;
+    tm.collect(st, tl);
+  }
+  (void)hipEventDestroy(e_begin);
+  (void)hipEventDestroy(e_end);
+  return SPTR_OK;
+}
+
+int sptr_read_rgb8(sptr_ctx* x, uint8_t* rgb) {
+  if (!x || !rgb) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (!c.image.p) return fail(c, SPTR_ERR_NO_SCENE, "read_rgb8: nothing rendered");
+  API_HIP(hipSetDevice(c.device));
+  API_HIP(hipMemcpy(rgb, c.image.p, (size_t)c.W * c.H * 3, hipMemcpyDeviceToHost));
+  return SPTR_OK;
+}
+
+int sptr_read_accum(sptr_ctx* x, float* out) {
+  if (!x || !out) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (!c.accum.p) return fail(c, SPTR_ERR_NO_SCENE, "read_accum: nothing rendered");
+  API_HIP(hipSetDevice(c.device));
+  std::vector<float> a((size_t)c.P * 4);
+  API_HIP(hipMemcpy(a.data(), c.accum.p, a.size() * 4, hipMemcpyDeviceToHost));
+  std::memset(out, 0, (size_t)c.W * c.H * 3 * 4);
+  for (uint32_t l = 0; l < c.P; ++l) {
+    int px, py;
+    if (!host_local_pixel(c, l, px, py)) continue;
+    float* o = out + ((size_t)py * c.W + px) * 3;
+    o[0] = a[(size_t)l * 4 + 0];
+    o[1] = a[(size_t)l * 4 + 1];
+    o[2] = a[(size_t)l * 4 + 2];
+  }
+  return SPTR_OK;
+}
+
+int sptr_tiles_device(sptr_ctx* x, void** dptr, size_t* bytes) {
+  if (!x || !dptr || !bytes) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (!c.tiles.p) return fail(c, SPTR_ERR_NO_SCENE, "tiles_device: nothing rendered");
+  *dptr = c.tiles.p;
+  *bytes = (size_t)c.P * 4;
+  return SPTR_OK;
+}
+
+int sptr_unpack_tiles(sptr_ctx* x, const void* gathered, int32_t G, uint32_t tpr, int32_t W, int32_t H, void* out,
+                      void* stream) {
+  if (!x || !gathered || !out || G <= 0 || W <= 0 || H <= 0) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  if ((uint64_t)tpr * (uint64_t)G < (uint64_t)ntiles) return fail(c, SPTR_ERR_INVALID, "unpack: tiles_per_rank too small");
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  launch_unpack(static_cast<const uint32_t*>(gathered), G, tpr, W, H, static_cast<uint8_t*>(out), s);
+  API_HIP(hipGetLastError());
+  API_HIP(hipStreamSynchronize(s));
+  return SPTR_OK;
+}
+
+static int run_query(sptr_ctx* x, const float* rays, uint32_t n, bool anyhit, uint32_t* geom, uint32_t* prim, float* t,
+                     float* ng, uint8_t* occ) {
+  if (!x || (n && !rays)) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "query: no scene");
+  if (n == 0) return SPTR_OK;
+  API_HIP(hipSetDevice(c.device));
+  const size_t rb = (size_t)n * 32, refb = (size_t)n * 4, tb = (size_t)n * 4, nb = (size_t)n * 12, ob = (size_t)n;
+  API_HIP(ensure_buf(c.qbuf, rb + refb + tb + nb + ob + 64));
+  char* base = static_cast<char*>(c.qbuf.p);
+  float* d_rays = reinterpret_cast<float*>(base);
+  uint32_t* d_ref = reinterpret_cast<uint32_t*>(base + rb);
+  float* d_t = reinterpret_cast<float*>(base + rb + refb);
+  float* d_ng = reinterpret_cast<float*>(base + rb + refb + tb);
+  uint8_t* d_occ = reinterpret_cast<uint8_t*>(base + rb + refb + tb + nb);
+  API_HIP(hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
+  launch_query(scene_view(c), static_cast<const uint32_t*>(c.tri_orig.p), static_cast<const uint32_t*>(c.sph_orig.p),
+               d_rays, n, anyhit, d_ref, d_t, d_ng, d_occ, c.stream);
+  API_HIP(hipGetLastError());
+  API_HIP(hipStreamSynchronize(c.stream));
+  if (anyhit) {
+    API_HIP(hipMemcpy(occ, d_occ, ob, hipMemcpyDeviceToHost));
+    return SPTR_OK;
+  }
+  std::vector<uint32_t> ref(n);
+  API_HIP(hipMemcpy(ref.data(), d_ref, refb, hipMemcpyDeviceToHost));
+  API_HIP(hipMemcpy(t, d_t, tb, hipMemcpyDeviceToHost));
+  API_HIP(hipMemcpy(ng, d_ng, nb, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = ref[i];
+    if (r == kNoHit) {
+      geom[i] = prim[i] = 0xFFFFFFFFu;
+    } else if (r & kSphereBit) {
+      geom[i] = c.num_tri_geoms + (r & kIndexMask);
+      prim[i] = 0;
+    } else {
+      const uint32_t tri = r & kIndexMask;
+      const auto it = std::upper_bound(c.geom_first.begin(), c.geom_first.end(), tri);
+      const uint32_t g = (uint32_t)(it - c.geom_first.begin()) - 1u;
+      geom[i] = g;
+      prim[i] = tri - c.geom_first[g];
+    }
+  }
+  return SPTR_OK;
+}
+
+int sptr_intersect(sptr_ctx* x, const float* rays, uint32_t n, uint32_t* geom, uint32_t* prim, float* t, float* ng) {
+  if (!geom || !prim || !t || !ng) return SPTR_ERR_INVALID;
+  return run_query(x, rays, n, false, geom, prim, t, ng, nullptr);
+}
+
+int sptr_occluded(sptr_ctx* x, const float* rays, uint32_t n, uint8_t* occ) {
+  if (!occ) return SPTR_ERR_INVALID;
+  return run_query(x, rays, n, true, nullptr, nullptr, nullptr, nullptr, occ);
+}
+
+int sptr_primary_rays(sptr_ctx* x, const sptr_camera* cam, int32_t W, int32_t H, uint32_t acc, float* dirs,
+                      uint32_t* rng) {
+  if (!x || !cam || W <= 0 || H <= 0 || !dirs || !rng) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  sptr_frame f{};
+  f.width = W;
+  f.height = H;
+  f.camera = *cam;
+  f.frame_begin = acc;
+  f.max_depth = 1;
+  FrameView fv = frame_view(c, f);
+  const size_t n = (size_t)W * H;
+  API_HIP(ensure_buf(c.qbuf, n * 16 + 64));
+  float* d_dirs = static_cast<float*>(c.qbuf.p);
+  uint32_t* d_rng = reinterpret_cast<uint32_t*>(static_cast<char*>(c.qbuf.p) + n * 12);
+  launch_primary(fv, d_dirs, d_rng, c.stream);
+  API_HIP(hipGetLastError());
+  API_HIP(hipStreamSynchronize(c.stream));
+  API_HIP(hipMemcpy(dirs, d_dirs, n * 12, hipMemcpyDeviceToHost));
+  API_HIP(hipMemcpy(rng, d_rng, n * 4, hipMemcpyDeviceToHost));
+  return SPTR_OK;
+}
+
+}  // extern "C"

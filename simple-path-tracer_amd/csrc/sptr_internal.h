@@ -1,0 +1,176 @@
+// sptr_internal.h — device data layout and context of libsptr_hip (not part of the public ABI).
+//
+// HBM layout (SoA "float4 streams", one 16-B coalesced load per lane per stream):
+//   path state  : o[p] = (origin.xyz, rng bits)   d[p] = (dir.xyz, -)   thr[p]   rad[p]
+//   hit record  : hit[p] = (t bits, prim ref)      — written by k_trace, read by k_shade
+//   queues      : q0/q1 ping-pong u32 path ids (extension rays), sq u32 path ids (shadow rays)
+//   shadow task : stask[p*L + i] = {origin.xyz, tfar} {dir.xyz, -} {contrib.xyz, valid}
+// Path id p = sample_slot * P + local_pixel; local pixels are tile-packed (32x32 tiles of this
+// shard, row-major inside a tile) so a 64-lane wave covers two rows of one tile.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "sptr_hip.h"
+#include "sptr_math.h"
+
+namespace sptr {
+
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kSphereBit = 0x40000000u;
+constexpr uint32_t kIndexMask = 0x3FFFFFFFu;
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+constexpr int kTile = 32;
+constexpr int kTilePixels = kTile * kTile;
+constexpr int kMaxLights = 8;
+constexpr int kMaxDepth = 32;
+constexpr int kStack = 64;
+constexpr int kBlock = 256;
+constexpr uint32_t kLdsSceneBytes = 48 * 1024;  // scenes up to this size are staged whole into LDS
+
+// BVH2 node, 64 B: both child boxes + child links.  Link: internal node index, or
+// kLeafBit | [kSphereBit] | sorted primitive slot.
+struct BvhNode {
+  float4 lxy;  // left  lo.x hi.x lo.y hi.y
+  float4 rxy;  // right lo.x hi.x lo.y hi.y
+  float4 z;    // left lo.z hi.z, right lo.z hi.z
+  uint4 link;  // left, right, parent, pad
+};
+static_assert(sizeof(BvhNode) == 64, "node size");
+
+struct DevMaterial {  // == sptr_material
+  float albedo[3];
+  float metallic;
+  float roughness;
+  float emission[3];
+  float ior;
+  int32_t type;
+  float pad[2];
+};
+static_assert(sizeof(DevMaterial) == 48, "material size");
+
+struct DevLight {  // host-precomputed per Light::getRadiance (Light.cpp:43-79)
+  int32_t type;     // 0 directional, 1 point
+  float v[3];       // direction TO the light (normalize(-d)), or position
+  float radiance[3];  // color * intensity
+  float pad;
+};
+
+struct SceneView {
+  const BvhNode* nodes;
+  const float4* tris;  // 3 float4 per sorted triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z Ng.xyz
+  const float4* sph;   // sorted spheres: c.xyz r
+  const uint32_t* tri_geom;  // geomID per sorted triangle
+  const uint32_t* sph_geom;  // geomID per sorted sphere
+  uint32_t num_nodes, num_tris, num_sph, root;
+  uint32_t lds_bytes;  // 0: traverse from global memory
+};
+
+struct ShadeView {
+  const DevMaterial* mats;
+  uint32_t num_mats;
+  const uint32_t* geom_mat;  // geomID -> material index, resolved as MaterialManager::getMaterialFromHit
+  uint32_t num_lights;
+  DevLight lights[kMaxLights];
+  const float4* env;  // 6*S*S texels (rgb, -) or null for the procedural sky
+  int32_t env_size;
+  float env_intensity, env_clamp;
+  int32_t debug_mode;
+};
+
+struct FrameView {
+  int32_t W, H, ntx, G, R;
+  uint32_t P;   // local pixels (local tiles * 1024)
+  uint32_t k;   // samples in this wave
+  uint32_t acc0;  // accumulation index of sample slot 0
+  uint32_t max_depth;
+  vec3 cam_pos, cam_f, cam_r, cam_u;
+  float half_w, half_h;
+};
+
+// counters block (u32 unless noted); zeroed per wave
+enum : int {
+  kCntLive = 0,                     // [kMaxDepth+1] extension queue sizes per depth
+  kCntShadow = kCntLive + kMaxDepth + 1,  // [kMaxDepth] shadow queue sizes per depth
+  kCntWords = kCntShadow + kMaxDepth,
+};
+// 64-bit totals block
+enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotWords };
+
+struct WaveView {
+  float4* o;
+  float4* d;
+  float4* thr;
+  float4* rad;
+  uint2* hit;
+  uint32_t* q[2];
+  uint32_t* sq;
+  float4* stask;
+  uint32_t* cnt;
+  unsigned long long* tot;
+  uint32_t L;  // lights (tasks per path)
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int debug_mode = 0;
+  uint64_t wave_paths = 0;  // 0 = default
+  // scene
+  DevBuf nodes, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
+  uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
+  uint32_t num_tri_geoms = 0;
+  std::vector<uint32_t> geom_first;     // host copy for primID derivation
+  std::vector<uint32_t> geom_material;  // host copy
+  bool have_scene = false;
+  double build_ms = 0.0;
+  // shading state
+  std::vector<DevMaterial> mats_host;
+  DevBuf mats;
+  std::vector<DevLight> lights_host;
+  DevBuf env;
+  int32_t env_size = 0;
+  float env_intensity = 0.8f, env_clamp = 5.0f;
+  // wavefront buffers
+  uint64_t wave_cap = 0;  // paths
+  uint32_t wave_L = 0;
+  DevBuf w_o, w_d, w_thr, w_rad, w_hit, w_q0, w_q1, w_sq, w_stask, w_cnt, w_tot;
+  // pixel buffers
+  int32_t W = 0, H = 0, G = 1, R = 0;
+  uint32_t P = 0, local_tiles = 0;
+  DevBuf accum, tiles, image;
+  uint32_t last_samples = 0;  // accumulation count after the last render
+  // query scratch
+  DevBuf qbuf;
+};
+
+// kernels_lbvh.hip
+int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* h_idx, uint32_t ntris,
+               const float* h_sph, uint32_t nsph, const uint32_t* h_tri_geom, uint32_t sph_geom_base);
+
+// kernels_wavefront.hip
+SceneView scene_view(const Context& c);
+void launch_raygen(const FrameView& f, const WaveView& w, hipStream_t s);
+void launch_trace(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s);
+void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                  hipStream_t s);
+void launch_shadow(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,
+                       hipStream_t s);
+void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
+                    hipStream_t s);
+void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
+                   hipStream_t s);
+void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
+                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, hipStream_t s);
+void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s);
+
+}  // namespace sptr

@@ -1,0 +1,70 @@
+// hip_backend.h — backends::HipBackend, the MI355X drop-in for the reference's GPU backend slot.
+// Public surface = backends::OptixBackend (include/backends/OptixBackend.h:39-71): build(SceneDesc),
+// render(rgb, w, h, Camera), setEnvironment / setMaterialManager / setLightManager (non-owning;
+// the pointees must outlive rendering), destroy(), setDebugMode().  Progressive accumulation is
+// owned by the backend and restarts on resize or camera change, as OptixBackend::render does
+// (src/backends/OptixBackend.cpp:1518-1542).  Extras: setSettings, renderLinear, stats.
+// Errors: build() returns false; render() logs and leaves the buffer untouched (no exit()).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "scene_desc.h"
+#include "shading.h"
+
+namespace backends {
+
+class HipBackend {
+ public:
+  struct Settings {
+    uint32_t spp_per_call = 1;  // progressive frames per render() call (GLRenderer renders 1)
+    uint32_t max_depth = 6;     // PathTracer::Settings::max_depth used by the wavefront tile task
+  };
+
+  explicit HipBackend(int device = 0);
+  ~HipBackend();
+  HipBackend(const HipBackend&) = delete;
+  HipBackend& operator=(const HipBackend&) = delete;
+
+  bool build(const scene::SceneDesc& sceneDesc);
+  void render(unsigned char* pixels, int width, int height, const Camera& camera);
+  void setEnvironment(const EnvironmentManager* env) { env_ = env; env_dirty_ = true; }
+  void setMaterialManager(const MaterialManager* mm) { mm_ = mm; mats_dirty_ = true; }
+  void setLightManager(const LightManager* lm) { lm_ = lm; lights_dirty_ = true; }
+  void destroy();
+  void setDebugMode(int mode);
+
+  void setSettings(const Settings& s) { settings_ = s; }
+  const Settings& getSettings() const { return settings_; }
+  // linear accumulated radiance mean (width*height*3) of the current accumulation
+  bool renderLinear(float* rgb32, int width, int height, const Camera& camera);
+  const sptr_stats& stats() const { return stats_; }
+  uint32_t frameIndex() const { return frame_index_; }
+  const std::string& lastError() const { return err_; }
+  const std::vector<uint32_t>& getGeomMaterialMapping() const { return geom_material_; }
+
+ private:
+  bool ensureContext();
+  bool syncState();
+  bool renderInternal(int width, int height, const Camera& camera);
+
+  int device_;
+  sptr_ctx* ctx_ = nullptr;
+  const EnvironmentManager* env_ = nullptr;
+  const MaterialManager* mm_ = nullptr;
+  const LightManager* lm_ = nullptr;
+  bool env_dirty_ = true, mats_dirty_ = true, lights_dirty_ = true, built_ = false;
+  Settings settings_;
+  sptr_stats stats_{};
+  uint32_t frame_index_ = 0;
+  int last_w_ = 0, last_h_ = 0;
+  bool has_last_camera_ = false;
+  std::array<float, 9> last_cam_{};
+  std::vector<uint32_t> geom_material_;
+  std::string err_;
+  int debug_mode_ = 0;
+};
+
+}  // namespace backends

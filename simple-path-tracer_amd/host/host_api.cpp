@@ -1,0 +1,98 @@
+// host_api.cpp — C ABI access to the host-side scene layer (sptr_host_* in include/sptr_hip.h), so
+// foreign callers (ctypes harness, CLI) build scenes, cameras and material tables with exactly the
+// C++ code the HipBackend uses.
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "scene_desc.h"
+#include "shading.h"
+
+struct sptr_host_scene {
+  scene::FlatScene flat;
+};
+
+extern "C" {
+
+int sptr_host_builtin_scene(const char* name, uint32_t p0, uint32_t p1, sptr_host_scene** out) {
+  if (!name || !out) return SPTR_ERR_INVALID;
+  *out = nullptr;
+  const std::string n(name);
+  scene::SceneDesc sd;
+  if (n == "default") sd = scene::BuildDefaultScene();
+  else if (n == "default_emitter") sd = scene::BuildDefaultSceneWithEmitter();
+  else if (n == "test_triangle") sd = scene::BuildTestTriangleScene();
+  else if (n == "sphere_mesh") {
+    if (p0 == 0 || p1 == 0) return SPTR_ERR_INVALID;
+    sd = scene::BuildSphereMeshScene(p0, p1);
+  } else if (n.rfind("gltf:", 0) == 0) {
+    std::string err;
+    if (!scene::LoadGLTFScene(n.substr(5), p0, sd, &err)) return SPTR_ERR_INVALID;
+  } else {
+    return SPTR_ERR_INVALID;
+  }
+  sptr_host_scene* s = new sptr_host_scene();
+  s->flat = scene::Flatten(sd);
+  *out = s;
+  return SPTR_OK;
+}
+
+int sptr_host_scene_view(const sptr_host_scene* s, sptr_scene* view) {
+  if (!s || !view) return SPTR_ERR_INVALID;
+  *view = s->flat.view();
+  return SPTR_OK;
+}
+
+void sptr_host_scene_free(sptr_host_scene* s) { delete s; }
+
+int sptr_host_camera_lookat(const float pos[3], const float target[3], float fov_deg, float aspect, sptr_camera* out) {
+  if (!pos || !target || !out) return SPTR_ERR_INVALID;
+  const Camera c(vec3{pos[0], pos[1], pos[2]}, vec3{target[0], target[1], target[2]}, vec3{0.0f, 1.0f, 0.0f}, fov_deg,
+                 aspect);
+  *out = c.toDevice();
+  return SPTR_OK;
+}
+
+int sptr_host_preset_materials(int with_light, sptr_material* out, int capacity) {
+  MaterialManager mm;
+  if (with_light) mm.addMaterial(Materials::Light());
+  std::vector<sptr_material> v;
+  mm.buildDeviceMaterials(v);
+  if (out)
+    for (int i = 0; i < int(v.size()) && i < capacity; ++i) out[i] = v[size_t(i)];
+  return int(v.size());
+}
+
+int sptr_host_default_lights(sptr_light* out, int capacity) {
+  LightManager lm;  // setupLights, src/main.cpp:85-94
+  lm.addDirectionalLight(vec3{-0.5f, -1.0f, 0.3f}, vec3{1.0f, 0.95f, 0.8f}, 2.0f);
+  std::vector<sptr_light> v;
+  lm.buildDeviceLights(v);
+  if (out)
+    for (int i = 0; i < int(v.size()) && i < capacity; ++i) out[i] = v[size_t(i)];
+  return int(v.size());
+}
+
+int sptr_host_equirect_to_faces(const float* rgb, int32_t w, int32_t h, int32_t size, float* faces) {
+  if (!rgb || !faces || w <= 0 || h <= 0 || size < 2) return SPTR_ERR_INVALID;
+  EquirectToFaces(rgb, w, h, size, faces);
+  return SPTR_OK;
+}
+
+int sptr_host_load_hdr(const char* path, float** rgb, int32_t* w, int32_t* h) {
+  if (!path || !rgb || !w || !h) return SPTR_ERR_INVALID;
+  std::vector<float> v;
+  int ww = 0, hh = 0;
+  if (!LoadRadianceHDR(path, v, ww, hh, nullptr)) return SPTR_ERR_INVALID;
+  float* p = static_cast<float*>(std::malloc(v.size() * sizeof(float)));
+  if (!p) return SPTR_ERR_OOM;
+  std::memcpy(p, v.data(), v.size() * sizeof(float));
+  *rgb = p;
+  *w = ww;
+  *h = hh;
+  return SPTR_OK;
+}
+
+void sptr_host_free(void* p) { std::free(p); }
+
+}  // extern "C"

@@ -1,0 +1,401 @@
+"""sptr — Python (ctypes) binding of libsptr_hip.so, the MI355X wavefront path-tracing backend.
+
+This is the ctypes form of the binding a reference-side maintainer would add:
+every call goes straight to the C ABI in include/sptr_hip.h.  There is no CPU fallback: if the
+library is missing or no GPU is present, constructing a Renderer raises.
+
+Reference mapping: Renderer mirrors backends::OptixBackend (include/backends/OptixBackend.h:39-71)
+with the CPU wavefront integrator's semantics (src/wavefront/wf_pt_cpu.cpp:61-255).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsptr_hip.so")
+
+SPTR_FRAME_TIMING = 1
+SPTR_FRAME_NO_RESOLVE = 2
+SPTR_FRAME_COUNT_VISITS = 4
+
+
+class SptrError(RuntimeError):
+    pass
+
+
+class Scene(C.Structure):
+    _fields_ = [
+        ("positions", C.POINTER(C.c_float)), ("num_verts", C.c_uint32),
+        ("indices", C.POINTER(C.c_uint32)), ("num_tris", C.c_uint32),
+        ("tri_geom_first", C.POINTER(C.c_uint32)), ("num_tri_geoms", C.c_uint32),
+        ("spheres", C.POINTER(C.c_float)), ("num_spheres", C.c_uint32),
+        ("geom_material", C.POINTER(C.c_uint32)),
+    ]
+
+
+class Material(C.Structure):
+    _fields_ = [("albedo", C.c_float * 3), ("metallic", C.c_float), ("roughness", C.c_float),
+                ("emission", C.c_float * 3), ("ior", C.c_float), ("type", C.c_int32), ("pad", C.c_float * 2)]
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("v", C.c_float * 3), ("color", C.c_float * 3), ("intensity", C.c_float)]
+
+
+class Environment(C.Structure):
+    _fields_ = [("faces", C.POINTER(C.c_float)), ("size", C.c_int32), ("intensity", C.c_float),
+                ("max_clamp", C.c_float)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("forward", C.c_float * 3), ("right", C.c_float * 3),
+                ("up", C.c_float * 3), ("half_width", C.c_float), ("half_height", C.c_float)]
+
+    def as_array(self) -> np.ndarray:
+        return np.array(list(self.pos) + list(self.forward) + list(self.right) + list(self.up)
+                        + [self.half_width, self.half_height], dtype=np.float32)
+
+
+class Frame(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("camera", Camera), ("frame_begin", C.c_uint32),
+                ("spp", C.c_uint32), ("max_depth", C.c_uint32), ("shard_rank", C.c_int32),
+                ("shard_count", C.c_int32), ("flags", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays_closest", C.c_uint64), ("rays_shadow", C.c_uint64), ("samples", C.c_uint64),
+                ("waves", C.c_uint64), ("ms_total", C.c_double), ("ms_raygen", C.c_double),
+                ("ms_trace", C.c_double), ("ms_shade", C.c_double), ("ms_shadow", C.c_double),
+                ("ms_accum", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("shadow_node_visits", C.c_uint64),
+                ("shadow_prim_tests", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+# every symbol include/sptr_hip.h declares
+EXPORTS = [
+    "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
+    "sptr_set_wave_paths", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_environment", "sptr_scene_info", "sptr_render", "sptr_read_rgb8", "sptr_read_accum",
+    "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
+    "sptr_host_builtin_scene", "sptr_host_scene_view", "sptr_host_scene_free", "sptr_host_camera_lookat",
+    "sptr_host_preset_materials", "sptr_host_default_lights", "sptr_host_equirect_to_faces",
+    "sptr_host_load_hdr", "sptr_host_free",
+]
+
+
+def lib() -> C.CDLL:
+    """Load libsptr_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SptrError(f"{LIB_PATH} not built (run make in simple-path-tracer_amd/)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u32, u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+    fp, up, bp = C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)
+    sig = {
+        "sptr_abi_version": (C.c_int, []),
+        "sptr_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "sptr_destroy": (C.c_int, [vp]),
+        "sptr_last_error": (C.c_char_p, [vp]),
+        "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
+        "sptr_set_wave_paths": (C.c_int, [vp, u64]),
+        "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
+        "sptr_set_materials": (C.c_int, [vp, C.POINTER(Material), u32]),
+        "sptr_set_lights": (C.c_int, [vp, C.POINTER(Light), u32]),
+        "sptr_set_environment": (C.c_int, [vp, C.POINTER(Environment)]),
+        "sptr_scene_info": (C.c_int, [vp, up, up, up, C.POINTER(C.c_double)]),
+        "sptr_render": (C.c_int, [vp, C.POINTER(Frame), vp, C.POINTER(Stats)]),
+        "sptr_read_rgb8": (C.c_int, [vp, bp]),
+        "sptr_read_accum": (C.c_int, [vp, fp]),
+        "sptr_tiles_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
+        "sptr_unpack_tiles": (C.c_int, [vp, vp, i32, u32, i32, i32, vp, vp]),
+        "sptr_intersect": (C.c_int, [vp, fp, u32, up, up, fp, fp]),
+        "sptr_occluded": (C.c_int, [vp, fp, u32, bp]),
+        "sptr_primary_rays": (C.c_int, [vp, C.POINTER(Camera), i32, i32, u32, fp, up]),
+        "sptr_host_builtin_scene": (C.c_int, [C.c_char_p, u32, u32, C.POINTER(vp)]),
+        "sptr_host_scene_view": (C.c_int, [vp, C.POINTER(Scene)]),
+        "sptr_host_scene_free": (None, [vp]),
+        "sptr_host_camera_lookat": (C.c_int, [fp, fp, C.c_float, C.c_float, C.POINTER(Camera)]),
+        "sptr_host_preset_materials": (C.c_int, [C.c_int, C.POINTER(Material), C.c_int]),
+        "sptr_host_default_lights": (C.c_int, [C.POINTER(Light), C.c_int]),
+        "sptr_host_equirect_to_faces": (C.c_int, [fp, i32, i32, i32, fp]),
+        "sptr_host_load_hdr": (C.c_int, [C.c_char_p, C.POINTER(fp), C.POINTER(i32), C.POINTER(i32)]),
+        "sptr_host_free": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _f(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _u(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def _b(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+# --------------------------------------------------------------------------------- host scene layer
+@dataclass
+class FlatScene:
+    """World-space flattened scene in EmbreeBackend::build geomID order (numpy-owned copies)."""
+    positions: np.ndarray       # (V,3) float32
+    indices: np.ndarray         # (T,3) uint32
+    tri_geom_first: np.ndarray  # (G+1,) uint32
+    spheres: np.ndarray         # (S,4) float32
+    geom_material: np.ndarray   # (G+S,) uint32
+
+    def to_c(self) -> Scene:
+        self._keep = [np.ascontiguousarray(self.positions, np.float32), np.ascontiguousarray(self.indices, np.uint32),
+                      np.ascontiguousarray(self.tri_geom_first, np.uint32),
+                      np.ascontiguousarray(self.spheres, np.float32),
+                      np.ascontiguousarray(self.geom_material, np.uint32)]
+        p, i, g, s, m = self._keep
+        return Scene(_f(p), len(p), _u(i), len(i), _u(g), len(g) - 1, _f(s), len(s), _u(m))
+
+
+def builtin_scene(name: str, p0: int = 0, p1: int = 0) -> FlatScene:
+    """Scenes built by the C++ host layer: default, default_emitter, test_triangle,
+    sphere_mesh (p0 stacks, p1 slices), gltf:<path> (p0 = material)."""
+    L = lib()
+    h = C.c_void_p()
+    rc = L.sptr_host_builtin_scene(name.encode(), p0, p1, C.byref(h))
+    if rc != 0:
+        raise SptrError(f"builtin scene {name!r} failed ({rc})")
+    try:
+        v = Scene()
+        L.sptr_host_scene_view(h, C.byref(v))
+
+        def arr(ptr, n, dt, cols):
+            if n == 0:
+                return np.zeros((0, cols) if cols > 1 else (0,), dt)
+            a = np.ctypeslib.as_array(ptr, shape=(n * cols,)).copy().astype(dt)
+            return a.reshape(n, cols) if cols > 1 else a
+
+        return FlatScene(
+            positions=arr(v.positions, v.num_verts, np.float32, 3),
+            indices=arr(v.indices, v.num_tris, np.uint32, 3),
+            tri_geom_first=arr(v.tri_geom_first, v.num_tri_geoms + 1, np.uint32, 1),
+            spheres=arr(v.spheres, v.num_spheres, np.float32, 4),
+            geom_material=arr(v.geom_material, v.num_tri_geoms + v.num_spheres, np.uint32, 1),
+        )
+    finally:
+        L.sptr_host_scene_free(h)
+
+
+def camera_lookat(pos=(0.0, 3.0, 8.0), target=(0.0, 1.0, 0.0), fov=60.0, aspect=800 / 600) -> Camera:
+    """Camera(pos, target, +Y, fov, aspect) as src/main.cpp:97-103 sets it up."""
+    L = lib()
+    c = Camera()
+    p = np.array(pos, np.float32)
+    t = np.array(target, np.float32)
+    rc = L.sptr_host_camera_lookat(_f(p), _f(t), C.c_float(fov), C.c_float(aspect), C.byref(c))
+    if rc != 0:
+        raise SptrError("camera_lookat failed")
+    return c
+
+
+def preset_materials(with_light: bool = False) -> list:
+    L = lib()
+    arr = (Material * 16)()
+    n = L.sptr_host_preset_materials(1 if with_light else 0, arr, 16)
+    return [arr[i] for i in range(n)]
+
+
+def materials_as_array(mats) -> np.ndarray:
+    """(n,12) float32: albedo3 metallic roughness emission3 ior type pad pad (oracle layout)."""
+    out = np.zeros((len(mats), 12), np.float32)
+    for i, m in enumerate(mats):
+        out[i, 0:3] = list(m.albedo)
+        out[i, 3] = m.metallic
+        out[i, 4] = m.roughness
+        out[i, 5:8] = list(m.emission)
+        out[i, 8] = m.ior
+        out[i, 9] = m.type
+    return out
+
+
+def default_lights() -> list:
+    L = lib()
+    arr = (Light * 8)()
+    n = L.sptr_host_default_lights(arr, 8)
+    return [arr[i] for i in range(n)]
+
+
+def lights_as_array(lights) -> np.ndarray:
+    out = np.zeros((len(lights), 8), np.float32)
+    for i, l in enumerate(lights):
+        out[i, 0] = l.type
+        out[i, 1:4] = list(l.v)
+        out[i, 4:7] = list(l.color)
+        out[i, 7] = l.intensity
+    return out
+
+
+def equirect_to_faces(rgb: np.ndarray, size: int = 512) -> np.ndarray:
+    L = lib()
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    h, w = rgb.shape[:2]
+    faces = np.zeros((6, size, size, 3), np.float32)
+    if L.sptr_host_equirect_to_faces(_f(rgb), w, h, size, _f(faces)) != 0:
+        raise SptrError("equirect_to_faces failed")
+    return faces
+
+
+def load_hdr(path: str) -> np.ndarray:
+    L = lib()
+    p = C.POINTER(C.c_float)()
+    w, h = C.c_int32(), C.c_int32()
+    if L.sptr_host_load_hdr(path.encode(), C.byref(p), C.byref(w), C.byref(h)) != 0:
+        raise SptrError(f"cannot read {path}")
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
+    finally:
+        L.sptr_host_free(p)
+
+
+# --------------------------------------------------------------------------------- device renderer
+class Renderer:
+    """One sptr context (one GPU).  Raises SptrError on any failure; never falls back to the CPU."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        self._L = L
+        h = C.c_void_p()
+        rc = L.sptr_create(device, C.byref(h))
+        if rc != 0:
+            raise SptrError(f"sptr_create(device={device}) failed ({rc}); a HIP GPU is required")
+        self._h = h
+        self.width = self.height = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.sptr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self._L.sptr_last_error(self._h)
+            raise SptrError(f"{what}: rc={rc}: {msg.decode() if msg else ''}")
+
+    def upload_scene(self, s: FlatScene):
+        cs = s.to_c()
+        self._check(self._L.sptr_upload_scene(self._h, C.byref(cs)), "upload_scene")
+
+    def scene_info(self) -> dict:
+        n, nn, dep = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        ms = C.c_double()
+        self._check(self._L.sptr_scene_info(self._h, C.byref(n), C.byref(nn), C.byref(dep), C.byref(ms)), "info")
+        return {"prims": n.value, "nodes": nn.value, "depth": dep.value, "build_ms": ms.value}
+
+    def set_materials(self, mats):
+        arr = (Material * len(mats))(*mats)
+        self._check(self._L.sptr_set_materials(self._h, arr, len(mats)), "set_materials")
+
+    def set_lights(self, lights):
+        arr = (Light * max(1, len(lights)))(*lights)
+        self._check(self._L.sptr_set_lights(self._h, arr, len(lights)), "set_lights")
+
+    def set_environment(self, faces: np.ndarray | None = None, intensity: float = 0.8, max_clamp: float = 5.0):
+        e = Environment()
+        if faces is not None:
+            self._env_keep = np.ascontiguousarray(faces, np.float32)
+            e.faces = _f(self._env_keep)
+            e.size = self._env_keep.shape[1]
+        e.intensity = intensity
+        e.max_clamp = max_clamp
+        self._check(self._L.sptr_set_environment(self._h, C.byref(e)), "set_environment")
+
+    def set_wave_paths(self, n: int):
+        self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
+
+    def set_debug_mode(self, m: int):
+        self._check(self._L.sptr_set_debug_mode(self._h, m), "set_debug_mode")
+
+    def render(self, cam: Camera, width: int, height: int, spp: int = 1, frame_begin: int = 1,
+               max_depth: int = 6, shard_rank: int = 0, shard_count: int = 1, flags: int = 0,
+               stream: int | None = None) -> Stats:
+        f = Frame(width, height, cam, frame_begin, spp, max_depth, shard_rank, shard_count, flags)
+        st = Stats()
+        self._check(self._L.sptr_render(self._h, C.byref(f), C.c_void_p(stream) if stream else None, C.byref(st)),
+                    "render")
+        self.width, self.height = width, height
+        return st
+
+    def read_rgb8(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 3), np.uint8)
+        self._check(self._L.sptr_read_rgb8(self._h, _b(out)), "read_rgb8")
+        return out
+
+    def read_accum(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 3), np.float32)
+        self._check(self._L.sptr_read_accum(self._h, _f(out)), "read_accum")
+        return out
+
+    def tiles_device(self) -> tuple[int, int]:
+        p = C.c_void_p()
+        n = C.c_size_t()
+        self._check(self._L.sptr_tiles_device(self._h, C.byref(p), C.byref(n)), "tiles_device")
+        return p.value, n.value
+
+    def unpack_tiles(self, gathered_ptr: int, shard_count: int, tiles_per_rank: int, width: int, height: int,
+                     out_ptr: int, stream: int | None = None):
+        self._check(self._L.sptr_unpack_tiles(self._h, C.c_void_p(gathered_ptr), shard_count, tiles_per_rank, width,
+                                              height, C.c_void_p(out_ptr),
+                                              C.c_void_p(stream) if stream else None), "unpack_tiles")
+
+    def intersect(self, rays: np.ndarray):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        n = len(rays)
+        geom = np.zeros(n, np.uint32)
+        prim = np.zeros(n, np.uint32)
+        t = np.zeros(n, np.float32)
+        ng = np.zeros((n, 3), np.float32)
+        self._check(self._L.sptr_intersect(self._h, _f(rays), n, _u(geom), _u(prim), _f(t), _f(ng)), "intersect")
+        return geom, prim, t, ng
+
+    def occluded(self, rays: np.ndarray) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros(len(rays), np.uint8)
+        self._check(self._L.sptr_occluded(self._h, _f(rays), len(rays), _b(out)), "occluded")
+        return out
+
+    def primary_rays(self, cam: Camera, width: int, height: int, acc: int):
+        dirs = np.zeros((height, width, 3), np.float32)
+        rng = np.zeros((height, width), np.uint32)
+        self._check(self._L.sptr_primary_rays(self._h, C.byref(cam), width, height, acc, _f(dirs), _u(rng)),
+                    "primary_rays")
+        return dirs, rng
+
+
+def setup_default(r: Renderer, scene: str = "default", p0: int = 0, p1: int = 0, env_faces=None) -> FlatScene:
+    """Upload a builtin scene with the reference's default state (presets, one sun, sky)."""
+    s = builtin_scene(scene, p0, p1)
+    r.upload_scene(s)
+    r.set_materials(preset_materials(with_light=(scene == "default_emitter")))
+    r.set_lights(default_lights())
+    r.set_environment(env_faces)
+    return s
