@@ -1,17 +1,19 @@
 // kernels_wavefront.hip — the wavefront stages of the MI355X (gfx950) path tracer.
 //
-//   k_raygen  : path init for every (sample slot, tile-packed pixel) of a wave; wave64 ballot append
-//               into the depth-0 queue.                  (GLRenderer.cpp:384-408, Camera.cpp:95-106)
+//   raygen    : path init (seeding, jitter, camera ray) is a device function evaluated inside the
+//               bounce-0 trace and shade kernels: bounce 0 covers every path densely, so it needs
+//               no queue and no path-state round trip.  (GLRenderer.cpp:384-408, Camera.cpp:95-106)
 //   k_trace   : closest-hit BVH2 traversal + Embree-style Moeller-Trumbore triangles + the
 //               reference's quadratic spheres, one thread per queued path.   (wf_pt_cpu.cpp:28-56)
-//   k_shade   : miss/env, emission, direct-light shadow tasks, metal/glass/diffuse continuation with
-//               ballot-compacted next queue and shadow queue.           (wf_pt_cpu.cpp:94-248)
+//   k_shade   : miss/env, emission, direct-light shadow tasks, metal/glass/diffuse continuation;
+//               survivors and shadow rays are compacted by wave64 ballot + LDS staging, one global
+//               atomic per ~2K queue entries.                        (wf_pt_cpu.cpp:94-248)
 //   k_shadow  : any-hit traversal of the shadow tasks, adds unoccluded light. (Light.cpp:16-40)
 //   k_accum   : per-pixel sum of the wave's samples in accumulation order.  (GLRenderer.cpp:411-413)
 //   k_resolve : mean -> ACES -> gamma 1/2.2 -> clamp -> 8-bit truncation.   (GLRenderer.cpp:416-431)
 //
-// Kernels run a fixed grid (<= 8 blocks per CU) and grid-stride over a device-side queue count, so a
-// wave needs no host round trip between stages.  Arithmetic order follows the CPU reference line
+// Kernels run a fixed grid (<= 8 blocks per CU); each block takes a contiguous slice of the
+// device-side queue, so a wavefront batch needs no host round trip between stages.  Arithmetic order follows the CPU reference line
 // for line (see sptr_math.h); the file is compiled with -ffp-contract=off.  Box tests are the one
 // place that uses fma: they only prune traversal and are padded to stay conservative.
 #include <hip/hip_runtime.h>
@@ -34,6 +36,49 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
   if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// LDS-staged queue append.  Lanes append into a block-local LDS buffer (one LDS atomic per wave);
+// the block flushes the buffer to the global queue with ONE global atomic once it holds more than
+// kStageCap - kBlock entries.  A single global counter takes ~88 returning atomics/us on MI355X,
+// so per-wave global appends serialise; per-~2K-entry flushes do not.
+constexpr uint32_t kStageCap = 2048;
+struct alignas(16) Stage {  // 16-B multiple: keeps the dynamic-LDS base aligned (Guideline 17)
+  uint32_t buf[kStageCap];
+  uint32_t n;
+  uint32_t base;
+  uint32_t pad[2];
+};
+static_assert(sizeof(Stage) % 16 == 0, "Stage must be a 16-byte multiple");
+__device__ __forceinline__ void stage_push(Stage& st, bool pred, uint32_t val) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0ull) return;
+  const uint32_t lane = lane_id();
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0u;
+  if ((int)lane == leader) base = atomicAdd(&st.n, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  if (pred) st.buf[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = val;
+}
+// Block-uniform call.  Flushes when nearly full, or whenever `force` and non-empty.
+__device__ __forceinline__ void stage_flush(Stage& st, uint32_t* gq, uint32_t* gcnt, bool force) {
+  __syncthreads();
+  const uint32_t n = st.n;
+  if (n > kStageCap - kBlock || (force && n > 0u)) {
+    if (threadIdx.x == 0) st.base = atomicAdd(gcnt, n);
+    __syncthreads();
+    const uint32_t b = st.base;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gq[b + i] = st.buf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) st.n = 0u;
+    __syncthreads();
+  }
+}
+// Contiguous per-block slice [lo, hi) of n items, whole multiples of the block size.
+__device__ __forceinline__ void block_slice(uint32_t n, uint32_t& lo, uint32_t& hi) {
+  const uint32_t per = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+  lo = min(n, blockIdx.x * per);
+  hi = min(n, lo + per);
 }
 
 __device__ __forceinline__ vec3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
@@ -272,54 +317,26 @@ __device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long lon
   }
 }
 
-// --------------------------------------------------------------------------------- k_raygen
-__global__ void __launch_bounds__(kBlock) k_raygen(FrameView f, WaveView w) {
-  const uint32_t C = f.P * f.k;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < C; base += grid_threads()) {
-    const uint32_t p = base + threadIdx.x;
-    bool live = false;
-    if (p < C) {
-      const uint32_t s = p / f.P, l = p - s * f.P;
-      int x, y;
-      live = local_pixel(f, l, x, y);
-      w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (live) {
-        const uint32_t acc = f.acc0 + s;
-        const uint32_t ps = (uint32_t)(y * f.W + x);
-        uint32_t r = wang_hash(ps ^ acc * 9781u);
-        const float jx = rand01(r);
-        const float jy = rand01(r);
-        const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
-        const vec3 d = safe_normalize(dir);
-        const uint32_t rng = wang_hash((ps ^ acc) ^ 1u);
-        w.o[p] = f4(f.cam_pos, __uint_as_float(rng));
-        w.d[p] = f4(d, 0.0f);
-        w.thr[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-      }
-    }
-    const uint32_t slot = wave_append(&w.cnt[kCntLive], live);
-    if (live) w.q[0][slot] = p;
-  }
-}
-
-// --------------------------------------------------------------------------------- k_trace
-template <bool kLds, bool kCount>
-__global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, WaveView w, int depth) {
-  extern __shared__ float4 lds[];
-  const Staged sc = stage_scene<kLds>(sv, lds);
-  const uint32_t n = w.cnt[kCntLive + depth];
-  const uint32_t* q = w.q[depth & 1];
-  Visits vc;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
-    const uint32_t p = q[i];
-    const float4 o4 = w.o[p], d4 = w.d[p];
-    const Ray r = make_ray(xyz(o4), xyz(d4));
-    float tfar = __builtin_huge_valf();
-    uint32_t ref = kNoHit;
-    traverse<false, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
-    w.hit[p] = make_uint2(__float_as_uint(tfar), ref);
-  }
-  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+// --------------------------------------------------------------------------------- path init
+// GLRenderer::renderWavefrontTileTask seeding + WavefrontPathTracerCPU::traceRay's first rng, for
+// path p = sample_slot * P + local pixel.  Returns false for tile slots outside the image.
+struct Primary {
+  vec3 d;
+  uint32_t rng;
+};
+__device__ __forceinline__ bool primary_path(const FrameView& f, uint32_t p, Primary& out) {
+  const uint32_t s = p / f.P, l = p - s * f.P;
+  int x, y;
+  if (!local_pixel(f, l, x, y)) return false;
+  const uint32_t acc = f.acc0 + s;
+  const uint32_t ps = (uint32_t)(y * f.W + x);
+  uint32_t r = wang_hash(ps ^ acc * 9781u);
+  const float jx = rand01(r);
+  const float jy = rand01(r);
+  const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
+  out.d = safe_normalize(dir);
+  out.rng = wang_hash((ps ^ acc) ^ 1u);
+  return true;
 }
 
 // --------------------------------------------------------------------------------- shading math
@@ -412,39 +429,125 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
   return (kD * diffuse + spec) * NdotL;
 }
 
+// --------------------------------------------------------------------------------- k_trace
+// Closest hit for every path queued at this bounce.  A miss ends the path here: the environment
+// term (wf_pt_cpu.cpp:98-103) is added in place, so only hits are compacted into the shade queue.
+// kPrimary: bounce 0, one thread per path slot, camera ray computed in place (no queue, no state).
+template <bool kLds, bool kCount, bool kPrimary>
+__global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
+  extern __shared__ float4 lds[];
+  __shared__ Stage st_hit;
+  if (threadIdx.x == 0) st_hit.n = 0u;
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  __syncthreads();
+  const uint32_t n = kPrimary ? f.P * f.k : w.cnt[kCntLive + depth];
+  if (kPrimary && blockIdx.x == 0 && threadIdx.x == 0) w.cnt[kCntLive] = f.valid * f.k;
+  const uint32_t* q = w.q[depth & 1];
+  Visits vc;
+  uint32_t lo, hi;
+  block_slice(n, lo, hi);
+  for (uint32_t base = lo; base < hi; base += kBlock) {
+    const uint32_t i = base + threadIdx.x;
+    bool active = i < hi, hit = false;
+    uint32_t p = 0;
+    vec3 o, d;
+    if (active) {
+      if (kPrimary) {
+        Primary pr;
+        p = i;
+        active = primary_path(f, p, pr);
+        o = f.cam_pos;
+        d = pr.d;
+      } else {
+        p = q[i];
+        o = xyz(w.o[p]);
+        d = xyz(w.d[p]);
+      }
+    }
+    if (active) {
+      const Ray r = make_ray(o, d);
+      float tfar = __builtin_huge_valf();
+      uint32_t ref = kNoHit;
+      hit = traverse<false, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
+      if (hit) {
+        w.hit[p] = make_uint2(__float_as_uint(tfar), ref);
+      } else if (sh.debug_mode == 1) {
+        w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else {
+        const vec3 e = env_color(sh, safe_normalize(d));
+        vec3 rv;
+        if (kPrimary) {
+          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+        } else {
+          rv = xyz(w.rad[p]) + xyz(w.thr[p]) * e;
+        }
+        w.rad[p] = f4(rv, 0.0f);
+      }
+    }
+    stage_push(st_hit, hit, p);
+    stage_flush(st_hit, w.qh, &w.cnt[kCntHit + depth], false);
+  }
+  stage_flush(st_hit, w.qh, &w.cnt[kCntHit + depth], true);
+  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+}
+
 // --------------------------------------------------------------------------------- k_shade
+// One thread per path that hit something at this bounce (misses were finished by k_trace).  Radiance is read lazily (only when something is
+// added) and written back once; bounce 0 starts from zero radiance and unit throughput in
+// registers.  Shadow task per (path, light): {origin.xyz, tfar} {contrib.xyz, valid} [{dir.xyz}]
+// — the direction slot exists only when a point light is present (directional lights take the
+// constant direction from the light table).
+template <bool kPrimary>
 __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
-  __shared__ DevMaterial smat[64];
-  const uint32_t nm = sh.num_mats < 64u ? sh.num_mats : 64u;
+  __shared__ DevMaterial smat[32];
+  __shared__ Stage st_next, st_shadow;
+  const uint32_t nm = sh.num_mats < 32u ? sh.num_mats : 32u;
   for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
     reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
+  if (threadIdx.x == 0) {
+    st_next.n = 0u;
+    st_shadow.n = 0u;
+  }
   __syncthreads();
 
-  const uint32_t n = w.cnt[kCntLive + depth];
-  const uint32_t* q = w.q[depth & 1];
+  const uint32_t n = w.cnt[kCntHit + depth];
+  const uint32_t* q = w.qh;
   uint32_t* qn = w.q[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += grid_threads()) {
+  const uint32_t ts = w.tstride;
+  uint32_t lo, hi;
+  block_slice(n, lo, hi);
+  for (uint32_t base = lo; base < hi; base += kBlock) {
     const uint32_t i = base + threadIdx.x;
     bool cont = false, shadow = false;
     uint32_t p = 0;
-    if (i < n) {
+    bool active = i < hi;
+    vec3 ro, rd, thr;
+    uint32_t rng = 0u;
+    if (active) {
       p = q[i];
+      if (kPrimary) {
+        Primary pr;
+        primary_path(f, p, pr);
+        ro = f.cam_pos;
+        rd = pr.d;
+        thr = v3(1.0f, 1.0f, 1.0f);
+        rng = pr.rng;
+      } else {
+        const float4 o4 = w.o[p];
+        ro = xyz(o4);
+        rd = xyz(w.d[p]);
+        thr = xyz(w.thr[p]);
+        rng = __float_as_uint(o4.w);
+      }
+    }
+    if (active) {
       const uint2 h = w.hit[p];
-      const float4 o4 = w.o[p], d4 = w.d[p], t4 = w.thr[p];
-      const vec3 ro = xyz(o4), rd = xyz(d4);
-      vec3 thr = xyz(t4);
-      uint32_t rng = __float_as_uint(o4.w);
-      if (h.y == kNoHit) {  // miss -> environment, path ends
-        if (sh.debug_mode == 1) {
-          w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        } else {
-          const vec3 e = env_color(sh, safe_normalize(rd));
-          const vec3 rv = xyz(w.rad[p]) + thr * e;
-          w.rad[p] = f4(rv, 0.0f);
-        }
-      } else if (sh.debug_mode == 1) {
-        w.rad[p] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      vec3 radv = v3(0.0f, 0.0f, 0.0f);
+      bool loaded = kPrimary, dirty = kPrimary;
+      if (sh.debug_mode == 1) {
+        radv = v3(1.0f, 1.0f, 1.0f);
+        dirty = true;
       } else {
         const float t = __uint_as_float(h.x);
         const vec3 P = ro + t * rd;
@@ -465,10 +568,14 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, Fr
         const DevMaterial m = (mid < nm) ? smat[mid] : sh.mats[mid];
         const vec3 emission = v3(m.emission[0], m.emission[1], m.emission[2]);
         if (dot(emission, emission) > 0.0f) {
-          const vec3 rv = xyz(w.rad[p]) + thr * emission;
-          w.rad[p] = f4(rv, 0.0f);
+          if (!loaded) {
+            radv = xyz(w.rad[p]);
+            loaded = true;
+          }
+          radv = radv + thr * emission;
+          dirty = true;
         }
-        // direct light: build shadow tasks (contribution precomputed; added if unoccluded)
+        // direct light: shadow tasks carry the precomputed contribution, added if unoccluded
         {
           const vec3 view = -rd;
           for (uint32_t li = 0; li < sh.num_lights; ++li) {
@@ -487,9 +594,9 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, Fr
               Li = v3(L.radiance[0], L.radiance[1], L.radiance[2]) / att;
             }
             const float cs = fmax_g(dot(nrm, ldir), 0.0f);
-            float4* task = w.stask + ((size_t)p * w.L + li) * 3;
+            float4* task = w.stask + ((size_t)p * w.L + li) * ts;
             if (cs <= 0.0f) {
-              task[2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              task[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
               continue;
             }
             const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
@@ -497,8 +604,8 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, Fr
             const vec3 fr = eval_brdf(m, nrm, view, ldir);
             const vec3 contrib = thr * (fr * Li * cs);
             task[0] = f4(so, ldist - 1e-4f);
-            task[1] = f4(ldir, 0.0f);
-            task[2] = f4(contrib, 1.0f);
+            task[1] = f4(contrib, 1.0f);
+            if (ts > 2u) task[2] = f4(ldir, 0.0f);
             shadow = true;
           }
         }
@@ -570,32 +677,39 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, Fr
           w.thr[p] = f4(thr, 0.0f);
         }
       }
+      if (dirty) w.rad[p] = f4(radv, 0.0f);
     }
-    const uint32_t slot = wave_append(&w.cnt[kCntLive + depth + 1], cont);
-    if (cont) qn[slot] = p;
-    const uint32_t sslot = wave_append(&w.cnt[kCntShadow + depth], shadow);
-    if (shadow) w.sq[sslot] = p;
+    stage_push(st_next, cont, p);
+    stage_push(st_shadow, shadow, p);
+    stage_flush(st_next, qn, &w.cnt[kCntLive + depth + 1], false);
+    stage_flush(st_shadow, w.sq, &w.cnt[kCntShadow + depth], false);
   }
+  stage_flush(st_next, qn, &w.cnt[kCntLive + depth + 1], true);
+  stage_flush(st_shadow, w.sq, &w.cnt[kCntShadow + depth], true);
 }
 
 // --------------------------------------------------------------------------------- k_shadow
 template <bool kLds, bool kCount>
-__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth) {
   extern __shared__ float4 lds[];
   const Staged sc = stage_scene<kLds>(sv, lds);
   const uint32_t n = w.cnt[kCntShadow + depth];
+  const uint32_t ts = w.tstride;
   Visits vc;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
+  uint32_t lo, hi;
+  block_slice(n, lo, hi);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     const uint32_t p = w.sq[i];
-    vec3 add = v3(0.0f, 0.0f, 0.0f);
     bool any = false;
     vec3 rv = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t li = 0; li < w.L; ++li) {
-      const float4* task = w.stask + ((size_t)p * w.L + li) * 3;
-      const float4 c = task[2];
+      const float4* task = w.stask + ((size_t)p * w.L + li) * ts;
+      const float4 c = task[1];
       if (c.w == 0.0f) continue;
-      const float4 a = task[0], b = task[1];
-      const Ray r = make_ray(xyz(a), xyz(b));
+      const float4 a = task[0];
+      const vec3 dir = (ts > 2u && sh.lights[li].type != 0) ? xyz(task[2])
+                                                             : v3(sh.lights[li].v[0], sh.lights[li].v[1], sh.lights[li].v[2]);
+      const Ray r = make_ray(xyz(a), dir);
       float tfar = a.w;
       uint32_t ref = kNoHit;
       const bool occ = traverse<true, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
@@ -605,7 +719,6 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, WaveView w, int
         rv = rv + xyz(c);
       }
     }
-    (void)add;
     if (any) w.rad[p] = f4(rv, 0.0f);
   }
   if (kCount) flush_visits(vc, w.tot, kTotShNodes);
@@ -749,34 +862,35 @@ SceneView scene_view(const Context& c) {
   return s;
 }
 
-void launch_raygen(const FrameView& f, const WaveView& w, hipStream_t s) {
-  hipLaunchKernelGGL(k_raygen, dim3(grid_for((uint64_t)f.P * f.k)), dim3(kBlock), 0, s, f, w);
-}
-
-void launch_trace(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s) {
+void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
+                  hipStream_t s) {
   const dim3 g(grid_for(1ull << 22)), b(kBlock);
-  if (sv.lds_bytes) {
-    if (count) hipLaunchKernelGGL((k_trace<true, true>), g, b, sv.lds_bytes, s, sv, w, depth);
-    else hipLaunchKernelGGL((k_trace<true, false>), g, b, sv.lds_bytes, s, sv, w, depth);
+  const uint32_t lb = sv.lds_bytes;
+#define SPTR_TRACE(L, C, P) hipLaunchKernelGGL((k_trace<L, C, P>), g, b, L ? lb : 0u, s, sv, sh, f, w, depth)
+  if (depth == 0) {
+    if (lb) { if (count) SPTR_TRACE(true, true, true); else SPTR_TRACE(true, false, true); }
+    else    { if (count) SPTR_TRACE(false, true, true); else SPTR_TRACE(false, false, true); }
   } else {
-    if (count) hipLaunchKernelGGL((k_trace<false, true>), g, b, 0, s, sv, w, depth);
-    else hipLaunchKernelGGL((k_trace<false, false>), g, b, 0, s, sv, w, depth);
+    if (lb) { if (count) SPTR_TRACE(true, true, false); else SPTR_TRACE(true, false, false); }
+    else    { if (count) SPTR_TRACE(false, true, false); else SPTR_TRACE(false, false, false); }
   }
+#undef SPTR_TRACE
 }
 
 void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s) {
-  hipLaunchKernelGGL(k_shade, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+  if (depth == 0) hipLaunchKernelGGL(k_shade<true>, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+  else hipLaunchKernelGGL(k_shade<false>, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
 }
 
-void launch_shadow(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s) {
+void launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, hipStream_t s) {
   const dim3 g(grid_for(1ull << 22)), b(kBlock);
   if (sv.lds_bytes) {
-    if (count) hipLaunchKernelGGL((k_shadow<true, true>), g, b, sv.lds_bytes, s, sv, w, depth);
-    else hipLaunchKernelGGL((k_shadow<true, false>), g, b, sv.lds_bytes, s, sv, w, depth);
+    if (count) hipLaunchKernelGGL((k_shadow<true, true>), g, b, sv.lds_bytes, s, sv, sh, w, depth);
+    else hipLaunchKernelGGL((k_shadow<true, false>), g, b, sv.lds_bytes, s, sv, sh, w, depth);
   } else {
-    if (count) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, s, sv, w, depth);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, s, sv, w, depth);
+    if (count) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, s, sv, sh, w, depth);
+    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, s, sv, sh, w, depth);
   }
 }
 

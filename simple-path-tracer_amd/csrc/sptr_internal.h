@@ -86,6 +86,7 @@ struct FrameView {
   uint32_t k;   // samples in this wave
   uint32_t acc0;  // accumulation index of sample slot 0
   uint32_t max_depth;
+  uint32_t valid;  // pixels of this shard inside the image
   vec3 cam_pos, cam_f, cam_r, cam_u;
   float half_w, half_h;
 };
@@ -94,7 +95,8 @@ struct FrameView {
 enum : int {
   kCntLive = 0,                     // [kMaxDepth+1] extension queue sizes per depth
   kCntShadow = kCntLive + kMaxDepth + 1,  // [kMaxDepth] shadow queue sizes per depth
-  kCntWords = kCntShadow + kMaxDepth,
+  kCntHit = kCntShadow + kMaxDepth,       // [kMaxDepth] shade (hit) queue sizes per depth
+  kCntWords = kCntHit + kMaxDepth,
 };
 // 64-bit totals block
 enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotWords };
@@ -105,12 +107,14 @@ struct WaveView {
   float4* thr;
   float4* rad;
   uint2* hit;
-  uint32_t* q[2];
+  uint32_t* q[2];  // paths to trace at bounce d (ping-pong)
+  uint32_t* qh;    // paths that hit at this bounce (shade queue)
   uint32_t* sq;
   float4* stask;
   uint32_t* cnt;
   unsigned long long* tot;
-  uint32_t L;  // lights (tasks per path)
+  uint32_t L;        // lights (tasks per path)
+  uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
 };
 
 struct DevBuf {
@@ -142,7 +146,7 @@ struct Context {
   // wavefront buffers
   uint64_t wave_cap = 0;  // paths
   uint32_t wave_L = 0;
-  DevBuf w_o, w_d, w_thr, w_rad, w_hit, w_q0, w_q1, w_sq, w_stask, w_cnt, w_tot;
+  DevBuf w_o, w_d, w_thr, w_rad, w_hit, w_q0, w_q1, w_qh, w_sq, w_stask, w_cnt, w_tot;
   // pixel buffers
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;
@@ -150,6 +154,7 @@ struct Context {
   uint32_t last_samples = 0;  // accumulation count after the last render
   // query scratch
   DevBuf qbuf;
+  std::vector<hipEvent_t> events;  // timing event pool
 };
 
 // kernels_lbvh.hip
@@ -158,11 +163,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
 
 // kernels_wavefront.hip
 SceneView scene_view(const Context& c);
-void launch_raygen(const FrameView& f, const WaveView& w, hipStream_t s);
-void launch_trace(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s);
+void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
+                  hipStream_t s);
 void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s);
-void launch_shadow(const SceneView& sv, const WaveView& w, int depth, bool count, hipStream_t s);
+void launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, hipStream_t s);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,
                        hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
