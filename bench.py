@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-paths", type=int, default=0)
+    ap.add_argument("--leaf-size", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -81,6 +82,8 @@ def main():
     r = sptr.Renderer(local)
     if args.wave_paths:
         r.set_wave_paths(args.wave_paths)
+    if args.leaf_size:
+        r.set_leaf_size(args.leaf_size)
     sptr.setup_default(r, SCENE)
     cam = sptr.camera_lookat(aspect=W / H)
     ntx, nty = (W + 31) // 32, (H + 31) // 32

@@ -140,8 +140,11 @@ int sptr_create(int device, sptr_ctx** out);
 int sptr_destroy(sptr_ctx* ctx);
 const char* sptr_last_error(const sptr_ctx* ctx);
 int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
-/* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default). */
+/* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default 2^27,
+ * at most 2^30). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
+/* Maximum primitives per BVH leaf range (1..8, default 4); applies to the next sptr_upload_scene. */
+int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 
 /* ---- scene / state (OptixBackend::build and setters) -------------------------------------------- */
 int sptr_upload_scene(sptr_ctx* ctx, const sptr_scene* scene); /* builds the LBVH on the device */
@@ -193,6 +196,13 @@ int sptr_host_preset_materials(int with_light, sptr_material* out, int capacity)
 int sptr_host_default_lights(sptr_light* out, int capacity);
 /* Cubemap::loadEquirectangular: RGB float equirect (w x h) -> 6 faces of size x size. */
 int sptr_host_equirect_to_faces(const float* rgb, int32_t w, int32_t h, int32_t size, float* faces);
+/* Host twins of the device tile packing (interleaved 32x32 tiles, shard R of G; see sptr_render):
+ * pack this shard's pixels of an RGB8 image into RGBA8 tile-packed words, and scatter gathered
+ * rank-major tile buffers back into an RGB8 image. */
+int sptr_host_pack_tiles(const uint8_t* rgb, int32_t width, int32_t height, int32_t shard_count, int32_t shard_rank,
+                         uint32_t* tiles);
+int sptr_host_unpack_tiles(const uint32_t* gathered, int32_t shard_count, uint32_t tiles_per_rank, int32_t width,
+                           int32_t height, uint8_t* rgb);
 /* Radiance .hdr reader (RGBE, RLE) -> RGB float; caller frees with sptr_host_free. */
 int sptr_host_load_hdr(const char* path, float** rgb, int32_t* w, int32_t* h);
 void sptr_host_free(void* p);

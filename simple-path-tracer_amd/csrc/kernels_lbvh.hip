@@ -13,6 +13,7 @@
 //                   the gfx950 guide, Guideline 16)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -129,7 +130,7 @@ __global__ void k_is_tri(uint32_t N, uint32_t ntri, const uint32_t* vals, uint32
 }
 
 __global__ void k_leaves(BuildIn in, const uint32_t* vals, const uint32_t* tri_slot, float4* tris, uint32_t* tri_geom,
-                         uint32_t* tri_orig, float4* sph, uint32_t* sph_geom, uint32_t* sph_orig, uint32_t* leaf_link) {
+                         uint32_t* tri_orig, float4* sph, uint32_t* sph_geom, uint32_t* sph_orig, uint32_t* prim_ref) {
   const uint32_t N = in.ntri + in.nsph;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
     const uint32_t prim = vals[i];
@@ -148,14 +149,14 @@ __global__ void k_leaves(BuildIn in, const uint32_t* vals, const uint32_t* tri_s
       tris[3 * slot + 2] = make_float4(e2.z, ng.x, ng.y, ng.z);
       tri_geom[slot] = in.tri_geom[prim];
       tri_orig[slot] = prim;
-      leaf_link[i] = kLeafBit | slot;
+      prim_ref[i] = slot;
     } else {
       const uint32_t slot = i - tri_slot[i];
       const uint32_t s = prim - in.ntri;
       sph[slot] = in.sph[s];
       sph_geom[slot] = in.sph_geom_base + s;
       sph_orig[slot] = s;
-      leaf_link[i] = kLeafBit | kSphereBit | slot;
+      prim_ref[i] = kSphereBit | slot;
     }
   }
 }
@@ -167,7 +168,15 @@ __device__ __forceinline__ int delta(const uint64_t* keys, int N, int i, int j) 
   return __clzll((long long)(a ^ b));
 }
 
-__global__ void k_karras(int N, const uint64_t* keys, const uint32_t* leaf_link, BvhNode* nodes, uint32_t* leaf_parent) {
+// Leaf range link for sorted primitives [lo, lo+cnt).
+__device__ __forceinline__ uint32_t range_link(uint32_t lo, uint32_t cnt) {
+  return kLeafBit | (lo << kLeafCountBits) | (cnt - 1u);
+}
+
+// Karras 2012 hierarchy.  Child links become range leaves when the child subtree covers at most
+// leaf_max primitives; `kids` keeps the binary-tree child ids (leaf i -> kLeafBit | i) for refit.
+__global__ void k_karras(int N, const uint64_t* keys, uint32_t leaf_max, BvhNode* nodes, uint2* kids,
+                         uint32_t* leaf_parent) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
     const int d = (delta(keys, N, i, i + 1) - delta(keys, N, i, i - 1)) >= 0 ? 1 : -1;
     const int dmin = delta(keys, N, i, i - d);
@@ -186,24 +195,26 @@ __global__ void k_karras(int N, const uint64_t* keys, const uint32_t* leaf_link,
     }
     const int gamma = i + s * d + min(d, 0);
     const int lo = min(i, j), hi = max(i, j);
-    uint32_t left, right;
+    uint32_t kl, kr;  // binary-tree child ids
     if (lo == gamma) {
-      left = leaf_link[gamma];
+      kl = kLeafBit | (uint32_t)gamma;
       leaf_parent[gamma] = (uint32_t)i;
     } else {
-      left = (uint32_t)gamma;
+      kl = (uint32_t)gamma;
       nodes[gamma].link.z = (uint32_t)i;
     }
     if (hi == gamma + 1) {
-      right = leaf_link[gamma + 1];
+      kr = kLeafBit | (uint32_t)(gamma + 1);
       leaf_parent[gamma + 1] = (uint32_t)i;
     } else {
-      right = (uint32_t)(gamma + 1);
+      kr = (uint32_t)(gamma + 1);
       nodes[gamma + 1].link.z = (uint32_t)i;
     }
-    nodes[i].link.x = left;
-    nodes[i].link.y = right;
+    const uint32_t nl = (uint32_t)(gamma - lo + 1), nr = (uint32_t)(hi - gamma);
+    nodes[i].link.x = nl <= leaf_max ? range_link((uint32_t)lo, nl) : kl;
+    nodes[i].link.y = nr <= leaf_max ? range_link((uint32_t)(gamma + 1), nr) : kr;
     nodes[i].link.w = 0u;
+    kids[i] = make_uint2(kl, kr);
   }
 }
 
@@ -217,13 +228,13 @@ __device__ __forceinline__ float ld_agent(const float* p) {
 
 // Each leaf walks up; at each node the first arriving child stops, the second merges both child
 // boxes (read back through agent-scope loads) and continues.  Also records the leaf depth.
-__global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const float4* bhi, const uint32_t* leaf_link,
+__global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const float4* bhi, const uint2* kids,
                         const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* max_depth) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
     const uint32_t prim = vals[i];
     const float4 a = blo[prim], b = bhi[prim];
     float lo[3] = {a.x, a.y, a.z}, hi[3] = {b.x, b.y, b.z};
-    uint32_t child = leaf_link[i];
+    uint32_t child = kLeafBit | (uint32_t)i;
     uint32_t par = leaf_parent[i];
     // depth of this leaf (walk the parent chain)
     {
@@ -236,7 +247,7 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
     }
     for (;;) {
       BvhNode* nd = nodes + par;
-      const bool left = (nd->link.x == child);
+      const bool left = (kids[par].x == child);
       float* f = reinterpret_cast<float*>(nd);
       // lxy = f[0..3], rxy = f[4..7], z = f[8..11]
       if (left) {
@@ -314,6 +325,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));
+  LB_CHECK(realloc_buf(c.prim_ref, ((size_t)N + 3) / 4 * 16));
   if (N == 0) {
     c.root = kNoHit;
     return SPTR_OK;
@@ -337,8 +349,9 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   float4 *blo = nullptr, *bhi = nullptr;
   uint32_t* cb = nullptr;
   uint64_t *keys = nullptr, *keys_s = nullptr;
-  uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_link = nullptr,
-           *leaf_parent = nullptr, *rflags = nullptr, *dmax = nullptr;
+  uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
+           *rflags = nullptr, *dmax = nullptr;
+  uint2* kids = nullptr;
   LB_CHECK(tmp.alloc(&blo, N));
   LB_CHECK(tmp.alloc(&bhi, N));
   LB_CHECK(tmp.alloc(&cb, 8));
@@ -348,7 +361,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(tmp.alloc(&vals_s, N));
   LB_CHECK(tmp.alloc(&flag, N));
   LB_CHECK(tmp.alloc(&slot, N));
-  LB_CHECK(tmp.alloc(&leaf_link, N));
+  LB_CHECK(tmp.alloc(&kids, N));
   LB_CHECK(tmp.alloc(&leaf_parent, N));
   LB_CHECK(tmp.alloc(&rflags, N));
   LB_CHECK(tmp.alloc(&dmax, 1));
@@ -372,26 +385,26 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   hipLaunchKernelGGL(k_leaves, dim3(blocks_for(N)), dim3(256), 0, s, in, vals_s, slot,
                      static_cast<float4*>(c.tris.p), static_cast<uint32_t*>(c.tri_geom.p),
                      static_cast<uint32_t*>(c.tri_orig.p), static_cast<float4*>(c.sph.p),
-                     static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p), leaf_link);
+                     static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p),
+                     static_cast<uint32_t*>(c.prim_ref.p));
   LB_CHECK(hipGetLastError());
+  const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size, kMaxLeafSize));
   if (N == 1) {
-    uint32_t link = 0;
-    LB_CHECK(hipMemcpyAsync(&link, leaf_link, 4, hipMemcpyDeviceToHost, s));
-    LB_CHECK(hipStreamSynchronize(s));
-    c.root = link;
+    c.root = kLeafBit | 0u;  // range [0, 1)
     c.bvh_depth = 0;
   } else {
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
     LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
-    hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_link, nodes, leaf_parent);
-    hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, leaf_link,
-                       leaf_parent, nodes, rflags, dmax);
+    hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
+                       leaf_parent);
+    hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, kids, leaf_parent,
+                       nodes, rflags, dmax);
     LB_CHECK(hipGetLastError());
     uint32_t dep = 0;
     LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
     LB_CHECK(hipStreamSynchronize(s));
-    c.root = 0;
+    c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;
     if (dep >= (uint32_t)kStack) {
       c.err = "lbvh: tree depth " + std::to_string(dep) + " exceeds the traversal stack";

@@ -6,8 +6,8 @@
 //   k_trace   : closest-hit BVH2 traversal + Embree-style Moeller-Trumbore triangles + the
 //               reference's quadratic spheres, one thread per queued path.   (wf_pt_cpu.cpp:28-56)
 //   k_shade   : miss/env, emission, direct-light shadow tasks, metal/glass/diffuse continuation;
-//               survivors and shadow rays are compacted by wave64 ballot + LDS staging, one global
-//               atomic per ~2K queue entries.                        (wf_pt_cpu.cpp:94-248)
+//               survivors and shadow rays are compacted by wave64 ballot + per-wave LDS staging,
+//               one global atomic per ~450 queue entries.                        (wf_pt_cpu.cpp:94-248)
 //   k_shadow  : any-hit traversal of the shadow tasks, adds unoccluded light. (Light.cpp:16-40)
 //   k_accum   : per-pixel sum of the wave's samples in accumulation order.  (GLRenderer.cpp:411-413)
 //   k_resolve : mean -> ACES -> gamma 1/2.2 -> clamp -> 8-bit truncation.   (GLRenderer.cpp:416-431)
@@ -19,6 +19,14 @@
 #include <hip/hip_runtime.h>
 
 #include "sptr_internal.h"
+
+// Occupancy hints (min waves per SIMD); 1 = let the register allocator decide.
+#ifndef SPTR_TRACE_WAVES
+#define SPTR_TRACE_WAVES 7  // measured: 7 -> +6% on C2 (SGPR-limited to 6 otherwise)
+#endif
+#ifndef SPTR_SHADE_WAVES
+#define SPTR_SHADE_WAVES 1
+#endif
 
 namespace sptr {
 
@@ -38,41 +46,43 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-// LDS-staged queue append.  Lanes append into a block-local LDS buffer (one LDS atomic per wave);
-// the block flushes the buffer to the global queue with ONE global atomic once it holds more than
-// kStageCap - kBlock entries.  A single global counter takes ~88 returning atomics/us on MI355X,
-// so per-wave global appends serialise; per-~2K-entry flushes do not.
-constexpr uint32_t kStageCap = 2048;
+// LDS-staged queue append, per wave.  Each wave appends into its own LDS slice (ballot + popcount,
+// count kept in a wave-uniform register) and flushes the slice to the global queue with ONE global
+// atomic once it holds more than kWaveCap - 64 entries.  A single global counter takes ~88 returning
+// atomics/us on MI355X, so per-wave global appends serialise; per-~450-entry flushes do not, and
+// no block-wide barrier is needed (waves of a block never wait for each other's traversal).
+constexpr uint32_t kWaveCap = 512;
+constexpr uint32_t kWavesPerBlock = kBlock / 64;
 struct alignas(16) Stage {  // 16-B multiple: keeps the dynamic-LDS base aligned (Guideline 17)
-  uint32_t buf[kStageCap];
-  uint32_t n;
-  uint32_t base;
-  uint32_t pad[2];
+  uint32_t buf[kWavesPerBlock][kWaveCap];
 };
 static_assert(sizeof(Stage) % 16 == 0, "Stage must be a 16-byte multiple");
-__device__ __forceinline__ void stage_push(Stage& st, bool pred, uint32_t val) {
+struct WaveQueue {
+  uint32_t* buf;  // this wave's LDS slice
+  uint32_t n;     // entries staged (wave-uniform)
+};
+__device__ __forceinline__ WaveQueue wave_queue(Stage& st) {
+  return WaveQueue{st.buf[threadIdx.x >> 6], 0u};
+}
+__device__ __forceinline__ void wq_flush(WaveQueue& wq, uint32_t* gq, uint32_t* gcnt) {
+  if (wq.n == 0u) return;
+  const uint32_t lane = lane_id();
+  uint32_t b = 0u;
+  if (lane == 0u) b = atomicAdd(gcnt, wq.n);
+  b = __shfl(b, 0);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < wq.n; i += 64u) gq[b + i] = wq.buf[i];
+  __builtin_amdgcn_wave_barrier();
+  wq.n = 0u;
+}
+// All lanes of the wave call this together.
+__device__ __forceinline__ void wq_push(WaveQueue& wq, bool pred, uint32_t val, uint32_t* gq, uint32_t* gcnt) {
   const unsigned long long m = __ballot(pred);
   if (m == 0ull) return;
   const uint32_t lane = lane_id();
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  uint32_t base = 0u;
-  if ((int)lane == leader) base = atomicAdd(&st.n, (uint32_t)__popcll(m));
-  base = __shfl(base, leader);
-  if (pred) st.buf[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = val;
-}
-// Block-uniform call.  Flushes when nearly full, or whenever `force` and non-empty.
-__device__ __forceinline__ void stage_flush(Stage& st, uint32_t* gq, uint32_t* gcnt, bool force) {
-  __syncthreads();
-  const uint32_t n = st.n;
-  if (n > kStageCap - kBlock || (force && n > 0u)) {
-    if (threadIdx.x == 0) st.base = atomicAdd(gcnt, n);
-    __syncthreads();
-    const uint32_t b = st.base;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gq[b + i] = st.buf[i];
-    __syncthreads();
-    if (threadIdx.x == 0) st.n = 0u;
-    __syncthreads();
-  }
+  if (pred) wq.buf[wq.n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = val;
+  wq.n += (uint32_t)__popcll(m);
+  if (wq.n > kWaveCap - 64u) wq_flush(wq, gq, gcnt);
 }
 // Contiguous per-block slice [lo, hi) of n items, whole multiples of the block size.
 __device__ __forceinline__ void block_slice(uint32_t n, uint32_t& lo, uint32_t& hi) {
@@ -91,7 +101,8 @@ __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim
 __device__ __forceinline__ bool local_pixel(const FrameView& f, uint32_t l, int& x, int& y) {
   const uint32_t lt = l >> 10, w = l & 1023u;
   const uint32_t t = lt * (uint32_t)f.G + (uint32_t)f.R;
-  const int tx = (int)(t % (uint32_t)f.ntx), ty = (int)(t / (uint32_t)f.ntx);
+  const uint32_t tyu = fast_div(f.div_ntx, t);
+  const int tx = (int)(t - tyu * (uint32_t)f.ntx), ty = (int)tyu;
   x = tx * kTile + (int)(w & 31u);
   y = ty * kTile + (int)(w >> 5);
   return x < f.W && y < f.H;
@@ -113,25 +124,28 @@ __device__ __forceinline__ Ray make_ray(vec3 o, vec3 d) {
   Ray r;
   r.o = o;
   r.d = d;
+  // v_rcp_f32 (1 ulp): the inverse direction only feeds the conservative box test
   const float eps = 1e-20f;
-  const float ix = 1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x));
-  const float iy = 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y));
-  const float iz = 1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z));
-  r.inv = v3(ix, iy, iz);
-  r.oinv = v3(o.x * ix, o.y * iy, o.z * iz);
+  r.inv = v3(__builtin_amdgcn_rcpf(fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
+             __builtin_amdgcn_rcpf(fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+             __builtin_amdgcn_rcpf(fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+  r.oinv = v3(0.0f, 0.0f, 0.0f);
   return r;
 }
 
-// Slab test of one child box; conservative by a few ulps (only prunes, never decides a hit).
+// Slab test of one child box.  (b - o) * inv avoids the cancellation of the fma(b, inv, -o*inv)
+// form near the origin; the exit distance is padded by 2^-20 relative (~8 ulp) to absorb the
+// subtraction, product and v_rcp rounding, so the test only prunes and never rejects a box that
+// the exact test would accept at a primitive's hit distance.
 __device__ __forceinline__ bool slab(float xlo, float xhi, float ylo, float yhi, float zlo, float zhi, const Ray& r,
                                      float tnear, float tfar, float& tent) {
-  const float tx0 = __builtin_fmaf(xlo, r.inv.x, -r.oinv.x), tx1 = __builtin_fmaf(xhi, r.inv.x, -r.oinv.x);
-  const float ty0 = __builtin_fmaf(ylo, r.inv.y, -r.oinv.y), ty1 = __builtin_fmaf(yhi, r.inv.y, -r.oinv.y);
-  const float tz0 = __builtin_fmaf(zlo, r.inv.z, -r.oinv.z), tz1 = __builtin_fmaf(zhi, r.inv.z, -r.oinv.z);
+  const float tx0 = (xlo - r.o.x) * r.inv.x, tx1 = (xhi - r.o.x) * r.inv.x;
+  const float ty0 = (ylo - r.o.y) * r.inv.y, ty1 = (yhi - r.o.y) * r.inv.y;
+  const float tz0 = (zlo - r.o.z) * r.inv.z, tz1 = (zhi - r.o.z) * r.inv.z;
   const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tnear));
   const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tfar));
   tent = tmin;
-  return tmin <= tmax * 1.0000003f;
+  return tmin <= tmax * 1.00000095f;
 }
 
 __device__ __forceinline__ float e_dot(vec3 a, vec3 b) {
@@ -197,42 +211,48 @@ struct Visits {
   uint32_t nodes = 0, tris = 0, sph = 0;
 };
 
-// Leaf primitive test.  Closest: updates tfar/ref, returns hit.  Any-hit: returns occlusion.
+// Leaf = contiguous range of sorted primitive references (LBVH subtrees cover contiguous ranges):
+// every primitive of the range is tested in a uniform loop.  Closest: updates tfar/ref.  Any-hit:
+// returns on the first occluder.
 template <bool kAny, bool kCount>
-__device__ __forceinline__ bool leaf_test(uint32_t link, const float4* tris, const float4* sph, const Ray& r,
-                                          float tnear, float& tfar, uint32_t& ref, Visits& vc) {
-  const uint32_t idx = link & kIndexMask;
-  float t;
-  if (link & kSphereBit) {
-    if (kCount) ++vc.sph;
-    const float4 s = sph[idx];
-    if (kAny) return sphere_occ(s, r, tnear, tfar);
-    if (sphere_hit(s, r, tnear, tfar, t)) {
-      tfar = t;
-      ref = link & ~kLeafBit;
-      return true;
+__device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                          const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc) {
+  const uint32_t start = (link & ~kLeafBit) >> kLeafCountBits, cnt = (link & kLeafCountMask) + 1u;
+  bool hit = false;
+  for (uint32_t j = 0; j < cnt; ++j) {
+    const uint32_t pr = prim_ref[start + j];
+    const uint32_t idx = pr & kIndexMask;
+    float t;
+    if (pr & kSphereBit) {
+      if (kCount) ++vc.sph;
+      const float4 s = sph[idx];
+      if (kAny) {
+        if (sphere_occ(s, r, tnear, tfar)) return true;
+      } else if (sphere_hit(s, r, tnear, tfar, t)) {
+        tfar = t;
+        ref = pr;
+        hit = true;
+      }
+    } else {
+      if (kCount) ++vc.tris;
+      if (tri_hit(tris, idx, r, tnear, tfar, t)) {
+        if (kAny) return true;
+        tfar = t;
+        ref = pr;
+        hit = true;
+      }
     }
-    return false;
   }
-  if (kCount) ++vc.tris;
-  if (tri_hit(tris, idx, r, tnear, tfar, t)) {
-    if (kAny) return true;
-    tfar = t;
-    ref = link & ~kLeafBit;
-    return true;
-  }
-  return false;
+  return hit;
 }
 
 // BVH2 stack traversal: nearest child first; leaf children are tested as soon as their box is hit.
 template <bool kAny, bool kCount>
-__device__ __forceinline__ bool traverse(const BvhNode* nodes, const float4* tris, const float4* sph, uint32_t root,
-                                         const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc) {
+__device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* prim_ref, const float4* tris,
+                                         const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
+                                         uint32_t& ref, Visits& vc) {
   if (root == kNoHit) return false;
-  if (root & kLeafBit) {
-    const bool h = leaf_test<kAny, kCount>(root, tris, sph, r, tnear, tfar, ref, vc);
-    return h;
-  }
+  if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
   uint32_t stack[kStack];
   int sp = 0;
   uint32_t cur = root;
@@ -247,14 +267,14 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const float4* tri
     bool hr = slab(rxy.x, rxy.y, rxy.z, rxy.w, z.z, z.w, r, tnear, tfar, tr);
     uint32_t L = ln.x, R = ln.y;
     if (hl && (L & kLeafBit)) {
-      if (leaf_test<kAny, kCount>(L, tris, sph, r, tnear, tfar, ref, vc)) {
+      if (leaf_test<kAny, kCount>(L, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
         hit = true;
         if (kAny) return true;
       }
       hl = false;
     }
     if (hr && (R & kLeafBit)) {
-      if (leaf_test<kAny, kCount>(R, tris, sph, r, tnear, tfar, ref, vc)) {
+      if (leaf_test<kAny, kCount>(R, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
         hit = true;
         if (kAny) return true;
       }
@@ -283,22 +303,27 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const float4* tri
 // Stage the whole scene (nodes, triangles, spheres) into LDS when it fits (SceneView::lds_bytes).
 struct Staged {
   const BvhNode* nodes;
+  const uint32_t* prim_ref;
   const float4* tris;
   const float4* sph;
 };
 template <bool kLds>
 __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) {
-  Staged s{sv.nodes, sv.tris, sv.sph};
+  Staged s{sv.nodes, sv.prim_ref, sv.tris, sv.sph};
   if (kLds) {
     const uint32_t nn = sv.num_nodes * 4u, nt = sv.num_tris * 3u, ns = sv.num_sph;
+    const uint32_t np = (sv.num_tris + sv.num_sph + 3u) / 4u;  // prim refs, in float4 units
     const float4* gn = reinterpret_cast<const float4*>(sv.nodes);
+    const float4* gp = reinterpret_cast<const float4*>(sv.prim_ref);
     for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = gn[i];
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = sv.tris[i];
     for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) lds[nn + nt + i] = sv.sph[i];
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[nn + nt + ns + i] = gp[i];
     __syncthreads();
     s.nodes = reinterpret_cast<const BvhNode*>(lds);
     s.tris = lds + nn;
     s.sph = lds + nn + nt;
+    s.prim_ref = reinterpret_cast<const uint32_t*>(lds + nn + nt + ns);
   }
   return s;
 }
@@ -325,7 +350,7 @@ struct Primary {
   uint32_t rng;
 };
 __device__ __forceinline__ bool primary_path(const FrameView& f, uint32_t p, Primary& out) {
-  const uint32_t s = p / f.P, l = p - s * f.P;
+  const uint32_t s = fast_div(f.div_P, p), l = p - s * f.P;
   int x, y;
   if (!local_pixel(f, l, x, y)) return false;
   const uint32_t acc = f.acc0 + s;
@@ -340,6 +365,20 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, uint32_t p, Pri
 }
 
 // --------------------------------------------------------------------------------- shading math
+// Integer powers of x in [0,1] (the reference's pow(sun_dot, 64/8) and the Fresnel pow(.., 5)):
+// squaring chain in double, rounded once to float.  x^2 is exact in double; every later product
+// carries <= 2^-53 relative error, so the float result equals the correctly rounded pow except
+// when the exact value lies within ~6*2^-53 of a rounding midpoint (probability ~1e-8).
+__device__ __forceinline__ void pow8_64(float x, float& p8, float& p64) {
+  const double s = (double)x, s2 = s * s, s4 = s2 * s2, s8 = s4 * s4, s16 = s8 * s8, s32 = s16 * s16;
+  p8 = (float)s8;
+  p64 = (float)(s32 * s32);
+}
+__device__ __forceinline__ float pow5(float x) {
+  const double s = (double)x, s2 = s * s;
+  return (float)((s2 * s2) * s);
+}
+
 // EnvironmentManager::getSkyColor
 __device__ __forceinline__ vec3 sky_color(vec3 d) {
   float t = 0.5f * (d.y + 1.0f);
@@ -350,8 +389,10 @@ __device__ __forceinline__ vec3 sky_color(vec3 d) {
   vec3 c = mix(v3(0.7f, 0.8f, 0.9f), v3(0.2f, 0.4f, 0.8f), t);
   const vec3 sd = normalize(v3(0.3f, 0.6f, -0.8f));
   const float sdot = fmax_g(dot(d, sd), 0.0f);
-  const float si = powf(sdot, 64.0f);
-  const float sg = powf(sdot, 8.0f) * 0.3f;
+  float p8, p64;
+  pow8_64(sdot, p8, p64);
+  const float si = p64;
+  const float sg = p8 * 0.3f;
   c = c + v3(1.0f, 0.9f, 0.7f) * (si + sg);
   return c * 0.8f;
 }
@@ -361,7 +402,7 @@ __device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, i
   const float4 t = env[((size_t)face * S + y) * S + x];
   return v3(t.x, t.y, t.z);
 }
-__device__ vec3 env_color(const ShadeView& sh, vec3 dir) {
+__device__ vec3 env_color(const EnvView& sh, vec3 dir) {
   if (!sh.env) return sky_color(dir);
   const vec3 d = normalize(dir);
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
@@ -419,7 +460,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
   float f0d = (m.ior - 1.0f) / (m.ior + 1.0f);
   f0d *= f0d;
   const vec3 F0 = mix(v3(f0d, f0d, f0d), albedo, m.metallic);
-  const float pw = powf(clamp_g(1.0f - HdotV, 0.0f, 1.0f), 5.0f);
+  const float pw = pow5(clamp_g(1.0f - HdotV, 0.0f, 1.0f));
   const vec3 F = F0 + (1.0f - F0) * pw;
   const vec3 numer = (D * G) * F;
   const float denom = 4.0f * NdotV * NdotL + 0.0001f;
@@ -434,12 +475,11 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // term (wf_pt_cpu.cpp:98-103) is added in place, so only hits are compacted into the shade queue.
 // kPrimary: bounce 0, one thread per path slot, camera ray computed in place (no queue, no state).
 template <bool kLds, bool kCount, bool kPrimary>
-__global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES) k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth) {
   extern __shared__ float4 lds[];
   __shared__ Stage st_hit;
-  if (threadIdx.x == 0) st_hit.n = 0u;
+  WaveQueue wq_hit = wave_queue(st_hit);
   const Staged sc = stage_scene<kLds>(sv, lds);
-  __syncthreads();
   const uint32_t n = kPrimary ? f.P * f.k : w.cnt[kCntLive + depth];
   if (kPrimary && blockIdx.x == 0 && threadIdx.x == 0) w.cnt[kCntLive] = f.valid * f.k;
   const uint32_t* q = w.q[depth & 1];
@@ -468,7 +508,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, ShadeView sh, Fr
       const Ray r = make_ray(o, d);
       float tfar = __builtin_huge_valf();
       uint32_t ref = kNoHit;
-      hit = traverse<false, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
+      hit = traverse<false, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
       if (hit) {
         w.hit[p] = make_uint2(__float_as_uint(tfar), ref);
       } else if (sh.debug_mode == 1) {
@@ -484,10 +524,9 @@ __global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, ShadeView sh, Fr
         w.rad[p] = f4(rv, 0.0f);
       }
     }
-    stage_push(st_hit, hit, p);
-    stage_flush(st_hit, w.qh, &w.cnt[kCntHit + depth], false);
+    wq_push(wq_hit, hit, p, w.qh, &w.cnt[kCntHit + depth]);
   }
-  stage_flush(st_hit, w.qh, &w.cnt[kCntHit + depth], true);
+  wq_flush(wq_hit, w.qh, &w.cnt[kCntHit + depth]);
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
@@ -498,17 +537,14 @@ __global__ void __launch_bounds__(kBlock) k_trace(SceneView sv, ShadeView sh, Fr
 // — the direction slot exists only when a point light is present (directional lights take the
 // constant direction from the light table).
 template <bool kPrimary>
-__global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES) k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
   __shared__ DevMaterial smat[32];
   __shared__ Stage st_next, st_shadow;
   const uint32_t nm = sh.num_mats < 32u ? sh.num_mats : 32u;
   for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
     reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
-  if (threadIdx.x == 0) {
-    st_next.n = 0u;
-    st_shadow.n = 0u;
-  }
   __syncthreads();
+  WaveQueue wq_next = wave_queue(st_next), wq_shadow = wave_queue(st_shadow);
 
   const uint32_t n = w.cnt[kCntHit + depth];
   const uint32_t* q = w.qh;
@@ -679,13 +715,11 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneView sv, ShadeView sh, Fr
       }
       if (dirty) w.rad[p] = f4(radv, 0.0f);
     }
-    stage_push(st_next, cont, p);
-    stage_push(st_shadow, shadow, p);
-    stage_flush(st_next, qn, &w.cnt[kCntLive + depth + 1], false);
-    stage_flush(st_shadow, w.sq, &w.cnt[kCntShadow + depth], false);
+    wq_push(wq_next, cont, p, qn, &w.cnt[kCntLive + depth + 1]);
+    wq_push(wq_shadow, shadow, p, w.sq, &w.cnt[kCntShadow + depth]);
   }
-  stage_flush(st_next, qn, &w.cnt[kCntLive + depth + 1], true);
-  stage_flush(st_shadow, w.sq, &w.cnt[kCntShadow + depth], true);
+  wq_flush(wq_next, qn, &w.cnt[kCntLive + depth + 1]);
+  wq_flush(wq_shadow, w.sq, &w.cnt[kCntShadow + depth]);
 }
 
 // --------------------------------------------------------------------------------- k_shadow
@@ -712,7 +746,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
       const Ray r = make_ray(xyz(a), dir);
       float tfar = a.w;
       uint32_t ref = kNoHit;
-      const bool occ = traverse<true, kCount>(sc.nodes, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
+      const bool occ = traverse<true, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
         any = true;
@@ -775,9 +809,9 @@ __global__ void __launch_bounds__(kBlock) k_unpack(const uint32_t* g, int G, uin
   const uint32_t N = (uint32_t)W * (uint32_t)H;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += grid_threads()) {
     const int x = (int)(i % (uint32_t)W), y = (int)(i / (uint32_t)W);
-    const uint32_t t = (uint32_t)(y / kTile) * (uint32_t)ntx + (uint32_t)(x / kTile);
-    const uint32_t r = t % (uint32_t)G, lt = t / (uint32_t)G;
-    const uint32_t px = g[((size_t)r * tpr + lt) * kTilePixels + (uint32_t)(y % kTile) * kTile + (uint32_t)(x % kTile)];
+    uint32_t r, l;
+    pixel_shard(W, G, x, y, r, l);
+    const uint32_t px = g[(size_t)r * tpr * kTilePixels + l];
     rgb[(size_t)i * 3 + 0] = (uint8_t)(px & 0xFF);
     rgb[(size_t)i * 3 + 1] = (uint8_t)((px >> 8) & 0xFF);
     rgb[(size_t)i * 3 + 2] = (uint8_t)((px >> 16) & 0xFF);
@@ -795,10 +829,10 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
     float tfar = rr[7];
     uint32_t ref = kNoHit;
     if (anyhit) {
-      occ[i] = traverse<true, false>(sv.nodes, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc) ? 1 : 0;
+      occ[i] = traverse<true, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc) ? 1 : 0;
       continue;
     }
-    const bool hit = traverse<false, false>(sv.nodes, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc);
+    const bool hit = traverse<false, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc);
     // report (type bit | original primitive index) so the host can map to (geomID, primID)
     ref_out[i] = hit ? ((ref & kSphereBit) | ((ref & kSphereBit) ? sph_orig[ref & kIndexMask] : tri_orig[ref & kIndexMask]))
                      : kNoHit;
@@ -846,6 +880,35 @@ static inline unsigned grid_for(uint64_t work) {
   return (unsigned)(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
 }
 
+// Persistent-style grid for the queue kernels: exactly the blocks that are resident at once
+// (CUs x occupancy), so every block of the contiguous-slice schedule runs in the first and only
+// round (a grid of 8 blocks/CU where registers admit 7 would run a 1/7-occupancy tail round).
+struct GridCache {
+  const void* fn = nullptr;
+  uint32_t lds = 0;
+  unsigned blocks = 0;
+};
+static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
+  static GridCache cache[32];
+  static int cus = 0;
+  for (GridCache& g : cache)
+    if (g.fn == fn && g.lds == lds_bytes) return g.blocks;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds_bytes) != hipSuccess || per <= 0) per = 4;
+  const unsigned blocks = (unsigned)(cus * per);
+  for (GridCache& g : cache)
+    if (g.fn == nullptr) {
+      g = GridCache{fn, lds_bytes, blocks};
+      break;
+    }
+  return blocks;
+}
+
 SceneView scene_view(const Context& c) {
   SceneView s;
   s.nodes = static_cast<const BvhNode*>(c.nodes.p);
@@ -857,16 +920,21 @@ SceneView scene_view(const Context& c) {
   s.num_tris = c.num_tris;
   s.num_sph = c.num_sph;
   s.root = c.root;
-  const uint64_t bytes = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16;
+  s.prim_ref = static_cast<const uint32_t*>(c.prim_ref.p);
+  const uint64_t bytes = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
+                         ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
   return s;
 }
 
 void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
                   hipStream_t s) {
-  const dim3 g(grid_for(1ull << 22)), b(kBlock);
+  const dim3 b(kBlock);
   const uint32_t lb = sv.lds_bytes;
-#define SPTR_TRACE(L, C, P) hipLaunchKernelGGL((k_trace<L, C, P>), g, b, L ? lb : 0u, s, sv, sh, f, w, depth)
+  const EnvView ev = sh.env;
+#define SPTR_TRACE(L, C, P)                                                                          \
+  hipLaunchKernelGGL((k_trace<L, C, P>), dim3(resident_grid((const void*)&k_trace<L, C, P>, L ? lb : 0u)), b, \
+                     L ? lb : 0u, s, sv, ev, f, w, depth)
   if (depth == 0) {
     if (lb) { if (count) SPTR_TRACE(true, true, true); else SPTR_TRACE(true, false, true); }
     else    { if (count) SPTR_TRACE(false, true, true); else SPTR_TRACE(false, false, true); }
@@ -879,19 +947,23 @@ void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
 
 void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s) {
-  if (depth == 0) hipLaunchKernelGGL(k_shade<true>, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
-  else hipLaunchKernelGGL(k_shade<false>, dim3(grid_for(1ull << 22)), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+  if (depth == 0)
+    hipLaunchKernelGGL(k_shade<true>, dim3(resident_grid((const void*)&k_shade<true>, 0)), dim3(kBlock), 0, s, sv, sh, f,
+                       w, depth);
+  else
+    hipLaunchKernelGGL(k_shade<false>, dim3(resident_grid((const void*)&k_shade<false>, 0)), dim3(kBlock), 0, s, sv, sh,
+                       f, w, depth);
 }
 
 void launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, hipStream_t s) {
-  const dim3 g(grid_for(1ull << 22)), b(kBlock);
-  if (sv.lds_bytes) {
-    if (count) hipLaunchKernelGGL((k_shadow<true, true>), g, b, sv.lds_bytes, s, sv, sh, w, depth);
-    else hipLaunchKernelGGL((k_shadow<true, false>), g, b, sv.lds_bytes, s, sv, sh, w, depth);
-  } else {
-    if (count) hipLaunchKernelGGL((k_shadow<false, true>), g, b, 0, s, sv, sh, w, depth);
-    else hipLaunchKernelGGL((k_shadow<false, false>), g, b, 0, s, sv, sh, w, depth);
-  }
+  const dim3 b(kBlock);
+  const uint32_t lb = sv.lds_bytes;
+#define SPTR_SHADOW(L, C)                                                                           \
+  hipLaunchKernelGGL((k_shadow<L, C>), dim3(resident_grid((const void*)&k_shadow<L, C>, L ? lb : 0u)), b, \
+                     L ? lb : 0u, s, sv, sh, w, depth)
+  if (lb) { if (count) SPTR_SHADOW(true, true); else SPTR_SHADOW(true, false); }
+  else    { if (count) SPTR_SHADOW(false, true); else SPTR_SHADOW(false, false); }
+#undef SPTR_SHADOW
 }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,

@@ -71,22 +71,14 @@ int resolve_geom_materials(Context& c) {
   return SPTR_OK;
 }
 
-// tile-packed local pixel -> image coordinates (host twin of the kernels' local_pixel)
 inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
-  const int ntx = (c.W + kTile - 1) / kTile;
-  const uint32_t lt = l >> 10, w = l & 1023u;
-  const uint32_t t = lt * (uint32_t)c.G + (uint32_t)c.R;
-  x = (int)(t % (uint32_t)ntx) * kTile + (int)(w & 31u);
-  y = (int)(t / (uint32_t)ntx) * kTile + (int)(w >> 5);
-  return x < c.W && y < c.H;
+  return shard_pixel(c.W, c.H, c.G, c.R, l, x, y);
 }
 
 int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
   resized = false;
   if (c.W == W && c.H == H && c.G == G && c.R == R && c.accum.p) return SPTR_OK;
-  const int ntx = (W + kTile - 1) / kTile, nty = (H + kTile - 1) / kTile;
-  const int ntiles = ntx * nty;
-  const uint32_t local_tiles = (uint32_t)((ntiles - R + G - 1) / G);
+  const uint32_t local_tiles = shard_tiles(W, H, G, R);
   c.W = W;
   c.H = H;
   c.G = G;
@@ -154,6 +146,8 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.k = 1;
   v.acc0 = f.frame_begin;
   v.max_depth = f.max_depth;
+  v.div_P = make_fastdiv(c.P ? c.P : 1u);
+  v.div_ntx = make_fastdiv((uint32_t)v.ntx);
   v.valid = 0;
   {
     const int ntx = (c.W + kTile - 1) / kTile;
@@ -180,10 +174,11 @@ ShadeView shade_view(const Context& c) {
   s.geom_mat = static_cast<const uint32_t*>(c.geom_mat.p);
   s.num_lights = (uint32_t)c.lights_host.size();
   for (uint32_t i = 0; i < s.num_lights; ++i) s.lights[i] = c.lights_host[i];
-  s.env = static_cast<const float4*>(c.env.p);
-  s.env_size = c.env_size;
-  s.env_intensity = c.env_intensity;
-  s.env_clamp = c.env_clamp;
+  s.env.env = static_cast<const float4*>(c.env.p);
+  s.env.env_size = c.env_size;
+  s.env.env_intensity = c.env_intensity;
+  s.env.env_clamp = c.env_clamp;
+  s.env.debug_mode = c.debug_mode;
   s.debug_mode = c.debug_mode;
   return s;
 }
@@ -258,7 +253,7 @@ int sptr_destroy(sptr_ctx* x) {
   Context& c = x->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  DevBuf* bufs[] = {&c.nodes, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig, &c.sph_orig, &c.geom_mat,
+  DevBuf* bufs[] = {&c.nodes, &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig, &c.sph_orig, &c.geom_mat,
                     &c.mats,  &c.env,   &c.w_o,   &c.w_d,      &c.w_thr,    &c.w_rad,    &c.w_hit,    &c.w_q0,
                     &c.w_q1,  &c.w_qh, &c.w_sq,  &c.w_stask, &c.w_cnt,  &c.w_tot,    &c.accum,    &c.tiles,    &c.image,
                     &c.qbuf};
@@ -277,9 +272,16 @@ int sptr_set_debug_mode(sptr_ctx* x, int mode) {
   return SPTR_OK;
 }
 
+int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (n < 1 || n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 1..8");
+  x->c.leaf_size = n;
+  return SPTR_OK;
+}
+
 int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
   if (!x) return SPTR_ERR_INVALID;
-  if (max_paths > (1ull << 31)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^31");
+  if (max_paths > (1ull << 30)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^30");
   x->c.wave_paths = max_paths;
   return SPTR_OK;
 }

@@ -15,12 +15,18 @@
 
 #include "sptr_hip.h"
 #include "sptr_math.h"
+#include "tile_map.h"
 
 namespace sptr {
 
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kIndexMask = 0x3FFFFFFFu;
+// Leaf link: kLeafBit | start << kLeafCountBits | (count - 1): a contiguous range of up to 8 sorted
+// primitive references (prim_ref[start .. start+count)).  Primitive ref: [kSphereBit] | slot.
+constexpr uint32_t kLeafCountBits = 3;
+constexpr uint32_t kLeafCountMask = (1u << kLeafCountBits) - 1u;
+constexpr uint32_t kMaxLeafSize = 1u << kLeafCountBits;
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kTile = 32;
 constexpr int kTilePixels = kTile * kTile;
@@ -30,8 +36,7 @@ constexpr int kStack = 64;
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;  // scenes up to this size are staged whole into LDS
 
-// BVH2 node, 64 B: both child boxes + child links.  Link: internal node index, or
-// kLeafBit | [kSphereBit] | sorted primitive slot.
+// BVH2 node, 64 B: both child boxes + child links.  Link: internal node index, or a leaf range.
 struct BvhNode {
   float4 lxy;  // left  lo.x hi.x lo.y hi.y
   float4 rxy;  // right lo.x hi.x lo.y hi.y
@@ -60,6 +65,7 @@ struct DevLight {  // host-precomputed per Light::getRadiance (Light.cpp:43-79)
 
 struct SceneView {
   const BvhNode* nodes;
+  const uint32_t* prim_ref;  // sorted primitive refs (leaf ranges index this)
   const float4* tris;  // 3 float4 per sorted triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z Ng.xyz
   const float4* sph;   // sorted spheres: c.xyz r
   const uint32_t* tri_geom;  // geomID per sorted triangle
@@ -68,20 +74,26 @@ struct SceneView {
   uint32_t lds_bytes;  // 0: traverse from global memory
 };
 
-struct ShadeView {
-  const DevMaterial* mats;
-  uint32_t num_mats;
-  const uint32_t* geom_mat;  // geomID -> material index, resolved as MaterialManager::getMaterialFromHit
-  uint32_t num_lights;
-  DevLight lights[kMaxLights];
+struct EnvView {
   const float4* env;  // 6*S*S texels (rgb, -) or null for the procedural sky
   int32_t env_size;
   float env_intensity, env_clamp;
   int32_t debug_mode;
 };
 
+struct ShadeView {
+  const DevMaterial* mats;
+  uint32_t num_mats;
+  const uint32_t* geom_mat;  // geomID -> material index, resolved as MaterialManager::getMaterialFromHit
+  uint32_t num_lights;
+  DevLight lights[kMaxLights];
+  EnvView env;
+  int32_t debug_mode;
+};
+
 struct FrameView {
   int32_t W, H, ntx, G, R;
+  FastDiv div_P, div_ntx;
   uint32_t P;   // local pixels (local tiles * 1024)
   uint32_t k;   // samples in this wave
   uint32_t acc0;  // accumulation index of sample slot 0
@@ -129,7 +141,8 @@ struct Context {
   int debug_mode = 0;
   uint64_t wave_paths = 0;  // 0 = default
   // scene
-  DevBuf nodes, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
+  DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
+  uint32_t leaf_size = 4;  // max primitives per BVH leaf range (1..8)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_tri_geoms = 0;
   std::vector<uint32_t> geom_first;     // host copy for primID derivation

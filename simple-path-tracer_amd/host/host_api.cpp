@@ -5,6 +5,7 @@
 #include <cstring>
 #include <string>
 
+#include "../csrc/tile_map.h"
 #include "scene_desc.h"
 #include "shading.h"
 
@@ -76,6 +77,37 @@ int sptr_host_default_lights(sptr_light* out, int capacity) {
 int sptr_host_equirect_to_faces(const float* rgb, int32_t w, int32_t h, int32_t size, float* faces) {
   if (!rgb || !faces || w <= 0 || h <= 0 || size < 2) return SPTR_ERR_INVALID;
   EquirectToFaces(rgb, w, h, size, faces);
+  return SPTR_OK;
+}
+
+int sptr_host_pack_tiles(const uint8_t* rgb, int32_t W, int32_t H, int32_t G, int32_t R, uint32_t* tiles) {
+  if (!rgb || !tiles || W <= 0 || H <= 0 || G <= 0 || R < 0 || R >= G) return SPTR_ERR_INVALID;
+  const uint32_t n = sptr::shard_tiles(W, H, G, R) * 1024u;
+  for (uint32_t l = 0; l < n; ++l) {
+    int x, y;
+    if (!sptr::shard_pixel(W, H, G, R, l, x, y)) {
+      tiles[l] = 0u;
+      continue;
+    }
+    const uint8_t* p = rgb + ((size_t)y * W + x) * 3;
+    tiles[l] = uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | 0xFF000000u;
+  }
+  return SPTR_OK;
+}
+
+int sptr_host_unpack_tiles(const uint32_t* g, int32_t G, uint32_t tpr, int32_t W, int32_t H, uint8_t* rgb) {
+  if (!g || !rgb || W <= 0 || H <= 0 || G <= 0) return SPTR_ERR_INVALID;
+  if ((uint64_t)tpr * (uint64_t)G < (uint64_t)sptr::tiles_total(W, H)) return SPTR_ERR_INVALID;
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      uint32_t r, l;
+      sptr::pixel_shard(W, G, x, y, r, l);
+      const uint32_t px = g[(size_t)r * tpr * 1024u + l];
+      uint8_t* o = rgb + ((size_t)y * W + x) * 3;
+      o[0] = uint8_t(px & 0xFF);
+      o[1] = uint8_t((px >> 8) & 0xFF);
+      o[2] = uint8_t((px >> 16) & 0xFF);
+    }
   return SPTR_OK;
 }
 

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsptr_hip.so")
+LIB_PATH = os.environ.get("SPTR_LIB") or os.path.join(HERE, "libsptr_hip.so")  # SPTR_LIB: A/B builds
 
 SPTR_FRAME_TIMING = 1
 SPTR_FRAME_NO_RESOLVE = 2
@@ -83,12 +83,12 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_render", "sptr_read_rgb8", "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
     "sptr_host_builtin_scene", "sptr_host_scene_view", "sptr_host_scene_free", "sptr_host_camera_lookat",
     "sptr_host_preset_materials", "sptr_host_default_lights", "sptr_host_equirect_to_faces",
-    "sptr_host_load_hdr", "sptr_host_free",
+    "sptr_host_pack_tiles", "sptr_host_unpack_tiles", "sptr_host_load_hdr", "sptr_host_free",
 ]
 
 
@@ -109,6 +109,7 @@ def lib() -> C.CDLL:
         "sptr_last_error": (C.c_char_p, [vp]),
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
+        "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
         "sptr_set_materials": (C.c_int, [vp, C.POINTER(Material), u32]),
         "sptr_set_lights": (C.c_int, [vp, C.POINTER(Light), u32]),
@@ -129,6 +130,8 @@ def lib() -> C.CDLL:
         "sptr_host_preset_materials": (C.c_int, [C.c_int, C.POINTER(Material), C.c_int]),
         "sptr_host_default_lights": (C.c_int, [C.POINTER(Light), C.c_int]),
         "sptr_host_equirect_to_faces": (C.c_int, [fp, i32, i32, i32, fp]),
+        "sptr_host_pack_tiles": (C.c_int, [bp, i32, i32, i32, i32, up]),
+        "sptr_host_unpack_tiles": (C.c_int, [up, i32, u32, i32, i32, bp]),
         "sptr_host_load_hdr": (C.c_int, [C.c_char_p, C.POINTER(fp), C.POINTER(i32), C.POINTER(i32)]),
         "sptr_host_free": (None, [vp]),
     }
@@ -259,6 +262,31 @@ def equirect_to_faces(rgb: np.ndarray, size: int = 512) -> np.ndarray:
     return faces
 
 
+def tiles_per_rank(width: int, height: int, shard_count: int) -> int:
+    ntiles = ((width + 31) // 32) * ((height + 31) // 32)
+    return (ntiles + shard_count - 1) // shard_count
+
+
+def pack_tiles(rgb: np.ndarray, shard_count: int, shard_rank: int) -> np.ndarray:
+    """Host twin of the device tile packing: this shard's pixels as RGBA8 words, tile-packed and
+    padded to tiles_per_rank tiles (the all-gather send buffer)."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    out = np.zeros(tiles_per_rank(w, h, shard_count) * 1024, np.uint32)
+    if lib().sptr_host_pack_tiles(_b(rgb), w, h, shard_count, shard_rank, _u(out)) != 0:
+        raise SptrError("pack_tiles failed")
+    return out
+
+
+def unpack_tiles(gathered: np.ndarray, shard_count: int, width: int, height: int) -> np.ndarray:
+    g = np.ascontiguousarray(gathered, np.uint32)
+    out = np.zeros((height, width, 3), np.uint8)
+    if lib().sptr_host_unpack_tiles(_u(g), shard_count, tiles_per_rank(width, height, shard_count), width, height,
+                                    _b(out)) != 0:
+        raise SptrError("unpack_tiles failed")
+    return out
+
+
 def load_hdr(path: str) -> np.ndarray:
     L = lib()
     p = C.POINTER(C.c_float)()
@@ -331,6 +359,9 @@ class Renderer:
 
     def set_wave_paths(self, n: int):
         self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
+
+    def set_leaf_size(self, n: int):
+        self._check(self._L.sptr_set_leaf_size(self._h, n), "set_leaf_size")
 
     def set_debug_mode(self, m: int):
         self._check(self._L.sptr_set_debug_mode(self._h, m), "set_debug_mode")

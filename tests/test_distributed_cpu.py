@@ -1,0 +1,63 @@
+"""CPU, world_size 2 over gloo: the multi-GPU data path of bench.py / DESIGN.md §Multi-GPU.
+
+Each rank renders its interleaved 32x32 tiles (oracle stands in for the GPU render here — this is a
+test of sharding + packing + the one all-gather + unpack, not of the renderer), packs them with the
+product's sptr_host_pack_tiles, all-gathers, and unpacks with sptr_host_unpack_tiles.  The gathered
+image must equal a single-rank render bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W, H, SPP = 100, 70, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, os.path.join(ROOT, "simple-path-tracer_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import sptr
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P = oracle.Prepared(oracle.builtin_scene("default"), bvh=True)
+    cam = oracle.camera(aspect=W / H)
+    _, rgb, cnt = P.render(cam, W, H, oracle.preset_materials(False), oracle.default_lights(), frames=SPP,
+                           shard_rank=rank, shard_count=world, threads=2)
+    tiles = sptr.pack_tiles(rgb, world, rank)
+    tpr = sptr.tiles_per_rank(W, H, world)
+    assert tiles.size == tpr * 1024
+    gathered = torch.zeros(world * tiles.size, dtype=torch.int32)
+    dist.all_gather_into_tensor(gathered, torch.from_numpy(tiles.view(np.int32)))
+    rays = torch.tensor([cnt["rays_closest"] + cnt["rays_shadow"]], dtype=torch.float64)
+    dist.all_reduce(rays)
+    if rank == 0:
+        img = sptr.unpack_tiles(gathered.numpy().view(np.uint32), world, W, H)
+        np.save(os.path.join(out_dir, "img.npy"), img)
+        np.save(os.path.join(out_dir, "rays.npy"), rays.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_tile_gather(tmp_path):
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    P = oracle.Prepared(oracle.builtin_scene("default"), bvh=True)
+    _, full, cnt = P.render(oracle.camera(aspect=W / H), W, H, oracle.preset_materials(False),
+                            oracle.default_lights(), frames=SPP, threads=4)
+    assert np.array_equal(np.load(tmp_path / "img.npy"), full)
+    # rays are partitioned, not duplicated: the sum over ranks equals the single-rank count
+    assert float(np.load(tmp_path / "rays.npy")[0]) == cnt["rays_closest"] + cnt["rays_shadow"]

@@ -234,3 +234,21 @@ def test_debug_mode_hit_miss(renderer):
     g, _, _, _ = _oracle_scene("default").intersect(rays)
     hit = (g != 0xFFFFFFFF).reshape(H, W)
     assert ((acc[..., 0] == 1.0) == hit).mean() >= 0.999
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 8])
+def test_leaf_size_invariance(renderer, leaf):
+    """BVH leaf-range size only changes traversal work, never the image (default leaf size 4)."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, "default_emitter")
+    renderer.render(cam, W, H, spp=3)
+    ref_acc = renderer.read_accum().copy()
+    renderer.set_leaf_size(leaf)
+    try:
+        sptr.setup_default(renderer, "default_emitter")
+        renderer.render(cam, W, H, spp=3)
+        acc = renderer.read_accum()
+    finally:
+        renderer.set_leaf_size(4)
+    assert np.array_equal(acc.view(np.uint32), ref_acc.view(np.uint32))
