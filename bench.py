@@ -1,33 +1,40 @@
 #!/usr/bin/env python3
-"""Benchmark: Mrays/s (+ Msamples/s) of the MI355X wavefront path tracer on BASELINE config C2.
+"""Benchmark: Mrays/s (+ Msamples/s) of the MI355X wavefront path tracer.
 
-Workload (BASELINE.json configs[1]): default scene + emissive sphere (diffuse, metal, dielectric and
-emissive materials), 1920x1080, 64 spp, max depth 6, procedural sky, one directional sun; inputs
-synthetic (the reference's own procedural scene — no datasets).  One "step" = one complete 64-spp
-render of the frame: every rank renders its interleaved 32x32 tiles, resolves them, and the
-resolved RGBA8 tiles are all-gathered over RCCL and unpacked into the 1920x1080 RGB8 image.
+Default workload = BASELINE.json configs[1] (C2): default scene + emissive sphere (diffuse, metal,
+dielectric and emissive materials), 1920x1080, 64 spp, max depth 6, procedural sky, one sun.
+Inputs are synthetic (the reference's own procedural scene; no datasets).  --workload c1|c3|c4|c5
+selects the other configurations (simple-path-tracer_amd/workloads.py); c5 is the HBM roofline run.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU, RCCL backend)
+One "step" = one complete render of the frame at the workload's spp: every rank renders its
+interleaved 32x32 tiles and resolves them; the resolved RGBA8 tiles are all-gathered over RCCL and
+rank 0 unpacks them into the W x H RGB8 image.
 
-value = all ranks' rays (closest-hit + any-hit queries) / max-over-ranks wall time of K steps.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+value = all ranks' rays (closest-hit + any-hit queries, = the reference's rtcIntersect1 +
+rtcOccluded1 calls) / max-over-ranks wall time of the K timed steps.  Work per rank shrinks as N
+grows (fixed frame), so scaling is "strong".
 """
 import argparse
+import glob
 import json
 import os
 import sys
 import time
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "simple-path-tracer_amd"))
 import sptr  # noqa: E402
+import workloads  # noqa: E402
 
-W, H, SPP, DEPTH, SCENE = 1920, 1080, 64, 6, "default_emitter"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+STREAM_BYTES_PER_RAY = 36.0  # path id 4 + origin 12 + dir 12 in, t 4 + prim 4 out
+CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 8, "c4": 4, "c5": 1}
 
 
 class _DevArray:
@@ -38,25 +45,63 @@ class _DevArray:
                                          "version": 3}
 
 
-def trace_bytes(st, rays):
-    """B_ray = 28 (path id + origin + dir) + 8 (t + prim id) + 64*nodes + 48*tris + 16*spheres."""
-    return 36.0 * rays + 64.0 * st.node_visits + 48.0 * st.tri_tests + 16.0 * st.sphere_tests
+def roofline(cnt, stats, layout, wl_name, steps):
+    """Roofline of the dominant kernel, k_trace (all bounces; one template).
+
+    Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 + 64 n_node + 48 n_tri + 16 n_sph with the
+    visit counts taken from an instrumented pass over the same rays.  When the scene is staged in
+    LDS (lds_bytes > 0), node and primitive fetches never reach HBM, so the HBM-algorithmic bytes
+    are the 36-byte ray stream only; the full B_ray figure is reported beside it."""
+    launches = sum(s.trace_launches for s in stats)
+    avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
+    launches_per_step = max(1, launches // max(1, steps))
+    stream = STREAM_BYTES_PER_RAY * cnt.rays_closest
+    scene = 64.0 * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
+    lds = layout["lds_bytes"] > 0
+    hbm_alg = stream + (0.0 if lds else scene)
+    per_launch = hbm_alg / launches_per_step
+    achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic, src = None, None
+    # latest round's PMC pass (tools/gpu_profile.sh): FETCH_SIZE x2 + WRITE_SIZE per k_trace launch
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{wl_name}_trace.json")))
+    if found:
+        pmc = found[-1]
+        with open(pmc) as f:
+            d = json.load(f)
+        traffic, src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
+    return {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+            "launches_per_step": launches_per_step,
+            "scene_in_lds": lds,
+            "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
+            "per_ray": {"nodes": round(cnt.node_visits / max(1, cnt.rays_closest), 3),
+                        "tris": round(cnt.tri_tests / max(1, cnt.rays_closest), 3),
+                        "spheres": round(cnt.sphere_tests / max(1, cnt.rays_closest), 3)}}
 
 
-def cpu_baseline(cam):
+def cpu_baseline(wl, flat, cam):
+    """The oracle (C++ restatement of the reference's CPU wavefront integrator, Embree semantics with
+    its own median-split BVH) on the host cores, on the same scene and camera: a reported baseline."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # test infrastructure, used only as the timed CPU baseline
+    import oracle  # test infrastructure, used here only as the timed CPU baseline
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    P = oracle.Prepared(oracle.builtin_scene(SCENE), bvh=True)
+    spp = min(wl.spp, CPU_SAMPLE_SPP.get(wl.name, 1))
+    scene = {k: getattr(flat, k) for k in ("positions", "indices", "tri_geom_first", "spheres", "geom_material")}
     t0 = time.perf_counter()
-    _, _, cnt = P.render(cam.as_array(), W, H, oracle.preset_materials(True), oracle.default_lights(),
-                         frames=SPP, max_depth=DEPTH, threads=threads)
+    P = oracle.Prepared(scene, bvh=True)
+    t_build = time.perf_counter() - t0
+    faces = workloads.hdr_env_faces() if wl.hdr_env else None
+    t0 = time.perf_counter()
+    _, _, cnt = P.render(cam.as_array(), wl.width, wl.height, oracle.preset_materials(wl.scene == "default_emitter"),
+                         oracle.default_lights(), frames=spp, max_depth=wl.max_depth, threads=threads, env_faces=faces)
     dt = time.perf_counter() - t0
     rays = cnt["rays_closest"] + cnt["rays_shadow"]
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"full workload: {W}x{H} x {SPP} spp, {rays} rays in {dt:.2f} s "
-                      f"(oracle C++ restatement + median-split BVH, std::thread over 32x32 tiles)",
+            "sample": f"{wl.width}x{wl.height} x {spp} spp of {wl.spp} ({'full workload' if spp == wl.spp else 'first spp'})"
+                      f", {rays} rays in {dt:.2f} s (+{t_build:.2f} s BVH build); oracle/wf_oracle.cpp with a"
+                      f" median-split BVH, std::thread over 32x32 tiles",
             "msamples_per_s": round(cnt["samples"] / dt / 1e6, 3)}
 
 
@@ -65,10 +110,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c2", choices=sorted(workloads.WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
     args = ap.parse_args()
+    wl = workloads.WORKLOADS[args.workload]
+    W, H = wl.width, wl.height
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -84,16 +132,16 @@ def main():
         r.set_wave_paths(args.wave_paths)
     if args.leaf_size:
         r.set_leaf_size(args.leaf_size)
-    sptr.setup_default(r, SCENE)
-    cam = sptr.camera_lookat(aspect=W / H)
-    ntx, nty = (W + 31) // 32, (H + 31) // 32
-    tiles_per_rank = (ntx * nty + world - 1) // world
+    flat = workloads.setup(r, wl)
+    layout, info = r.scene_layout(), r.scene_info()
+    cam = workloads.camera(wl)
+    tiles_per_rank = sptr.tiles_per_rank(W, H, world)
     send = torch.zeros(tiles_per_rank * 1024, dtype=torch.int32, device=dev)
     gathered = torch.zeros(world * tiles_per_rank * 1024, dtype=torch.int32, device=dev)
     image = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev)
 
     def step(flags=0):
-        st = r.render(cam, W, H, spp=SPP, max_depth=DEPTH, shard_rank=rank, shard_count=world, flags=flags)
+        st = r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=rank, shard_count=world, flags=flags)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
         send[: local_tiles.numel()].copy_(local_tiles)
@@ -132,20 +180,8 @@ def main():
         elapsed, rays, samples = float(tmax[0]), float(tsum[1]), float(tsum[2])
 
     if rank == 0:
-        ms_trace = sum(s.ms_trace for s in stats)
-        launches = sum(s.trace_launches for s in stats)
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / len(stats), 3)
-                    for k in ("raygen", "trace", "shade", "shadow", "accum")}
-        # per-launch algorithmic bytes of the trace kernel (counted pass scaled to the timed steps)
-        bytes_step = trace_bytes(cnt, cnt.rays_closest)
-        avg_launch_s = (ms_trace / launches) * 1e-3
-        bytes_launch = bytes_step / max(1, cnt.trace_launches or (launches / len(stats)))
-        achieved = bytes_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "trace_pmc_bytes.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                    for k in ("trace", "shade", "shadow", "accum")}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),
@@ -159,22 +195,19 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (reference's procedural default scene + emissive sphere; no datasets)",
-            "config": {"workload": f"C2: default scene + emitter, {W}x{H}, {SPP} spp, depth {DEPTH}",
-                       "scene": SCENE, "width": W, "height": H, "spp": SPP, "max_depth": DEPTH,
+            "data": "synthetic (the reference's procedural scenes; no datasets)",
+            "config": {"workload": wl.description, "scene": os.path.basename(wl.scene), "width": W, "height": H,
+                       "spp": wl.spp, "max_depth": wl.max_depth,
                        "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL all-gather"},
-            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_launch": round(bytes_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
-                         "note": "algorithmic bytes per SURVEY 8(d); BVH/prims of this scene are LDS-staged"},
+            "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
             "stage_ms_per_step": stage_ms,
             "rays_per_step": int(rays / args.steps),
-            "visits": {"node": cnt.node_visits, "tri": cnt.tri_tests, "sphere": cnt.sphere_tests,
-                       "closest_rays": cnt.rays_closest},
+            "scene": {"prims": info["prims"], "nodes": info["nodes"], "bvh_depth": info["depth"],
+                      "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"]},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cam)
+            line["cpu_baseline"] = cpu_baseline(wl, flat, cam)
         print(json.dumps(line), flush=True)
     r.close()
     if distributed:

@@ -153,6 +153,13 @@ int sptr_set_lights(sptr_ctx* ctx, const sptr_light* lights, uint32_t count);
 int sptr_set_environment(sptr_ctx* ctx, const sptr_environment* env);
 int sptr_scene_info(const sptr_ctx* ctx, uint32_t* num_prims, uint32_t* num_nodes, uint32_t* bvh_depth,
                     double* build_ms);
+/* Device layout of the uploaded scene (DESIGN.md "Data layout in HBM"). lds_bytes = bytes staged into
+ * LDS per block by the trace/shadow kernels, 0 when the scene is traversed from HBM/L2. */
+typedef struct sptr_scene_layout {
+  uint32_t num_tris, num_spheres, num_nodes, leaf_size, bvh_depth, lds_bytes;
+  uint64_t node_bytes, tri_bytes, sphere_bytes, prim_ref_bytes;
+} sptr_scene_layout;
+int sptr_scene_layout_info(const sptr_ctx* ctx, sptr_scene_layout* out);
 
 /* ---- rendering ---------------------------------------------------------------------------------- */
 /* Renders on the context's stream, or on `stream` (a hipStream_t) when not NULL; returns after the

@@ -324,6 +324,23 @@ int sptr_scene_info(const sptr_ctx* x, uint32_t* num_prims, uint32_t* num_nodes,
   return SPTR_OK;
 }
 
+int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
+  if (!x || !out) return SPTR_ERR_INVALID;
+  const Context& c = x->c;
+  const SceneView sv = scene_view(c);
+  out->num_tris = c.num_tris;
+  out->num_spheres = c.num_sph;
+  out->num_nodes = c.num_nodes;
+  out->leaf_size = c.leaf_size;
+  out->bvh_depth = c.bvh_depth;
+  out->lds_bytes = sv.lds_bytes;
+  out->node_bytes = (uint64_t)c.num_nodes * sizeof(BvhNode);
+  out->tri_bytes = (uint64_t)c.num_tris * 48u;
+  out->sphere_bytes = (uint64_t)c.num_sph * 16u;
+  out->prim_ref_bytes = ((uint64_t)c.num_tris + c.num_sph) * 4u;
+  return SPTR_OK;
+}
+
 int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
   if (!x || (n && !m)) return SPTR_ERR_INVALID;
   Context& c = x->c;

@@ -78,13 +78,24 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class SceneLayout(C.Structure):
+    _fields_ = [("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_nodes", C.c_uint32),
+                ("leaf_size", C.c_uint32), ("bvh_depth", C.c_uint32), ("lds_bytes", C.c_uint32),
+                ("node_bytes", C.c_uint64), ("tri_bytes", C.c_uint64), ("sphere_bytes", C.c_uint64),
+                ("prim_ref_bytes", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _lib = None
 
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
     "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
-    "sptr_set_environment", "sptr_scene_info", "sptr_render", "sptr_read_rgb8", "sptr_read_accum",
+    "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_read_rgb8",
+    "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
     "sptr_host_builtin_scene", "sptr_host_scene_view", "sptr_host_scene_free", "sptr_host_camera_lookat",
     "sptr_host_preset_materials", "sptr_host_default_lights", "sptr_host_equirect_to_faces",
@@ -115,6 +126,7 @@ def lib() -> C.CDLL:
         "sptr_set_lights": (C.c_int, [vp, C.POINTER(Light), u32]),
         "sptr_set_environment": (C.c_int, [vp, C.POINTER(Environment)]),
         "sptr_scene_info": (C.c_int, [vp, up, up, up, C.POINTER(C.c_double)]),
+        "sptr_scene_layout_info": (C.c_int, [vp, C.POINTER(SceneLayout)]),
         "sptr_render": (C.c_int, [vp, C.POINTER(Frame), vp, C.POINTER(Stats)]),
         "sptr_read_rgb8": (C.c_int, [vp, bp]),
         "sptr_read_accum": (C.c_int, [vp, fp]),
@@ -338,6 +350,11 @@ class Renderer:
         ms = C.c_double()
         self._check(self._L.sptr_scene_info(self._h, C.byref(n), C.byref(nn), C.byref(dep), C.byref(ms)), "info")
         return {"prims": n.value, "nodes": nn.value, "depth": dep.value, "build_ms": ms.value}
+
+    def scene_layout(self) -> dict:
+        lay = SceneLayout()
+        self._check(self._L.sptr_scene_layout_info(self._h, C.byref(lay)), "scene_layout")
+        return lay.as_dict()
 
     def set_materials(self, mats):
         arr = (Material * len(mats))(*mats)
