@@ -33,62 +33,77 @@ namespace sptr {
 // --------------------------------------------------------------------------------- small helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-// Wave-aggregated queue append: one atomic per wave; lanes keep their relative order.
-// Must be reached by all active lanes of the wave together.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+// Block-local dense append: one LDS atomic per wave; the lanes' outputs land contiguously in the
+// block's segment.  Every lane of the wave must call it together (it ballots).
+__device__ __forceinline__ uint32_t block_append(uint32_t* s_cnt, bool pred) {
   const unsigned long long m = __ballot(pred);
   if (m == 0ull) return 0u;
   const uint32_t lane = lane_id();
   const int leader = __ffsll((unsigned long long)m) - 1;
   uint32_t base = 0u;
-  if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  if ((int)lane == leader) base = atomicAdd(s_cnt, (uint32_t)__popcll(m));
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
-
-// LDS-staged queue append, per wave.  Each wave appends into its own LDS slice (ballot + popcount,
-// count kept in a wave-uniform register) and flushes the slice to the global queue with ONE global
-// atomic once it holds more than kWaveCap - 64 entries.  A single global counter takes ~88 returning
-// atomics/us on MI355X, so per-wave global appends serialise; per-~450-entry flushes do not, and
-// no block-wide barrier is needed (waves of a block never wait for each other's traversal).
-constexpr uint32_t kWaveCap = 512;
-constexpr uint32_t kWavesPerBlock = kBlock / 64;
-struct alignas(16) Stage {  // 16-B multiple: keeps the dynamic-LDS base aligned (Guideline 17)
-  uint32_t buf[kWavesPerBlock][kWaveCap];
-};
-static_assert(sizeof(Stage) % 16 == 0, "Stage must be a 16-byte multiple");
-struct WaveQueue {
-  uint32_t* buf;  // this wave's LDS slice
-  uint32_t n;     // entries staged (wave-uniform)
-};
-__device__ __forceinline__ WaveQueue wave_queue(Stage& st) {
-  return WaveQueue{st.buf[threadIdx.x >> 6], 0u};
-}
-__device__ __forceinline__ void wq_flush(WaveQueue& wq, uint32_t* gq, uint32_t* gcnt) {
-  if (wq.n == 0u) return;
-  const uint32_t lane = lane_id();
-  uint32_t b = 0u;
-  if (lane == 0u) b = atomicAdd(gcnt, wq.n);
-  b = __shfl(b, 0);
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t i = lane; i < wq.n; i += 64u) gq[b + i] = wq.buf[i];
-  __builtin_amdgcn_wave_barrier();
-  wq.n = 0u;
-}
-// All lanes of the wave call this together.
-__device__ __forceinline__ void wq_push(WaveQueue& wq, bool pred, uint32_t val, uint32_t* gq, uint32_t* gcnt) {
-  const unsigned long long m = __ballot(pred);
-  if (m == 0ull) return;
-  const uint32_t lane = lane_id();
-  if (pred) wq.buf[wq.n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = val;
-  wq.n += (uint32_t)__popcll(m);
-  if (wq.n > kWaveCap - 64u) wq_flush(wq, gq, gcnt);
-}
-// Contiguous per-block slice [lo, hi) of n items, whole multiples of the block size.
-__device__ __forceinline__ void block_slice(uint32_t n, uint32_t& lo, uint32_t& hi) {
-  const uint32_t per = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+// Contiguous per-block slice [lo, hi) of n items, whole multiples of the block size; per = slice
+// length of every block (the segment stride of this kernel's outputs).
+__device__ __forceinline__ void block_slice(uint32_t n, uint32_t& lo, uint32_t& hi, uint32_t& per) {
+  per = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
   lo = min(n, blockIdx.x * per);
   hi = min(n, lo + per);
+}
+
+// Consumer prologue: exclusive scan of the producer's per-block segment counts into LDS
+// (s_off[0..nseg]); returns the total.  Contains block barriers: call from every thread.
+__device__ uint32_t seg_scan(const SegTable& t, uint32_t nseg, uint32_t* s_off, uint32_t& per) {
+  __shared__ uint32_t s_wave[kBlock / 64];
+  const uint32_t chunk = (nseg + kBlock - 1) / kBlock;
+  const uint32_t b0 = threadIdx.x * chunk;
+  uint32_t sum = 0u;
+  for (uint32_t j = 0; j < chunk; ++j)
+    if (b0 + j < nseg) sum += t.cnt[b0 + j];
+  uint32_t incl = sum;
+  const uint32_t lane = lane_id();
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off);
+    if (lane >= (uint32_t)off) incl += v;
+  }
+  if (lane == 63u) s_wave[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += s_wave[w];
+  for (uint32_t j = 0; j < chunk; ++j)
+    if (b0 + j < nseg) {
+      s_off[b0 + j] = run;
+      run += t.cnt[b0 + j];
+    }
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0u;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) tot += s_wave[w];
+    s_off[nseg] = tot;
+  }
+  per = *t.per;
+  __syncthreads();
+  return s_off[nseg];
+}
+// Compacted index i -> physical slot: the largest segment b with s_off[b] <= i (a fixed 11-step
+// search over LDS; empty segments are skipped because the largest such b is the non-empty one).
+__device__ __forceinline__ uint32_t seg_slot(const uint32_t* s_off, uint32_t nseg, uint32_t per, uint32_t i) {
+  uint32_t b = 0u;
+#pragma unroll
+  for (uint32_t step = kMaxSegs / 2; step; step >>= 1) {
+    const uint32_t c = b + step;
+    if (c < nseg && s_off[c] <= i) b = c;
+  }
+  return b * per + (i - s_off[b]);
+}
+// Producer epilogue: publish this block's output count (and, from block 0, the segment stride).
+__device__ __forceinline__ void seg_publish(const SegTable& t, const uint32_t* s_cnt, uint32_t per) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    t.cnt[blockIdx.x] = *s_cnt;
+    if (blockIdx.x == 0) *t.per = per;
+  }
 }
 
 __device__ __forceinline__ vec3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
@@ -471,126 +486,134 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 }
 
 // --------------------------------------------------------------------------------- k_trace
-// Closest hit for every path queued at this bounce.  A miss ends the path here: the environment
-// term (wf_pt_cpu.cpp:98-103) is added in place, so only hits are compacted into the shade queue.
-// kPrimary: bounce 0, one thread per path slot, camera ray computed in place (no queue, no state).
+// Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
+// (wf_pt_cpu.cpp:98-103) is added to rad[p] in place, so only hits go on to k_shade, as dense hit
+// records in this block's segment.  kPrimary: bounce 0, one thread per path slot, camera ray
+// computed in place (no input stream at all).  Input of later bounces: the dense ray stream
+// rs[depth&1] written by the previous k_shade, addressed through its segment table.
 template <bool kLds, bool kCount, bool kPrimary>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES) k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
+    k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
   extern __shared__ float4 lds[];
-  __shared__ Stage st_hit;
-  WaveQueue wq_hit = wave_queue(st_hit);
+  __shared__ uint32_t s_cnt;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
+  if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
-  const uint32_t n = kPrimary ? f.P * f.k : w.cnt[kCntLive + depth];
-  if (kPrimary && blockIdx.x == 0 && threadIdx.x == 0) w.cnt[kCntLive] = f.valid * f.k;
-  const uint32_t* q = w.q[depth & 1];
+  uint32_t n, per_in = 0u;
+  if (kPrimary) {
+    n = f.P * f.k;
+    __syncthreads();
+  } else {
+    n = seg_scan(w.segN, nseg_in, s_off, per_in);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+  const RayStream rs = w.rs[depth & 1];
   Visits vc;
-  uint32_t lo, hi;
-  block_slice(n, lo, hi);
+  uint32_t lo, hi, per;
+  block_slice(n, lo, hi, per);
   for (uint32_t base = lo; base < hi; base += kBlock) {
     const uint32_t i = base + threadIdx.x;
     bool active = i < hi, hit = false;
-    uint32_t p = 0;
+    uint32_t id = 0u, pid = 0u, ref = kNoHit;
+    float tfar = __builtin_huge_valf();
     vec3 o, d;
     if (active) {
       if (kPrimary) {
         Primary pr;
-        p = i;
-        active = primary_path(f, p, pr);
+        id = pid = i;
+        active = primary_path(f, i, pr);
         o = f.cam_pos;
         d = pr.d;
       } else {
-        p = q[i];
-        o = xyz(w.o[p]);
-        d = xyz(w.d[p]);
+        id = seg_slot(s_off, nseg_in, per_in, i);
+        const float4 o4 = rs.o[id], d4 = rs.d[id];
+        o = xyz(o4);
+        d = xyz(d4);
+        pid = __float_as_uint(d4.w);
       }
     }
     if (active) {
       const Ray r = make_ray(o, d);
-      float tfar = __builtin_huge_valf();
-      uint32_t ref = kNoHit;
       hit = traverse<false, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
-      if (hit) {
-        w.hit[p] = make_uint2(__float_as_uint(tfar), ref);
-      } else if (sh.debug_mode == 1) {
-        w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      } else {
-        const vec3 e = env_color(sh, safe_normalize(d));
-        vec3 rv;
-        if (kPrimary) {
-          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+      if (!hit) {
+        if (sh.debug_mode == 1) {
+          w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          rv = xyz(w.rad[p]) + xyz(w.thr[p]) * e;
+          const vec3 e = env_color(sh, safe_normalize(d));
+          vec3 rv;
+          if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+          else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
+          w.rad[pid] = f4(rv, 0.0f);
         }
-        w.rad[p] = f4(rv, 0.0f);
       }
     }
-    wq_push(wq_hit, hit, p, w.qh, &w.cnt[kCntHit + depth]);
+    const uint32_t j = block_append(&s_cnt, hit);
+    if (hit) w.hrec[lo + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
   }
-  wq_flush(wq_hit, w.qh, &w.cnt[kCntHit + depth]);
+  seg_publish(w.segH, &s_cnt, per);
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
 // --------------------------------------------------------------------------------- k_shade
-// One thread per path that hit something at this bounce (misses were finished by k_trace).  Radiance is read lazily (only when something is
+// One thread per hit record of this bounce.  Radiance is read lazily (only when something is
 // added) and written back once; bounce 0 starts from zero radiance and unit throughput in
-// registers.  Shadow task per (path, light): {origin.xyz, tfar} {contrib.xyz, valid} [{dir.xyz}]
-// — the direction slot exists only when a point light is present (directional lights take the
-// constant direction from the light table).
+// registers.  Outputs, each dense in this block's segment: the continuation rays (rs[(d+1)&1]) and
+// one shadow record per path with >= 1 lit light: L tasks {origin.xyz, tfar} {contrib.xyz, p}
+// [{dir.xyz}] (valid = contrib slot w != 0 is encoded by p+1; the direction slot exists only when a
+// point light is present).
 template <bool kPrimary>
-__global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES) k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
+    k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
+  extern __shared__ uint32_t s_off[];
   __shared__ DevMaterial smat[32];
-  __shared__ Stage st_next, st_shadow;
+  __shared__ uint32_t s_cnt_n, s_cnt_s;
   const uint32_t nm = sh.num_mats < 32u ? sh.num_mats : 32u;
   for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
     reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
-  __syncthreads();
-  WaveQueue wq_next = wave_queue(st_next), wq_shadow = wave_queue(st_shadow);
+  if (threadIdx.x == 0) s_cnt_n = s_cnt_s = 0u;
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segH, nseg_in, s_off, per_in);
 
-  const uint32_t n = w.cnt[kCntHit + depth];
-  const uint32_t* q = w.qh;
-  uint32_t* qn = w.q[(depth + 1) & 1];
+  const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
-  const uint32_t ts = w.tstride;
-  uint32_t lo, hi;
-  block_slice(n, lo, hi);
+  const uint32_t ts = w.tstride, L = w.L;
+  uint32_t lo, hi, per;
+  block_slice(n, lo, hi, per);
   for (uint32_t base = lo; base < hi; base += kBlock) {
     const uint32_t i = base + threadIdx.x;
-    bool cont = false, shadow = false;
-    uint32_t p = 0;
-    bool active = i < hi;
-    vec3 ro, rd, thr;
-    uint32_t rng = 0u;
+    const bool active = i < hi;
+    bool cont = false, shadow = false, dirty = kPrimary;
+    uint32_t p = 0u, rng = 0u;
+    vec3 ro, rd, thr, radv = v3(0.0f, 0.0f, 0.0f), P, nrm, no, nd;
+    DevMaterial m;
     if (active) {
-      p = q[i];
+      const uint4 h = w.hrec[seg_slot(s_off, nseg_in, per_in, i)];
       if (kPrimary) {
         Primary pr;
+        p = h.x;
         primary_path(f, p, pr);
         ro = f.cam_pos;
         rd = pr.d;
         thr = v3(1.0f, 1.0f, 1.0f);
         rng = pr.rng;
       } else {
-        const float4 o4 = w.o[p];
+        const float4 o4 = rin.o[h.x], d4 = rin.d[h.x];
         ro = xyz(o4);
-        rd = xyz(w.d[p]);
-        thr = xyz(w.thr[p]);
+        rd = xyz(d4);
+        thr = xyz(rin.thr[h.x]);
         rng = __float_as_uint(o4.w);
+        p = __float_as_uint(d4.w);
       }
-    }
-    if (active) {
-      const uint2 h = w.hit[p];
-      vec3 radv = v3(0.0f, 0.0f, 0.0f);
-      bool loaded = kPrimary, dirty = kPrimary;
       if (sh.debug_mode == 1) {
         radv = v3(1.0f, 1.0f, 1.0f);
         dirty = true;
       } else {
-        const float t = __uint_as_float(h.x);
-        const vec3 P = ro + t * rd;
-        const uint32_t idx = h.y & kIndexMask;
+        const float t = __uint_as_float(h.y);
+        P = ro + t * rd;
+        const uint32_t idx = h.z & kIndexMask;
         vec3 ng;
         uint32_t mid;
-        if (h.y & kSphereBit) {
+        if (h.z & kSphereBit) {
           const float4 s = sv.sph[idx];
           ng = v3((P.x - s.x) / s.w, (P.y - s.y) / s.w, (P.z - s.z) / s.w);
           mid = sh.geom_mat[sv.sph_geom[idx]];
@@ -599,153 +622,180 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES) k_shade(SceneView sv
           ng = v3(c.y, c.z, c.w);
           mid = sh.geom_mat[sv.tri_geom[idx]];
         }
-        vec3 nrm = safe_normalize(ng);
+        nrm = safe_normalize(ng);
         if (dot(nrm, rd) > 0.0f) nrm = -nrm;
-        const DevMaterial m = (mid < nm) ? smat[mid] : sh.mats[mid];
+        m = (mid < nm) ? smat[mid] : sh.mats[mid];
         const vec3 emission = v3(m.emission[0], m.emission[1], m.emission[2]);
         if (dot(emission, emission) > 0.0f) {
-          if (!loaded) {
-            radv = xyz(w.rad[p]);
-            loaded = true;
-          }
+          if (!kPrimary) radv = xyz(w.rad[p]);
           radv = radv + thr * emission;
           dirty = true;
         }
-        // direct light: shadow tasks carry the precomputed contribution, added if unoccluded
-        {
-          const vec3 view = -rd;
-          for (uint32_t li = 0; li < sh.num_lights; ++li) {
-            const DevLight& L = sh.lights[li];
-            vec3 ldir, Li;
-            float ldist;
-            if (L.type == 0) {
-              ldir = v3(L.v[0], L.v[1], L.v[2]);
-              ldist = __builtin_huge_valf();
-              Li = v3(L.radiance[0], L.radiance[1], L.radiance[2]);
-            } else {
-              const vec3 lv = v3(L.v[0], L.v[1], L.v[2]) - P;
-              ldist = sqrtf(dot(lv, lv));
-              ldir = lv / ldist;
-              const float att = 1.0f + 0.09f * ldist + 0.032f * ldist * ldist;
-              Li = v3(L.radiance[0], L.radiance[1], L.radiance[2]) / att;
-            }
-            const float cs = fmax_g(dot(nrm, ldir), 0.0f);
-            float4* task = w.stask + ((size_t)p * w.L + li) * ts;
-            if (cs <= 0.0f) {
-              task[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-              continue;
-            }
-            const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
-            const vec3 so = P + nrm * eps;
-            const vec3 fr = eval_brdf(m, nrm, view, ldir);
-            const vec3 contrib = thr * (fr * Li * cs);
-            task[0] = f4(so, ldist - 1e-4f);
-            task[1] = f4(contrib, 1.0f);
-            if (ts > 2u) task[2] = f4(ldir, 0.0f);
-            shadow = true;
-          }
-        }
-        // continuation
-        vec3 no, nd;
-        const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
-        if (m.metallic > 0.5f) {
-          no = P + nrm * 1e-4f;
-          nd = safe_normalize(reflect(rd, nrm));
-          thr = thr * (albedo * m.metallic);
-          cont = true;
-        } else if (m.metallic < 0.1f && m.ior > 1.3f) {
-          const float ior = m.ior;
-          const float cosine = -dot(rd, nrm);
-          const float eta = (cosine >= 0.0f) ? (1.0f / ior) : ior;
-          const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
-          float r0 = (1.0f - ior) / (1.0f + ior);
-          r0 = r0 * r0;
-          const float xc = 1.0f - clamp_std(fabsf(cosine), 0.0f, 1.0f);
-          const float F = r0 + (1.0f - r0) * xc * xc * xc * xc * xc;
-          const float xi = rand01(rng);
-          if (xi < F) {
-            no = P + nrm * 1e-4f;
-            nd = safe_normalize(reflect(rd, nrm));
-            thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
+        // any light facing the surface -> this path gets a shadow record
+        for (uint32_t li = 0; li < sh.num_lights; ++li) {
+          const DevLight& Lt = sh.lights[li];
+          vec3 ldir;
+          if (Lt.type == 0) {
+            ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
           } else {
-            const float ci = -dot(nrm, rd);
-            const float kk = 1.0f - eta * eta * (1.0f - ci * ci);
-            vec3 refr = v3(0.0f, 0.0f, 0.0f);
-            if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
-            if (dot(refr, refr) > 0.0f) {
-              no = P - nrm * 1e-4f;
-              nd = safe_normalize(refr);
-              thr = thr * v3(tr, tr, tr);
-            } else {
-              no = P + nrm * 1e-4f;
-              nd = safe_normalize(reflect(rd, nrm));
-            }
+            const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - P;
+            ldir = lv / sqrtf(dot(lv, lv));
           }
-          cont = true;
-        } else {
-          const float r1 = rand01(rng);
-          const float r2 = rand01(rng);
-          const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
-          const float rr = sqrtf(r2);
-          const float lx = rr * cosf(phi), ly = rr * sinf(phi);
-          const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
-          const vec3 nn = safe_normalize(nrm);
-          const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
-                                                 : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
-          const vec3 bt = cross(tg, nn);
-          const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
-          no = P + nrm * 1e-4f;
-          const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
-          const float xi = rand01(rng);
-          cont = true;
-          if ((uint32_t)depth > 2u) {
-            if (xi >= surv) cont = false;
-            else thr = thr * (albedo / fmax_g(surv, 1e-6f));
-          } else {
-            thr = thr * albedo;
-          }
-          nd = safe_normalize(sdir);
-        }
-        cont = cont && !last;
-        if (cont) {
-          w.o[p] = f4(no, __uint_as_float(rng));
-          w.d[p] = f4(nd, 0.0f);
-          w.thr[p] = f4(thr, 0.0f);
+          if (fmax_g(dot(nrm, ldir), 0.0f) > 0.0f) shadow = true;
         }
       }
-      if (dirty) w.rad[p] = f4(radv, 0.0f);
     }
-    wq_push(wq_next, cont, p, qn, &w.cnt[kCntLive + depth + 1]);
-    wq_push(wq_shadow, shadow, p, w.sq, &w.cnt[kCntShadow + depth]);
+    const uint32_t js = block_append(&s_cnt_s, shadow);
+    if (shadow) {
+      // direct light: shadow tasks carry the precomputed contribution, added if unoccluded
+      float4* task = w.stask + (size_t)(lo + js) * L * ts;
+      const vec3 view = -rd;
+      for (uint32_t li = 0; li < L; ++li, task += ts) {
+        const DevLight& Lt = sh.lights[li];
+        vec3 ldir, Li;
+        float ldist;
+        if (Lt.type == 0) {
+          ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
+          ldist = __builtin_huge_valf();
+          Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+        } else {
+          const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - P;
+          ldist = sqrtf(dot(lv, lv));
+          ldir = lv / ldist;
+          const float att = 1.0f + 0.09f * ldist + 0.032f * ldist * ldist;
+          Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]) / att;
+        }
+        const float cs = fmax_g(dot(nrm, ldir), 0.0f);
+        if (cs <= 0.0f) {
+          task[1] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0u));
+          continue;
+        }
+        const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
+        const vec3 so = P + nrm * eps;
+        const vec3 fr = eval_brdf(m, nrm, view, ldir);
+        const vec3 contrib = thr * (fr * Li * cs);
+        task[0] = f4(so, ldist - 1e-4f);
+        task[1] = f4(contrib, __uint_as_float(p + 1u));
+        if (ts > 2u) task[2] = f4(ldir, 0.0f);
+      }
+    }
+    if (active && sh.debug_mode != 1) {
+      // continuation
+      const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+      if (m.metallic > 0.5f) {
+        no = P + nrm * 1e-4f;
+        nd = safe_normalize(reflect(rd, nrm));
+        thr = thr * (albedo * m.metallic);
+        cont = true;
+      } else if (m.metallic < 0.1f && m.ior > 1.3f) {
+        const float ior = m.ior;
+        const float cosine = -dot(rd, nrm);
+        const float eta = (cosine >= 0.0f) ? (1.0f / ior) : ior;
+        const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
+        float r0 = (1.0f - ior) / (1.0f + ior);
+        r0 = r0 * r0;
+        const float xc = 1.0f - clamp_std(fabsf(cosine), 0.0f, 1.0f);
+        const float F = r0 + (1.0f - r0) * xc * xc * xc * xc * xc;
+        const float xi = rand01(rng);
+        if (xi < F) {
+          no = P + nrm * 1e-4f;
+          nd = safe_normalize(reflect(rd, nrm));
+          thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
+        } else {
+          const float ci = -dot(nrm, rd);
+          const float kk = 1.0f - eta * eta * (1.0f - ci * ci);
+          vec3 refr = v3(0.0f, 0.0f, 0.0f);
+          if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
+          if (dot(refr, refr) > 0.0f) {
+            no = P - nrm * 1e-4f;
+            nd = safe_normalize(refr);
+            thr = thr * v3(tr, tr, tr);
+          } else {
+            no = P + nrm * 1e-4f;
+            nd = safe_normalize(reflect(rd, nrm));
+          }
+        }
+        cont = true;
+      } else {
+        const float r1 = rand01(rng);
+        const float r2 = rand01(rng);
+        const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
+        const float rr = sqrtf(r2);
+        const float lx = rr * cosf(phi), ly = rr * sinf(phi);
+        const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
+        const vec3 nn = safe_normalize(nrm);
+        const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
+                                               : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
+        const vec3 bt = cross(tg, nn);
+        const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
+        no = P + nrm * 1e-4f;
+        const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
+        const float xi = rand01(rng);
+        cont = true;
+        if ((uint32_t)depth > 2u) {
+          if (xi >= surv) cont = false;
+          else thr = thr * (albedo / fmax_g(surv, 1e-6f));
+        } else {
+          thr = thr * albedo;
+        }
+        nd = safe_normalize(sdir);
+      }
+      cont = cont && !last;
+    }
+    if (active && dirty) w.rad[p] = f4(radv, 0.0f);
+    const uint32_t jn = block_append(&s_cnt_n, cont);
+    if (cont) {
+      rout.o[lo + jn] = f4(no, __uint_as_float(rng));
+      rout.d[lo + jn] = f4(nd, __uint_as_float(p));
+      rout.thr[lo + jn] = f4(thr, 0.0f);
+    }
   }
-  wq_flush(wq_next, qn, &w.cnt[kCntLive + depth + 1]);
-  wq_flush(wq_shadow, w.sq, &w.cnt[kCntShadow + depth]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    w.segN.cnt[blockIdx.x] = s_cnt_n;
+    w.segS.cnt[blockIdx.x] = s_cnt_s;
+    if (blockIdx.x == 0) {
+      *w.segN.per = per;
+      *w.segS.per = per;
+    }
+  }
 }
 
 // --------------------------------------------------------------------------------- k_shadow
+// One thread per shadow record: any-hit test of each of its light tasks in light order; the
+// unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
+// queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount>
-__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth) {
+__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
   extern __shared__ float4 lds[];
+  __shared__ uint32_t s_rays;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
+  if (threadIdx.x == 0) s_rays = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
-  const uint32_t n = w.cnt[kCntShadow + depth];
-  const uint32_t ts = w.tstride;
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
+  const uint32_t ts = w.tstride, L = w.L;
   Visits vc;
-  uint32_t lo, hi;
-  block_slice(n, lo, hi);
+  uint32_t lo, hi, per, rays = 0u;
+  block_slice(n, lo, hi, per);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-    const uint32_t p = w.sq[i];
+    const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, i) * L * ts;
     bool any = false;
+    uint32_t p = 0u;
     vec3 rv = v3(0.0f, 0.0f, 0.0f);
-    for (uint32_t li = 0; li < w.L; ++li) {
-      const float4* task = w.stask + ((size_t)p * w.L + li) * ts;
+    for (uint32_t li = 0; li < L; ++li, task += ts) {
       const float4 c = task[1];
-      if (c.w == 0.0f) continue;
+      const uint32_t tag = __float_as_uint(c.w);
+      if (tag == 0u) continue;
+      p = tag - 1u;
       const float4 a = task[0];
-      const vec3 dir = (ts > 2u && sh.lights[li].type != 0) ? xyz(task[2])
-                                                             : v3(sh.lights[li].v[0], sh.lights[li].v[1], sh.lights[li].v[2]);
+      const vec3 dir = (ts > 2u && sh.lights[li].type != 0)
+                           ? xyz(task[2])
+                           : v3(sh.lights[li].v[0], sh.lights[li].v[1], sh.lights[li].v[2]);
       const Ray r = make_ray(xyz(a), dir);
       float tfar = a.w;
       uint32_t ref = kNoHit;
+      ++rays;
       const bool occ = traverse<true, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
@@ -755,24 +805,28 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
     }
     if (any) w.rad[p] = f4(rv, 0.0f);
   }
+  for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+  if (lane_id() == 0u) atomicAdd(&s_rays, rays);
+  __syncthreads();
+  if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
   if (kCount) flush_visits(vc, w.tot, kTotShNodes);
 }
 
 // --------------------------------------------------------------------------------- k_accum / resolve
-__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset, int max_depth) {
+__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset) {
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     vec3 a = reset ? v3(0.0f, 0.0f, 0.0f) : xyz(accum[l]);
     for (uint32_t s = 0; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
     accum[l] = f4(a, 0.0f);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    unsigned long long live = 0, sh = 0;
-    for (int d = 0; d < max_depth; ++d) {
-      live += w.cnt[kCntLive + d];
-      sh += w.cnt[kCntShadow + d];
+  if (blockIdx.x == 0) {  // fold the per-block any-hit tallies of this batch into the totals
+    unsigned long long s = 0ull;
+    for (uint32_t b = threadIdx.x; b < kMaxSegs; b += kBlock) {
+      s += w.bstat[b];
+      w.bstat[b] = 0ull;
     }
-    w.tot[kTotClosest] += live;
-    w.tot[kTotShadow] += sh;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane_id() == 0u) atomicAdd(&w.tot[kTotShadow], s);
   }
 }
 
@@ -900,7 +954,8 @@ static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
   }
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds_bytes) != hipSuccess || per <= 0) per = 4;
-  const unsigned blocks = (unsigned)(cus * per);
+  unsigned blocks = (unsigned)(cus * per);
+  if (blocks > kMaxSegs) blocks = kMaxSegs;  // producer grids index the segment tables
   for (GridCache& g : cache)
     if (g.fn == nullptr) {
       g = GridCache{fn, lds_bytes, blocks};
@@ -927,48 +982,67 @@ SceneView scene_view(const Context& c) {
   return s;
 }
 
-void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
-                  hipStream_t s) {
+static unsigned trace_lds(const SceneView& sv, bool lds, bool primary, uint32_t nseg) {
+  return (lds ? sv.lds_bytes : 0u) + (primary ? 0u : (4u * (nseg + 1u) + 15u) / 16u * 16u);
+}
+
+unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                      bool count, uint32_t nseg, hipStream_t s) {
   const dim3 b(kBlock);
-  const uint32_t lb = sv.lds_bytes;
+  const bool L = sv.lds_bytes != 0;
+  const bool P = depth == 0;
+  const unsigned lb = trace_lds(sv, L, P, nseg);
   const EnvView ev = sh.env;
-#define SPTR_TRACE(L, C, P)                                                                          \
-  hipLaunchKernelGGL((k_trace<L, C, P>), dim3(resident_grid((const void*)&k_trace<L, C, P>, L ? lb : 0u)), b, \
-                     L ? lb : 0u, s, sv, ev, f, w, depth)
-  if (depth == 0) {
-    if (lb) { if (count) SPTR_TRACE(true, true, true); else SPTR_TRACE(true, false, true); }
-    else    { if (count) SPTR_TRACE(false, true, true); else SPTR_TRACE(false, false, true); }
+  unsigned g = 0;
+#define SPTR_TRACE(Lc, C, Pc)                                                                       \
+  do {                                                                                              \
+    g = resident_grid((const void*)&k_trace<Lc, C, Pc>, lb);                                        \
+    hipLaunchKernelGGL((k_trace<Lc, C, Pc>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);         \
+  } while (0)
+  if (P) {
+    if (L) { if (count) SPTR_TRACE(true, true, true); else SPTR_TRACE(true, false, true); }
+    else   { if (count) SPTR_TRACE(false, true, true); else SPTR_TRACE(false, false, true); }
   } else {
-    if (lb) { if (count) SPTR_TRACE(true, true, false); else SPTR_TRACE(true, false, false); }
-    else    { if (count) SPTR_TRACE(false, true, false); else SPTR_TRACE(false, false, false); }
+    if (L) { if (count) SPTR_TRACE(true, true, false); else SPTR_TRACE(true, false, false); }
+    else   { if (count) SPTR_TRACE(false, true, false); else SPTR_TRACE(false, false, false); }
   }
 #undef SPTR_TRACE
+  return g;
 }
 
-void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
-                  hipStream_t s) {
-  if (depth == 0)
-    hipLaunchKernelGGL(k_shade<true>, dim3(resident_grid((const void*)&k_shade<true>, 0)), dim3(kBlock), 0, s, sv, sh, f,
-                       w, depth);
-  else
-    hipLaunchKernelGGL(k_shade<false>, dim3(resident_grid((const void*)&k_shade<false>, 0)), dim3(kBlock), 0, s, sv, sh,
-                       f, w, depth);
+unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                      uint32_t nseg, hipStream_t s) {
+  const unsigned lb = (4u * (nseg + 1u) + 15u) / 16u * 16u;
+  unsigned g;
+  if (depth == 0) {
+    g = resident_grid((const void*)&k_shade<true>, lb);
+    hipLaunchKernelGGL(k_shade<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+  } else {
+    g = resident_grid((const void*)&k_shade<false>, lb);
+    hipLaunchKernelGGL(k_shade<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+  }
+  return g;
 }
 
-void launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, hipStream_t s) {
+unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count,
+                       uint32_t nseg, hipStream_t s) {
   const dim3 b(kBlock);
-  const uint32_t lb = sv.lds_bytes;
-#define SPTR_SHADOW(L, C)                                                                           \
-  hipLaunchKernelGGL((k_shadow<L, C>), dim3(resident_grid((const void*)&k_shadow<L, C>, L ? lb : 0u)), b, \
-                     L ? lb : 0u, s, sv, sh, w, depth)
-  if (lb) { if (count) SPTR_SHADOW(true, true); else SPTR_SHADOW(true, false); }
-  else    { if (count) SPTR_SHADOW(false, true); else SPTR_SHADOW(false, false); }
+  const bool L = sv.lds_bytes != 0;
+  const unsigned lb = trace_lds(sv, L, false, nseg);
+  unsigned g = 0;
+#define SPTR_SHADOW(Lc, C)                                                                          \
+  do {                                                                                              \
+    g = resident_grid((const void*)&k_shadow<Lc, C>, lb);                                           \
+    hipLaunchKernelGGL((k_shadow<Lc, C>), dim3(g), b, lb, s, sv, sh, w, depth, nseg);               \
+  } while (0)
+  if (L) { if (count) SPTR_SHADOW(true, true); else SPTR_SHADOW(true, false); }
+  else   { if (count) SPTR_SHADOW(false, true); else SPTR_SHADOW(false, false); }
 #undef SPTR_SHADOW
+  return g;
 }
 
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, reset ? 1 : 0, max_depth);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, hipStream_t s) {
+  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, reset ? 1 : 0);
 }
 
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,

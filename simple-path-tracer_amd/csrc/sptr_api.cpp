@@ -96,42 +96,45 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
   return SPTR_OK;
 }
 
-int ensure_wave(Context& c, uint64_t cap, uint32_t L) {
-  if (c.wave_cap >= cap && c.wave_L >= L && c.w_o.p) return SPTR_OK;
+int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts) {
+  L = L ? L : 1u;
+  if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
   const size_t n = (size_t)cap;
-  API_HIP(ensure_buf(c.w_o, n * 16));
-  API_HIP(ensure_buf(c.w_d, n * 16));
-  API_HIP(ensure_buf(c.w_thr, n * 16));
+  for (auto& b : c.w_rs)
+    for (DevBuf& x : b) API_HIP(ensure_buf(x, n * 16));
+  API_HIP(ensure_buf(c.w_hrec, n * 16));
   API_HIP(ensure_buf(c.w_rad, n * 16));
-  API_HIP(ensure_buf(c.w_hit, n * 8));
-  API_HIP(ensure_buf(c.w_q0, n * 4));
-  API_HIP(ensure_buf(c.w_q1, n * 4));
-  API_HIP(ensure_buf(c.w_qh, n * 4));
-  API_HIP(ensure_buf(c.w_sq, n * 4));
-  API_HIP(ensure_buf(c.w_stask, n * (L ? L : 1) * 48));  // up to 3 float4 per (path, light)
+  API_HIP(ensure_buf(c.w_stask, n * L * ts * 16));
   c.wave_cap = cap;
-  c.wave_L = L ? L : 1;
+  c.wave_L = L;
+  c.wave_ts = ts;
   return SPTR_OK;
+}
+
+uint32_t task_stride(const Context& c) {
+  for (const DevLight& l : c.lights_host)
+    if (l.type != 0) return 3u;
+  return 2u;
 }
 
 WaveView wave_view(Context& c) {
   WaveView w;
-  w.o = static_cast<float4*>(c.w_o.p);
-  w.d = static_cast<float4*>(c.w_d.p);
-  w.thr = static_cast<float4*>(c.w_thr.p);
+  for (int b = 0; b < 2; ++b) {
+    w.rs[b].o = static_cast<float4*>(c.w_rs[b][0].p);
+    w.rs[b].d = static_cast<float4*>(c.w_rs[b][1].p);
+    w.rs[b].thr = static_cast<float4*>(c.w_rs[b][2].p);
+  }
+  w.hrec = static_cast<uint4*>(c.w_hrec.p);
   w.rad = static_cast<float4*>(c.w_rad.p);
-  w.hit = static_cast<uint2*>(c.w_hit.p);
-  w.q[0] = static_cast<uint32_t*>(c.w_q0.p);
-  w.q[1] = static_cast<uint32_t*>(c.w_q1.p);
-  w.qh = static_cast<uint32_t*>(c.w_qh.p);
-  w.sq = static_cast<uint32_t*>(c.w_sq.p);
   w.stask = static_cast<float4*>(c.w_stask.p);
-  w.cnt = static_cast<uint32_t*>(c.w_cnt.p);
+  uint32_t* seg = static_cast<uint32_t*>(c.w_seg.p);  // 3 tables of kMaxSegs counts + 1 stride
+  w.segN = SegTable{seg, seg + kMaxSegs};
+  w.segH = SegTable{seg + (kMaxSegs + 4), seg + (kMaxSegs + 4) + kMaxSegs};
+  w.segS = SegTable{seg + 2 * (kMaxSegs + 4), seg + 2 * (kMaxSegs + 4) + kMaxSegs};
+  w.bstat = reinterpret_cast<unsigned long long*>(seg + 3 * (kMaxSegs + 4));
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
   w.L = (uint32_t)c.lights_host.size();
-  w.tstride = 2u;
-  for (const DevLight& l : c.lights_host)
-    if (l.type != 0) w.tstride = 3u;
+  w.tstride = task_stride(c);
   return w;
 }
 
@@ -240,7 +243,9 @@ int sptr_create(int device, sptr_ctx** out) {
     delete x;
     return SPTR_ERR_HIP;
   }
-  if (ensure_buf(c.w_cnt, kCntWords * 4) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess) {
+  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + kMaxSegs * 8;
+  if (ensure_buf(c.w_seg, seg_bytes) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
+      hipMemset(c.w_seg.p, 0, seg_bytes) != hipSuccess) {
     delete x;
     return SPTR_ERR_OOM;
   }
@@ -253,11 +258,12 @@ int sptr_destroy(sptr_ctx* x) {
   Context& c = x->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  DevBuf* bufs[] = {&c.nodes, &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig, &c.sph_orig, &c.geom_mat,
-                    &c.mats,  &c.env,   &c.w_o,   &c.w_d,      &c.w_thr,    &c.w_rad,    &c.w_hit,    &c.w_q0,
-                    &c.w_q1,  &c.w_qh, &c.w_sq,  &c.w_stask, &c.w_cnt,  &c.w_tot,    &c.accum,    &c.tiles,    &c.image,
-                    &c.qbuf};
+  DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
+                    &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_hrec, &c.w_rad,   &c.w_stask,
+                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf};
   for (DevBuf* b : bufs) free_buf(*b);
+  for (auto& b : c.w_rs)
+    for (DevBuf& x : b) free_buf(x);
   for (hipEvent_t e : c.events) (void)hipEventDestroy(e);
   if (c.stream) (void)hipStreamDestroy(c.stream);
   delete x;
@@ -429,7 +435,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const uint64_t wave_paths = c.wave_paths ? c.wave_paths : kDefaultWavePaths;
   uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
   k = std::min<uint32_t>(k, f->spp);
-  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size());
+  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c));
   if (rc != SPTR_OK) return rc;
 
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
@@ -454,20 +460,22 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
     fv.k = kk;
     fv.acc0 = f->frame_begin + done;
-    API_HIP(hipMemsetAsync(c.w_cnt.p, 0, kCntWords * 4, s));
+    // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
+    // its grid size = the number of segments its consumers scan
+    uint32_t g_shade = 0;
     for (int d = 0; d < D; ++d) {
       tm.begin(1);
-      launch_trace(sv, sh, fv, w, d, count, s);
+      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
       tm.begin(2);
-      launch_shade(sv, sh, fv, w, d, s);
+      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, s);
       tm.end();
       tm.begin(3);
-      launch_shadow(sv, sh, w, d, count, s);
+      launch_shadow(sv, sh, w, d, count, g_shade, s);
       tm.end();
     }
     tm.begin(4);
-    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), reset && done == 0, D, s);
+    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), reset && done == 0, s);
     tm.end();
     API_HIP(hipGetLastError());
     done += kk;

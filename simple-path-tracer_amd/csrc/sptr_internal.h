@@ -1,12 +1,17 @@
 // sptr_internal.h — device data layout and context of libsptr_hip (not part of the public ABI).
 //
-// HBM layout (SoA "float4 streams", one 16-B coalesced load per lane per stream):
-//   path state  : o[p] = (origin.xyz, rng bits)   d[p] = (dir.xyz, -)   thr[p]   rad[p]
-//   hit record  : hit[p] = (t bits, prim ref)      — written by k_trace, read by k_shade
-//   queues      : q0/q1 ping-pong u32 path ids (extension rays), sq u32 path ids (shadow rays)
-//   shadow task : stask[p*L + i] = {origin.xyz, tfar} {dir.xyz, -} {contrib.xyz, valid}
-// Path id p = sample_slot * P + local_pixel; local pixels are tile-packed (32x32 tiles of this
-// shard, row-major inside a tile) so a 64-lane wave covers two rows of one tile.
+// HBM layout: dense SoA "float4 streams", one 16-B coalesced load per lane per stream.
+//   path id      : p = sample_slot * P + local_pixel (local pixels tile-packed: 32x32 tiles of this
+//                  shard, row-major inside a tile, so a wave64 covers two rows of one tile)
+//   rad[p]       : radiance of path p (summed by k_accum in sample order)
+//   ray streams  : rs[b] = {o.xyz|rng, d.xyz|p, thr.xyz} indexed by *queue slot*, ping-pong b = depth&1;
+//                  written densely by k_shade, read densely by k_trace (no sparse gathers)
+//   hit records  : hrec[slot] = (input slot or p, t bits, prim ref), written densely by k_trace
+//   shadow tasks : stask[slot*L + i] = {origin.xyz, tfar} {contrib.xyz, p} [{dir.xyz}]
+// Queues are *block segments*: a producer block that consumed input slice [lo, hi) writes its
+// outputs densely to [lo*m, lo*m + n_b) (m = records per input) and publishes n_b in a segment
+// table; consumers scan the table (one LDS scan per block) and map compacted index -> slot.  No
+// global atomics on the data path, and every stream access is dense.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -103,29 +108,33 @@ struct FrameView {
   float half_w, half_h;
 };
 
-// counters block (u32 unless noted); zeroed per wave
-enum : int {
-  kCntLive = 0,                     // [kMaxDepth+1] extension queue sizes per depth
-  kCntShadow = kCntLive + kMaxDepth + 1,  // [kMaxDepth] shadow queue sizes per depth
-  kCntHit = kCntShadow + kMaxDepth,       // [kMaxDepth] shade (hit) queue sizes per depth
-  kCntWords = kCntHit + kMaxDepth,
-};
+constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
+
 // 64-bit totals block
 enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotWords };
 
+// Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
+// [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
+struct SegTable {
+  uint32_t* cnt;  // [kMaxSegs]
+  uint32_t* per;  // [1]
+};
+
+struct RayStream {
+  float4* o;    // origin.xyz, rng state bits
+  float4* d;    // direction.xyz, path id bits
+  float4* thr;  // throughput.xyz
+};
+
 struct WaveView {
-  float4* o;
-  float4* d;
-  float4* thr;
-  float4* rad;
-  uint2* hit;
-  uint32_t* q[2];  // paths to trace at bounce d (ping-pong)
-  uint32_t* qh;    // paths that hit at this bounce (shade queue)
-  uint32_t* sq;
-  float4* stask;
-  uint32_t* cnt;
+  RayStream rs[2];  // ping-pong by depth parity: bounce d traces rs[d&1], shade d writes rs[(d+1)&1]
+  uint4* hrec;      // (slot or path id, t bits, prim ref, -) per hit
+  float4* rad;      // per path id
+  float4* stask;    // per shade slot: L tasks of tstride float4
+  SegTable segN, segH, segS;  // next rays, hits, shadow tasks
   unsigned long long* tot;
-  uint32_t L;        // lights (tasks per path)
+  unsigned long long* bstat;  // [kMaxSegs] per-block any-hit tallies (k_shadow), folded by k_accum
+  uint32_t L;        // lights (tasks per shaded path)
   uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
 };
 
@@ -158,8 +167,8 @@ struct Context {
   float env_intensity = 0.8f, env_clamp = 5.0f;
   // wavefront buffers
   uint64_t wave_cap = 0;  // paths
-  uint32_t wave_L = 0;
-  DevBuf w_o, w_d, w_thr, w_rad, w_hit, w_q0, w_q1, w_qh, w_sq, w_stask, w_cnt, w_tot;
+  uint32_t wave_L = 0, wave_ts = 0;
+  DevBuf w_rs[2][3], w_hrec, w_rad, w_stask, w_seg, w_tot;
   // pixel buffers
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;
@@ -176,13 +185,14 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
 
 // kernels_wavefront.hip
 SceneView scene_view(const Context& c);
-void launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
-                  hipStream_t s);
-void launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
-                  hipStream_t s);
-void launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, hipStream_t s);
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, int max_depth,
-                       hipStream_t s);
+// Stage launchers return their (resident) grid size: the segment count their consumer scans.
+unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
+                  uint32_t nseg_in, hipStream_t s);
+unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                  uint32_t nseg_in, hipStream_t s);
+unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
+                   hipStream_t s);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
