@@ -181,7 +181,7 @@ def main():
 
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / len(stats), 3)
-                    for k in ("trace", "shade", "shadow", "accum")}
+                    for k in ("trace0", "trace", "shade0", "shade", "shadow", "accum")}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),

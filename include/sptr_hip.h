@@ -128,10 +128,12 @@ typedef struct sptr_stats {
   uint64_t samples;      /* pixel samples completed */
   uint64_t waves;        /* wavefront batches launched */
   double ms_total;       /* wall time of the call on the device stream */
-  double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_accum; /* SPTR_FRAME_TIMING only */
+  double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_accum; /* SPTR_FRAME_TIMING only; raygen is fused
+                                                                into the bounce-0 trace (ms_raygen = 0) */
   uint64_t trace_launches;
   uint64_t node_visits, tri_tests, sphere_tests; /* SPTR_FRAME_COUNT_VISITS only */
   uint64_t shadow_node_visits, shadow_prim_tests;
+  double ms_trace0, ms_shade0; /* SPTR_FRAME_TIMING: bounce-0 parts of ms_trace / ms_shade */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */
@@ -143,7 +145,7 @@ int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
 /* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default 2^27,
  * at most 2^30). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
-/* Maximum primitives per BVH leaf range (1..8, default 4); applies to the next sptr_upload_scene. */
+/* Maximum primitives per BVH leaf range (1..32, default 4); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 
 /* ---- scene / state (OptixBackend::build and setters) -------------------------------------------- */

@@ -18,6 +18,8 @@
 // place that uses fma: they only prune traversal and are padded to stay conservative.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "sptr_internal.h"
 
 // Occupancy hints (min waves per SIMD); 1 = let the register allocator decide.
@@ -45,12 +47,32 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* s_cnt, bool pred) {
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
-// Contiguous per-block slice [lo, hi) of n items, whole multiples of the block size; per = slice
-// length of every block (the segment stride of this kernel's outputs).
-__device__ __forceinline__ void block_slice(uint32_t n, uint32_t& lo, uint32_t& hi, uint32_t& per) {
-  per = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
-  lo = min(n, blockIdx.x * per);
-  hi = min(n, lo + per);
+// XCD-aware logical block index.  Workgroups are dispatched round-robin over the 8 XCDs, so with
+// the identity mapping neighbouring slices (neighbouring image regions for bounce 0) land on
+// different XCDs and every XCD's private 4 MB L2 has to hold the BVH working set of the whole
+// frame.  Remapping gives XCD x the contiguous logical range [x*G/8, (x+1)*G/8).
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t logical_block() {
+  const uint32_t g = gridDim.x, b = blockIdx.x;
+  return (g % kXcds) ? b : (b % kXcds) * (g / kXcds) + b / kXcds;
+}
+// Work schedule of the stage kernels: block-sized chunks dealt round-robin over the (logical)
+// blocks, chunk c -> block c % G.  Per-item cost varies by orders of magnitude across the image
+// (sky vs a 10M-triangle mesh), so contiguous per-block slices leave the kernel waiting on the
+// blocks that drew the expensive region; dealing chunks balances statistically and keeps all CUs
+// on one band of the frame at a time (shared BVH working set).  Every block processes at most
+// `per` items, which is the stride of its output segment: seg0 = logical block * per.
+struct Sched {
+  uint32_t first, step, per, seg0;
+};
+__device__ __forceinline__ Sched block_sched(uint32_t n) {
+  Sched s;
+  const uint32_t lb = logical_block();
+  s.first = lb * kBlock;
+  s.step = gridDim.x * kBlock;
+  s.per = (n + s.step - 1) / s.step * kBlock;
+  s.seg0 = lb * s.per;
+  return s;
 }
 
 // Consumer prologue: exclusive scan of the producer's per-block segment counts into LDS
@@ -101,7 +123,7 @@ __device__ __forceinline__ uint32_t seg_slot(const uint32_t* s_off, uint32_t nse
 __device__ __forceinline__ void seg_publish(const SegTable& t, const uint32_t* s_cnt, uint32_t per) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    t.cnt[blockIdx.x] = *s_cnt;
+    t.cnt[logical_block()] = *s_cnt;
     if (blockIdx.x == 0) *t.per = per;
   }
 }
@@ -261,14 +283,34 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
   return hit;
 }
 
+// Traversal stack: the top kLdsStack entries live in LDS (one column per thread, entry-major so a
+// wave's pushes at equal depth hit 64 distinct banks); deeper entries spill to a private array
+// (scratch), which only very deep traversals touch.  Scratch-only stacks put a ~500-cycle
+// dependent load on every pop.
+constexpr int kLdsStack = 12;
+struct TravStack {
+  uint32_t* lds;  // &s_stack[0][threadIdx.x]
+  uint32_t spill[kStack - kLdsStack];
+  __device__ __forceinline__ void put(int i, uint32_t v) {
+    if (i < kLdsStack) lds[i * kBlock] = v;
+    else spill[i - kLdsStack] = v;
+  }
+  __device__ __forceinline__ uint32_t get(int i) const { return i < kLdsStack ? lds[i * kBlock] : spill[i - kLdsStack]; }
+};
+struct alignas(16) LdsStack {
+  uint32_t e[kLdsStack][kBlock];
+};
+static_assert(sizeof(LdsStack) % 16 == 0, "keeps the dynamic-LDS base aligned");
+
 // BVH2 stack traversal: nearest child first; leaf children are tested as soon as their box is hit.
 template <bool kAny, bool kCount>
 __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* prim_ref, const float4* tris,
                                          const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                         uint32_t& ref, Visits& vc) {
+                                         uint32_t& ref, Visits& vc, LdsStack& ls) {
   if (root == kNoHit) return false;
   if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-  uint32_t stack[kStack];
+  TravStack stack;
+  stack.lds = &ls.e[0][threadIdx.x];
   int sp = 0;
   uint32_t cur = root;
   bool hit = false;
@@ -301,7 +343,7 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
         L = R;
         R = s;
       }
-      if (sp < kStack) stack[sp++] = R;
+      if (sp < kStack) stack.put(sp++, R);
       cur = L;
     } else if (hl) {
       cur = L;
@@ -309,7 +351,7 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
       cur = R;
     } else {
       if (sp == 0) break;
-      cur = stack[--sp];
+      cur = stack.get(--sp);
     }
   }
   return hit;
@@ -494,6 +536,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 template <bool kLds, bool kCount, bool kPrimary>
 __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
     k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
+  __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
@@ -509,11 +552,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
   if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
   const RayStream rs = w.rs[depth & 1];
   Visits vc;
-  uint32_t lo, hi, per;
-  block_slice(n, lo, hi, per);
-  for (uint32_t base = lo; base < hi; base += kBlock) {
+  const Sched sd = block_sched(n);
+  for (uint32_t base = sd.first; base < n; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
-    bool active = i < hi, hit = false;
+    bool active = i < n, hit = false;
     uint32_t id = 0u, pid = 0u, ref = kNoHit;
     float tfar = __builtin_huge_valf();
     vec3 o, d;
@@ -534,7 +576,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
     }
     if (active) {
       const Ray r = make_ray(o, d);
-      hit = traverse<false, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc);
+      hit = traverse<false, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc, s_stack);
       if (!hit) {
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -548,9 +590,12 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
       }
     }
     const uint32_t j = block_append(&s_cnt, hit);
-    if (hit) w.hrec[lo + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+    if (hit) {
+      if (sd.seg0 + j < w.seg_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+      else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
+    }
   }
-  seg_publish(w.segH, &s_cnt, per);
+  seg_publish(w.segH, &s_cnt, sd.per);
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
@@ -577,11 +622,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
   const uint32_t ts = w.tstride, L = w.L;
-  uint32_t lo, hi, per;
-  block_slice(n, lo, hi, per);
-  for (uint32_t base = lo; base < hi; base += kBlock) {
+  const Sched sd = block_sched(n);
+  for (uint32_t base = sd.first; base < n; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
-    const bool active = i < hi;
+    const bool active = i < n;
     bool cont = false, shadow = false, dirty = kPrimary;
     uint32_t p = 0u, rng = 0u;
     vec3 ro, rd, thr, radv = v3(0.0f, 0.0f, 0.0f), P, nrm, no, nd;
@@ -646,9 +690,13 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       }
     }
     const uint32_t js = block_append(&s_cnt_s, shadow);
+    if (shadow && sd.seg0 + js >= w.seg_cap) {
+      shadow = false;
+      w.tot[kTotOverflow] = 1ull;
+    }
     if (shadow) {
       // direct light: shadow tasks carry the precomputed contribution, added if unoccluded
-      float4* task = w.stask + (size_t)(lo + js) * L * ts;
+      float4* task = w.stask + (size_t)(sd.seg0 + js) * L * ts;
       const vec3 view = -rd;
       for (uint32_t li = 0; li < L; ++li, task += ts) {
         const DevLight& Lt = sh.lights[li];
@@ -744,19 +792,23 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     }
     if (active && dirty) w.rad[p] = f4(radv, 0.0f);
     const uint32_t jn = block_append(&s_cnt_n, cont);
+    if (cont && sd.seg0 + jn >= w.seg_cap) {
+      cont = false;
+      w.tot[kTotOverflow] = 1ull;
+    }
     if (cont) {
-      rout.o[lo + jn] = f4(no, __uint_as_float(rng));
-      rout.d[lo + jn] = f4(nd, __uint_as_float(p));
-      rout.thr[lo + jn] = f4(thr, 0.0f);
+      rout.o[sd.seg0 + jn] = f4(no, __uint_as_float(rng));
+      rout.d[sd.seg0 + jn] = f4(nd, __uint_as_float(p));
+      rout.thr[sd.seg0 + jn] = f4(thr, 0.0f);
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    w.segN.cnt[blockIdx.x] = s_cnt_n;
-    w.segS.cnt[blockIdx.x] = s_cnt_s;
+    w.segN.cnt[logical_block()] = s_cnt_n;
+    w.segS.cnt[logical_block()] = s_cnt_s;
     if (blockIdx.x == 0) {
-      *w.segN.per = per;
-      *w.segS.per = per;
+      *w.segN.per = sd.per;
+      *w.segS.per = sd.per;
     }
   }
 }
@@ -767,6 +819,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount>
 __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
+  __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
@@ -776,9 +829,9 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
   const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
   const uint32_t ts = w.tstride, L = w.L;
   Visits vc;
-  uint32_t lo, hi, per, rays = 0u;
-  block_slice(n, lo, hi, per);
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+  uint32_t rays = 0u;
+  const Sched sd = block_sched(n);
+  for (uint32_t i = sd.first + threadIdx.x; i < n; i += sd.step) {
     const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, i) * L * ts;
     bool any = false;
     uint32_t p = 0u;
@@ -796,7 +849,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
       float tfar = a.w;
       uint32_t ref = kNoHit;
       ++rays;
-      const bool occ = traverse<true, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc);
+      const bool occ =
+          traverse<true, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc, s_stack);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
         any = true;
@@ -876,6 +930,7 @@ __global__ void __launch_bounds__(kBlock) k_unpack(const uint32_t* g, int G, uin
 __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* tri_orig, const uint32_t* sph_orig,
                                                   const float* rays, uint32_t n, int anyhit, uint32_t* ref_out,
                                                   float* t_out, float* ng_out, uint8_t* occ) {
+  __shared__ LdsStack s_stack;
   Visits vc;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
     const float* rr = rays + (size_t)i * 8;
@@ -883,10 +938,13 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
     float tfar = rr[7];
     uint32_t ref = kNoHit;
     if (anyhit) {
-      occ[i] = traverse<true, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc) ? 1 : 0;
+      occ[i] = traverse<true, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc, s_stack)
+                   ? 1
+                   : 0;
       continue;
     }
-    const bool hit = traverse<false, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc);
+    const bool hit =
+        traverse<false, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc, s_stack);
     // report (type bit | original primitive index) so the host can map to (geomID, primID)
     ref_out[i] = hit ? ((ref & kSphereBit) | ((ref & kSphereBit) ? sph_orig[ref & kIndexMask] : tri_orig[ref & kIndexMask]))
                      : kNoHit;
@@ -954,6 +1012,12 @@ static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
   }
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds_bytes) != hipSuccess || per <= 0) per = 4;
+  static int cap = -1;  // SPTR_MAX_BLOCKS_PER_CU: experiment knob (resident blocks per CU)
+  if (cap < 0) {
+    const char* e = getenv("SPTR_MAX_BLOCKS_PER_CU");
+    cap = e ? atoi(e) : 0;
+  }
+  if (cap > 0 && per > cap) per = cap;
   unsigned blocks = (unsigned)(cus * per);
   if (blocks > kMaxSegs) blocks = kMaxSegs;  // producer grids index the segment tables
   for (GridCache& g : cache)

@@ -99,12 +99,15 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
 int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts) {
   L = L ? L : 1u;
   if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
-  const size_t n = (size_t)cap;
+  // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
+  // with per = ceil(n / (G*kBlock)) * kBlock, so the segment space G*per can exceed n by up to
+  // G*kBlock - 1 records: every segmented stream carries kMaxSegs*kBlock records of slack.
+  const size_t n = (size_t)cap, ns = n + (size_t)kMaxSegs * kBlock;
   for (auto& b : c.w_rs)
-    for (DevBuf& x : b) API_HIP(ensure_buf(x, n * 16));
-  API_HIP(ensure_buf(c.w_hrec, n * 16));
+    for (DevBuf& x : b) API_HIP(ensure_buf(x, ns * 16));
+  API_HIP(ensure_buf(c.w_hrec, ns * 16));
   API_HIP(ensure_buf(c.w_rad, n * 16));
-  API_HIP(ensure_buf(c.w_stask, n * L * ts * 16));
+  API_HIP(ensure_buf(c.w_stask, ns * L * ts * 16));
   c.wave_cap = cap;
   c.wave_L = L;
   c.wave_ts = ts;
@@ -135,6 +138,7 @@ WaveView wave_view(Context& c) {
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
+  w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
   return w;
 }
 
@@ -209,12 +213,14 @@ struct StageTimer {  // per-stage HIP events on the render stream (SPTR_FRAME_TI
     if (!on) return;
     (void)hipEventRecord(next(), s);
   }
-  void collect(double ms[5], uint64_t& trace_launches) {
+  // stages: 0 unused, 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum + resolve,
+  //         5 trace bounce 0 (raygen fused), 6 shade bounce 0
+  void collect(double ms[7], uint64_t& trace_launches) {
     for (auto& m : marks) {
       float t = 0.0f;
       (void)hipEventElapsedTime(&t, (*pool)[m.second], (*pool)[m.second + 1]);
       ms[m.first] += t;
-      if (m.first == 1) ++trace_launches;
+      if (m.first == 1 || m.first == 5) ++trace_launches;
     }
     marks.clear();
     used = 0;
@@ -280,7 +286,7 @@ int sptr_set_debug_mode(sptr_ctx* x, int mode) {
 
 int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   if (!x) return SPTR_ERR_INVALID;
-  if (n < 1 || n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 1..8");
+  if (n < 1 || n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 1..32");
   x->c.leaf_size = n;
   return SPTR_OK;
 }
@@ -299,7 +305,9 @@ int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
   if ((s->num_tris && (!s->indices || !s->positions || !s->tri_geom_first)) || (s->num_spheres && !s->spheres) ||
       ((s->num_tri_geoms + s->num_spheres) && !s->geom_material))
     return fail(c, SPTR_ERR_INVALID, "scene: null array with nonzero count");
-  if ((uint64_t)s->num_tris + s->num_spheres >= (1ull << 30)) return fail(c, SPTR_ERR_INVALID, "scene too large");
+  // leaf links keep 32 - 1 - kLeafCountBits bits of range start
+  if ((uint64_t)s->num_tris + s->num_spheres >= (1ull << (31 - kLeafCountBits)))
+    return fail(c, SPTR_ERR_INVALID, "scene too large (at most 2^26 primitives)");
   if (s->num_tri_geoms && s->tri_geom_first[s->num_tri_geoms] != s->num_tris)
     return fail(c, SPTR_ERR_INVALID, "scene: tri_geom_first must end at num_tris");
   for (uint64_t i = 0; i < (uint64_t)s->num_tris * 3; ++i)
@@ -464,10 +472,10 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
     for (int d = 0; d < D; ++d) {
-      tm.begin(1);
+      tm.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
-      tm.begin(2);
+      tm.begin(d == 0 ? 6 : 2);
       g_shade = launch_shade(sv, sh, fv, w, d, g_trace, s);
       tm.end();
       tm.begin(3);
@@ -494,16 +502,19 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   c.last_samples = total;
   unsigned long long tot[kTotWords];
   API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
+  if (tot[kTotOverflow]) return fail(c, SPTR_ERR_HIP, "render: segmented stream overflow (internal error)");
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, e_begin, e_end);
     stats->ms_total = ms;
-    double st[5] = {0, 0, 0, 0, 0};
+    double st[7] = {0, 0, 0, 0, 0, 0, 0};
     tm.collect(st, stats->trace_launches);
-    stats->ms_raygen = st[0];
-    stats->ms_trace = st[1];
-    stats->ms_shade = st[2];
+    stats->ms_raygen = 0.0;  // raygen is fused into the bounce-0 trace (ms_trace0)
+    stats->ms_trace = st[1] + st[5];
+    stats->ms_shade = st[2] + st[6];
+    stats->ms_trace0 = st[5];
+    stats->ms_shade0 = st[6];
     stats->ms_shadow = st[3];
     stats->ms_accum = st[4];
     stats->rays_closest = tot[kTotClosest];
@@ -516,7 +527,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     stats->shadow_node_visits = tot[kTotShNodes];
     stats->shadow_prim_tests = tot[kTotShPrims];
   } else {
-    double st[5] = {0, 0, 0, 0, 0};
+    double st[7] = {0, 0, 0, 0, 0, 0, 0};
     uint64_t tl = 0;
     tm.collect(st, tl);
   }

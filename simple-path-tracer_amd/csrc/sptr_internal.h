@@ -27,9 +27,9 @@ namespace sptr {
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kIndexMask = 0x3FFFFFFFu;
-// Leaf link: kLeafBit | start << kLeafCountBits | (count - 1): a contiguous range of up to 8 sorted
+// Leaf link: kLeafBit | start << kLeafCountBits | (count - 1): a contiguous range of up to 32 sorted
 // primitive references (prim_ref[start .. start+count)).  Primitive ref: [kSphereBit] | slot.
-constexpr uint32_t kLeafCountBits = 3;
+constexpr uint32_t kLeafCountBits = 5;  // start keeps 26 bits: up to 64M primitives
 constexpr uint32_t kLeafCountMask = (1u << kLeafCountBits) - 1u;
 constexpr uint32_t kMaxLeafSize = 1u << kLeafCountBits;
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
@@ -111,7 +111,7 @@ struct FrameView {
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 
 // 64-bit totals block
-enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotWords };
+enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotOverflow, kTotWords };
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
@@ -134,6 +134,7 @@ struct WaveView {
   SegTable segN, segH, segS;  // next rays, hits, shadow tasks
   unsigned long long* tot;
   unsigned long long* bstat;  // [kMaxSegs] per-block any-hit tallies (k_shadow), folded by k_accum
+  uint32_t seg_cap;  // records allocated per segmented stream (bounds guard)
   uint32_t L;        // lights (tasks per shaded path)
   uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
 };
@@ -151,7 +152,7 @@ struct Context {
   uint64_t wave_paths = 0;  // 0 = default
   // scene
   DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
-  uint32_t leaf_size = 4;  // max primitives per BVH leaf range (1..8)
+  uint32_t leaf_size = 4;  // max primitives per BVH leaf range (1..32)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_tri_geoms = 0;
   std::vector<uint32_t> geom_first;     // host copy for primID derivation

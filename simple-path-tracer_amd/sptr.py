@@ -72,7 +72,7 @@ class Stats(C.Structure):
                 ("ms_trace", C.c_double), ("ms_shade", C.c_double), ("ms_shadow", C.c_double),
                 ("ms_accum", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("shadow_node_visits", C.c_uint64),
-                ("shadow_prim_tests", C.c_uint64)]
+                ("shadow_prim_tests", C.c_uint64), ("ms_trace0", C.c_double), ("ms_shade0", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
