@@ -56,7 +56,8 @@ def roofline(cnt, stats, layout, wl_name, steps):
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
     launches_per_step = max(1, launches // max(1, steps))
     stream = STREAM_BYTES_PER_RAY * cnt.rays_closest
-    scene = 64.0 * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
+    node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0  # 64 BVH2, 128 BVH4
+    scene = node_b * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
     lds = layout["lds_bytes"] > 0
     hbm_alg = stream + (0.0 if lds else scene)
     per_launch = hbm_alg / launches_per_step
@@ -114,6 +115,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
+    ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
     args = ap.parse_args()
     wl = workloads.WORKLOADS[args.workload]
     W, H = wl.width, wl.height
@@ -132,6 +134,8 @@ def main():
         r.set_wave_paths(args.wave_paths)
     if args.leaf_size:
         r.set_leaf_size(args.leaf_size)
+    if args.bvh_width:
+        r.set_bvh_width(args.bvh_width)
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
     cam = workloads.camera(wl)
@@ -202,8 +206,9 @@ def main():
             "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
             "stage_ms_per_step": stage_ms,
             "rays_per_step": int(rays / args.steps),
-            "scene": {"prims": info["prims"], "nodes": info["nodes"], "bvh_depth": info["depth"],
-                      "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"]},
+            "scene": {"prims": info["prims"], "lbvh_nodes": info["nodes"], "bvh_depth": info["depth"],
+                      "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"],
+                      "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

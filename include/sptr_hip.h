@@ -145,8 +145,12 @@ int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
 /* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default 2^27,
  * at most 2^30). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
-/* Maximum primitives per BVH leaf range (1..32, default 4); applies to the next sptr_upload_scene. */
+/* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
+ * LDS, 2 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
+/* Traversal width: 2 (the LBVH as built), 4 (collapsed to 128-B BVH4 nodes), or 0 = automatic (the
+ * default: 2 for scenes staged in LDS, 4 otherwise). */
+int sptr_set_bvh_width(sptr_ctx* ctx, uint32_t width);
 
 /* ---- scene / state (OptixBackend::build and setters) -------------------------------------------- */
 int sptr_upload_scene(sptr_ctx* ctx, const sptr_scene* scene); /* builds the LBVH on the device */
@@ -160,6 +164,7 @@ int sptr_scene_info(const sptr_ctx* ctx, uint32_t* num_prims, uint32_t* num_node
 typedef struct sptr_scene_layout {
   uint32_t num_tris, num_spheres, num_nodes, leaf_size, bvh_depth, lds_bytes;
   uint64_t node_bytes, tri_bytes, sphere_bytes, prim_ref_bytes;
+  uint32_t bvh_width, pad; /* num_nodes / node_bytes describe the traversed (BVH2 or BVH4) nodes */
 } sptr_scene_layout;
 int sptr_scene_layout_info(const sptr_ctx* ctx, sptr_scene_layout* out);
 

@@ -11,6 +11,8 @@
 //   k_refit       : bottom-up box propagation; the second child to arrive at a node finishes it
 //                   (agent-scope release/acquire, write-through box stores — the hand-off recipe of
 //                   the gfx950 guide, Guideline 16)
+//   k_depth4 + scan + k_collapse4 : BVH4 — every reachable BVH2 node at even depth becomes a
+//                   BVH4 node whose (up to four) children are its grandchildren; leaves stay ranges
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -213,7 +215,7 @@ __global__ void k_karras(int N, const uint64_t* keys, uint32_t leaf_max, BvhNode
     const uint32_t nl = (uint32_t)(gamma - lo + 1), nr = (uint32_t)(hi - gamma);
     nodes[i].link.x = nl <= leaf_max ? range_link((uint32_t)lo, nl) : kl;
     nodes[i].link.y = nr <= leaf_max ? range_link((uint32_t)(gamma + 1), nr) : kr;
-    nodes[i].link.w = 0u;
+    nodes[i].link.w = (uint32_t)(hi - lo + 1);  // primitives under node i (reachability test)
     kids[i] = make_uint2(kl, kr);
   }
 }
@@ -275,6 +277,67 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
   }
 }
 
+// BVH4 collapse, pass 1: keep[i] = 1 for BVH2 nodes that are reachable through internal links
+// (covering more than leaf_max primitives) and lie at even depth.
+__global__ void k_depth4(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
+    uint32_t k = 0u;
+    if (nodes[i].link.w > leaf_max) {
+      uint32_t dep = 0u, q = (uint32_t)i;
+      while (q != 0u) {
+        q = nodes[q].link.z;
+        ++dep;
+      }
+      k = (dep & 1u) ? 0u : 1u;
+    }
+    keep[i] = k;
+  }
+}
+
+__device__ __forceinline__ void put_child(Bvh4Node& o, int k, float lx, float hx, float ly, float hy, float lz, float hz,
+                                          uint32_t link) {
+  reinterpret_cast<float*>(&o.lox)[k] = lx;
+  reinterpret_cast<float*>(&o.hix)[k] = hx;
+  reinterpret_cast<float*>(&o.loy)[k] = ly;
+  reinterpret_cast<float*>(&o.hiy)[k] = hy;
+  reinterpret_cast<float*>(&o.loz)[k] = lz;
+  reinterpret_cast<float*>(&o.hiz)[k] = hz;
+  reinterpret_cast<uint32_t*>(&o.link)[k] = link;
+}
+
+// BVH4 collapse, pass 2: node i (kept) -> BVH4 node idx[i]; an internal child (odd depth, not kept)
+// is replaced by its two children, in left-to-right order.
+__global__ void k_collapse4(int N, const BvhNode* nodes, const uint32_t* keep, const uint32_t* idx, Bvh4Node* out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
+    if (!keep[i]) continue;
+    const BvhNode nd = nodes[i];
+    Bvh4Node o;
+    o.link = make_uint4(kNoHit, kNoHit, kNoHit, kNoHit);
+    o.lox = o.hix = o.loy = o.hiy = o.loz = o.hiz = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int k = 0;
+    const uint32_t links[2] = {nd.link.x, nd.link.y};
+    for (int side = 0; side < 2; ++side) {
+      const uint32_t c = links[side];
+      if (c & kLeafBit) {
+        if (side == 0) put_child(o, k++, nd.lxy.x, nd.lxy.y, nd.lxy.z, nd.lxy.w, nd.z.x, nd.z.y, c);
+        else put_child(o, k++, nd.rxy.x, nd.rxy.y, nd.rxy.z, nd.rxy.w, nd.z.z, nd.z.w, c);
+        continue;
+      }
+      const BvhNode cn = nodes[c];
+      const uint32_t g0 = cn.link.x, g1 = cn.link.y;
+      put_child(o, k++, cn.lxy.x, cn.lxy.y, cn.lxy.z, cn.lxy.w, cn.z.x, cn.z.y, (g0 & kLeafBit) ? g0 : idx[g0]);
+      put_child(o, k++, cn.rxy.x, cn.rxy.y, cn.rxy.z, cn.rxy.w, cn.z.z, cn.z.w, (g1 & kLeafBit) ? g1 : idx[g1]);
+    }
+    uint32_t par = kNoHit;
+    if (i != 0) {
+      const uint32_t p1 = nd.link.z;  // odd-depth parent
+      par = idx[nodes[p1].link.z];    // its parent is kept
+    }
+    o.meta = make_uint4(par, (uint32_t)k, 0u, 0u);
+    out[idx[i]] = o;
+  }
+}
+
 struct Tmp {
   std::vector<void*> ptrs;
   ~Tmp() {
@@ -328,6 +391,8 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(realloc_buf(c.prim_ref, ((size_t)N + 3) / 4 * 16));
   if (N == 0) {
     c.root = kNoHit;
+    c.root4 = kNoHit;
+    c.num_nodes4 = 0;
     return SPTR_OK;
   }
   Tmp tmp;
@@ -388,9 +453,16 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
                      static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p),
                      static_cast<uint32_t*>(c.prim_ref.p));
   LB_CHECK(hipGetLastError());
-  const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size, kMaxLeafSize));
+  // automatic leaf size (measured, profiles/r01*): ranges of 8 for scenes small enough to be staged
+  // in LDS (fewer, divergence-free node steps), 2 for meshes traversed from L2/HBM
+  const uint32_t auto_leaf = ((uint64_t)(N > 1 ? N - 1 : 0) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 +
+                              ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : 2u;
+  const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size ? c.leaf_size : auto_leaf, kMaxLeafSize));
+  c.leaf_used = leaf_max;
   if (N == 1) {
     c.root = kLeafBit | 0u;  // range [0, 1)
+    c.root4 = c.root;
+    c.num_nodes4 = 0;
     c.bvh_depth = 0;
   } else {
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
@@ -409,6 +481,29 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     if (dep >= (uint32_t)kStack) {
       c.err = "lbvh: tree depth " + std::to_string(dep) + " exceeds the traversal stack";
       return SPTR_ERR_INVALID;
+    }
+    if (c.root & kLeafBit) {
+      c.num_nodes4 = 0;
+      c.root4 = c.root;
+    } else {
+      // BVH4: keep flags -> exclusive scan -> collapse (reusing flag/slot scratch arrays)
+      hipLaunchKernelGGL(k_depth4, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag);
+      LB_CHECK(hipGetLastError());
+      size_t s4 = 0;
+      LB_CHECK(rocprim::exclusive_scan(nullptr, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
+      void* st4 = nullptr;
+      LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&st4), s4));
+      LB_CHECK(rocprim::exclusive_scan(st4, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
+      uint32_t last_keep = 0, last_slot = 0;
+      LB_CHECK(hipMemcpyAsync(&last_keep, flag + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipMemcpyAsync(&last_slot, slot + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipStreamSynchronize(s));
+      c.num_nodes4 = last_slot + last_keep;
+      LB_CHECK(realloc_buf(c.nodes4, (size_t)c.num_nodes4 * sizeof(Bvh4Node)));
+      hipLaunchKernelGGL(k_collapse4, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
+                         static_cast<Bvh4Node*>(c.nodes4.p));
+      LB_CHECK(hipGetLastError());
+      c.root4 = 0u;  // node 0 (depth 0) is kept and scans to index 0
     }
   }
   LB_CHECK(hipStreamSynchronize(s));

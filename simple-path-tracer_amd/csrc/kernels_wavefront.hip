@@ -26,6 +26,10 @@
 #ifndef SPTR_TRACE_WAVES
 #define SPTR_TRACE_WAVES 7  // measured: 7 -> +6% on C2 (SGPR-limited to 6 otherwise)
 #endif
+#ifndef SPTR_TRACE4_WAVES
+#define SPTR_TRACE4_WAVES 6  // BVH4, bounces >= 1: 7 waves (72 VGPRs) spills; measured C5 12.7 -> 7.1 ms
+                             // (bounce 0 stays at 7: coherent rays gain more from occupancy, 8.4 -> 5.4)
+#endif
 #ifndef SPTR_SHADE_WAVES
 #define SPTR_SHADE_WAVES 1
 #endif
@@ -288,6 +292,15 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
 // (scratch), which only very deep traversals touch.  Scratch-only stacks put a ~500-cycle
 // dependent load on every pop.
 constexpr int kLdsStack = 12;
+#ifdef SPTR_EXPERIMENT_NO_SPILL  // timing experiment only: drops pushes beyond kLdsStack (wrong hits)
+struct TravStack {
+  uint32_t* lds;
+  __device__ __forceinline__ void put(int i, uint32_t v) {
+    if (i < kLdsStack) lds[i * kBlock] = v;
+  }
+  __device__ __forceinline__ uint32_t get(int i) const { return i < kLdsStack ? lds[i * kBlock] : 0u; }
+};
+#else
 struct TravStack {
   uint32_t* lds;  // &s_stack[0][threadIdx.x]
   uint32_t spill[kStack - kLdsStack];
@@ -297,6 +310,7 @@ struct TravStack {
   }
   __device__ __forceinline__ uint32_t get(int i) const { return i < kLdsStack ? lds[i * kBlock] : spill[i - kLdsStack]; }
 };
+#endif
 struct alignas(16) LdsStack {
   uint32_t e[kLdsStack][kBlock];
 };
@@ -357,20 +371,79 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
   return hit;
 }
 
+// BVH4 traversal: four slab tests per 128-B node; leaf children are tested as soon as their box is
+// hit; the nearest internal child is visited next and the other hit children are pushed.
+template <bool kAny, bool kCount>
+__device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t* prim_ref, const float4* tris,
+                                          const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
+                                          uint32_t& ref, Visits& vc, LdsStack& ls) {
+  if (root == kNoHit) return false;
+  if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
+  TravStack stack;
+  stack.lds = &ls.e[0][threadIdx.x];
+  int sp = 0;
+  uint32_t cur = root;
+  bool hit = false;
+  for (;;) {
+    const Bvh4Node* nd = nodes + cur;
+    const float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
+    const uint4 ln = nd->link;
+    if (kCount) ++vc.nodes;
+    float t0, t1, t2, t3;
+    bool h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tnear, tfar, t0) && ln.x != kNoHit;
+    bool h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tnear, tfar, t1) && ln.y != kNoHit;
+    bool h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tnear, tfar, t2) && ln.z != kNoHit;
+    bool h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tnear, tfar, t3) && ln.w != kNoHit;
+    uint32_t c0 = ln.x, c1 = ln.y, c2 = ln.z, c3 = ln.w;
+#define SPTR_LEAF4(H, C)                                                                      \
+  if (H && (C & kLeafBit)) {                                                                  \
+    if (leaf_test<kAny, kCount>(C, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {           \
+      hit = true;                                                                             \
+      if (kAny) return true;                                                                  \
+    }                                                                                         \
+    H = false;                                                                                \
+  }
+    SPTR_LEAF4(h0, c0)
+    SPTR_LEAF4(h1, c1)
+    SPTR_LEAF4(h2, c2)
+    SPTR_LEAF4(h3, c3)
+#undef SPTR_LEAF4
+    if (h0 || h1 || h2 || h3) {
+      // continue with the nearest hit child (lowest slot on ties); push the others, farthest last-in
+      float tn = h0 ? t0 : __builtin_huge_valf();
+      uint32_t cn = c0, kn = 0u;
+      if (h1 && (!h0 || t1 < tn)) { tn = t1; cn = c1; kn = 1u; }
+      if (h2 && ((!h0 && !h1) || t2 < tn)) { tn = t2; cn = c2; kn = 2u; }
+      if (h3 && ((!h0 && !h1 && !h2) || t3 < tn)) { tn = t3; cn = c3; kn = 3u; }
+      if (h3 && kn != 3u && sp < kStack) stack.put(sp++, c3);
+      if (h2 && kn != 2u && sp < kStack) stack.put(sp++, c2);
+      if (h1 && kn != 1u && sp < kStack) stack.put(sp++, c1);
+      if (h0 && kn != 0u && sp < kStack) stack.put(sp++, c0);
+      cur = cn;
+    } else {
+      if (sp == 0) break;
+      cur = stack.get(--sp);
+    }
+  }
+  return hit;
+}
+
 // Stage the whole scene (nodes, triangles, spheres) into LDS when it fits (SceneView::lds_bytes).
 struct Staged {
   const BvhNode* nodes;
+  const Bvh4Node* nodes4;
   const uint32_t* prim_ref;
   const float4* tris;
   const float4* sph;
 };
 template <bool kLds>
 __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) {
-  Staged s{sv.nodes, sv.prim_ref, sv.tris, sv.sph};
+  Staged s{sv.nodes, sv.nodes4, sv.prim_ref, sv.tris, sv.sph};
   if (kLds) {
-    const uint32_t nn = sv.num_nodes * 4u, nt = sv.num_tris * 3u, ns = sv.num_sph;
+    const bool w4 = sv.width == 4u;
+    const uint32_t nn = w4 ? sv.num_nodes4 * 8u : sv.num_nodes * 4u, nt = sv.num_tris * 3u, ns = sv.num_sph;
     const uint32_t np = (sv.num_tris + sv.num_sph + 3u) / 4u;  // prim refs, in float4 units
-    const float4* gn = reinterpret_cast<const float4*>(sv.nodes);
+    const float4* gn = w4 ? reinterpret_cast<const float4*>(sv.nodes4) : reinterpret_cast<const float4*>(sv.nodes);
     const float4* gp = reinterpret_cast<const float4*>(sv.prim_ref);
     for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lds[i] = gn[i];
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) lds[nn + i] = sv.tris[i];
@@ -378,11 +451,19 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[nn + nt + ns + i] = gp[i];
     __syncthreads();
     s.nodes = reinterpret_cast<const BvhNode*>(lds);
+    s.nodes4 = reinterpret_cast<const Bvh4Node*>(lds);
     s.tris = lds + nn;
     s.sph = lds + nn + nt;
     s.prim_ref = reinterpret_cast<const uint32_t*>(lds + nn + nt + ns);
   }
   return s;
+}
+
+template <bool kW4, bool kAny, bool kCount>
+__device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv, const Ray& r, float tnear, float& tfar,
+                                           uint32_t& ref, Visits& vc, LdsStack& ls) {
+  if (kW4) return traverse4<kAny, kCount>(sc.nodes4, sc.prim_ref, sc.tris, sc.sph, sv.root4, r, tnear, tfar, ref, vc, ls);
+  return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
 }
 
 __device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long long* tot, int base) {
@@ -533,8 +614,8 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // records in this block's segment.  kPrimary: bounce 0, one thread per path slot, camera ray
 // computed in place (no input stream at all).  Input of later bounces: the dense ray stream
 // rs[depth&1] written by the previous k_shade, addressed through its segment table.
-template <bool kLds, bool kCount, bool kPrimary>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
+template <bool kLds, bool kCount, bool kPrimary, bool kW4>
+__global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
@@ -576,7 +657,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
     }
     if (active) {
       const Ray r = make_ray(o, d);
-      hit = traverse<false, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 0.0f, tfar, ref, vc, s_stack);
+      hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
       if (!hit) {
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -817,7 +898,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // One thread per shadow record: any-hit test of each of its light tasks in light order; the
 // unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
-template <bool kLds, bool kCount>
+template <bool kLds, bool kCount, bool kW4>
 __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
@@ -849,8 +930,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
       float tfar = a.w;
       uint32_t ref = kNoHit;
       ++rays;
-      const bool occ =
-          traverse<true, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, 1e-4f, tfar, ref, vc, s_stack);
+      const bool occ = traverse_w<kW4, true, kCount>(sc, sv, r, 1e-4f, tfar, ref, vc, s_stack);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
         any = true;
@@ -931,6 +1011,7 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
                                                   const float* rays, uint32_t n, int anyhit, uint32_t* ref_out,
                                                   float* t_out, float* ng_out, uint8_t* occ) {
   __shared__ LdsStack s_stack;
+  const Staged sg{sv.nodes, sv.nodes4, sv.prim_ref, sv.tris, sv.sph};
   Visits vc;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
     const float* rr = rays + (size_t)i * 8;
@@ -938,13 +1019,14 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
     float tfar = rr[7];
     uint32_t ref = kNoHit;
     if (anyhit) {
-      occ[i] = traverse<true, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc, s_stack)
+      occ[i] = (sv.width == 4u ? traverse_w<true, true, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
+                               : traverse_w<false, true, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack))
                    ? 1
                    : 0;
       continue;
     }
-    const bool hit =
-        traverse<false, false>(sv.nodes, sv.prim_ref, sv.tris, sv.sph, sv.root, r, rr[6], tfar, ref, vc, s_stack);
+    const bool hit = sv.width == 4u ? traverse_w<true, false, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
+                                    : traverse_w<false, false, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack);
     // report (type bit | original primitive index) so the host can map to (geomID, primID)
     ref_out[i] = hit ? ((ref & kSphereBit) | ((ref & kSphereBit) ? sph_orig[ref & kIndexMask] : tri_orig[ref & kIndexMask]))
                      : kNoHit;
@@ -1031,6 +1113,7 @@ static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
 SceneView scene_view(const Context& c) {
   SceneView s;
   s.nodes = static_cast<const BvhNode*>(c.nodes.p);
+  s.nodes4 = static_cast<const Bvh4Node*>(c.nodes4.p);
   s.tris = static_cast<const float4*>(c.tris.p);
   s.sph = static_cast<const float4*>(c.sph.p);
   s.tri_geom = static_cast<const uint32_t*>(c.tri_geom.p);
@@ -1039,8 +1122,16 @@ SceneView scene_view(const Context& c) {
   s.num_tris = c.num_tris;
   s.num_sph = c.num_sph;
   s.root = c.root;
+  s.num_nodes4 = c.num_nodes4;
+  s.root4 = c.root4;
+  // width 0 = automatic: BVH2 for LDS-staged scenes (3-20 nodes: the extra slab tests of a BVH4
+  // node cost more than the saved steps), BVH4 for everything traversed from L2/HBM
+  const uint64_t bytes2 = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
+                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
+  s.width = c.bvh_width ? c.bvh_width : (bytes2 <= kLdsSceneBytes ? 2u : 4u);
   s.prim_ref = static_cast<const uint32_t*>(c.prim_ref.p);
-  const uint64_t bytes = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
+  const uint64_t node_bytes = s.width == 4u ? (uint64_t)c.num_nodes4 * sizeof(Bvh4Node) : (uint64_t)c.num_nodes * 64;
+  const uint64_t bytes = node_bytes + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
   return s;
@@ -1055,21 +1146,27 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
   const bool P = depth == 0;
+  const bool W = sv.width == 4u;
   const unsigned lb = trace_lds(sv, L, P, nseg);
   const EnvView ev = sh.env;
   unsigned g = 0;
-#define SPTR_TRACE(Lc, C, Pc)                                                                       \
+#define SPTR_TRACE(Lc, C, Pc, Wc)                                                                   \
   do {                                                                                              \
-    g = resident_grid((const void*)&k_trace<Lc, C, Pc>, lb);                                        \
-    hipLaunchKernelGGL((k_trace<Lc, C, Pc>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);         \
+    g = resident_grid((const void*)&k_trace<Lc, C, Pc, Wc>, lb);                                    \
+    hipLaunchKernelGGL((k_trace<Lc, C, Pc, Wc>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);     \
+  } while (0)
+#define SPTR_TRACE_W(Lc, C, Pc) \
+  do {                          \
+    if (W) SPTR_TRACE(Lc, C, Pc, true); else SPTR_TRACE(Lc, C, Pc, false); \
   } while (0)
   if (P) {
-    if (L) { if (count) SPTR_TRACE(true, true, true); else SPTR_TRACE(true, false, true); }
-    else   { if (count) SPTR_TRACE(false, true, true); else SPTR_TRACE(false, false, true); }
+    if (L) { if (count) SPTR_TRACE_W(true, true, true); else SPTR_TRACE_W(true, false, true); }
+    else   { if (count) SPTR_TRACE_W(false, true, true); else SPTR_TRACE_W(false, false, true); }
   } else {
-    if (L) { if (count) SPTR_TRACE(true, true, false); else SPTR_TRACE(true, false, false); }
-    else   { if (count) SPTR_TRACE(false, true, false); else SPTR_TRACE(false, false, false); }
+    if (L) { if (count) SPTR_TRACE_W(true, true, false); else SPTR_TRACE_W(true, false, false); }
+    else   { if (count) SPTR_TRACE_W(false, true, false); else SPTR_TRACE_W(false, false, false); }
   }
+#undef SPTR_TRACE_W
 #undef SPTR_TRACE
   return g;
 }
@@ -1092,15 +1189,21 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
                        uint32_t nseg, hipStream_t s) {
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
+  const bool W = sv.width == 4u;
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
-#define SPTR_SHADOW(Lc, C)                                                                          \
+#define SPTR_SHADOW(Lc, C, Wc)                                                                      \
   do {                                                                                              \
-    g = resident_grid((const void*)&k_shadow<Lc, C>, lb);                                           \
-    hipLaunchKernelGGL((k_shadow<Lc, C>), dim3(g), b, lb, s, sv, sh, w, depth, nseg);               \
+    g = resident_grid((const void*)&k_shadow<Lc, C, Wc>, lb);                                       \
+    hipLaunchKernelGGL((k_shadow<Lc, C, Wc>), dim3(g), b, lb, s, sv, sh, w, depth, nseg);           \
   } while (0)
-  if (L) { if (count) SPTR_SHADOW(true, true); else SPTR_SHADOW(true, false); }
-  else   { if (count) SPTR_SHADOW(false, true); else SPTR_SHADOW(false, false); }
+#define SPTR_SHADOW_W(Lc, C) \
+  do {                       \
+    if (W) SPTR_SHADOW(Lc, C, true); else SPTR_SHADOW(Lc, C, false); \
+  } while (0)
+  if (L) { if (count) SPTR_SHADOW_W(true, true); else SPTR_SHADOW_W(true, false); }
+  else   { if (count) SPTR_SHADOW_W(false, true); else SPTR_SHADOW_W(false, false); }
+#undef SPTR_SHADOW_W
 #undef SPTR_SHADOW
   return g;
 }

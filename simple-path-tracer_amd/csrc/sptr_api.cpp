@@ -286,8 +286,15 @@ int sptr_set_debug_mode(sptr_ctx* x, int mode) {
 
 int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   if (!x) return SPTR_ERR_INVALID;
-  if (n < 1 || n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 1..32");
+  if (n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 0 (automatic) or 1..32");
   x->c.leaf_size = n;
+  return SPTR_OK;
+}
+
+int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (width != 0 && width != 2 && width != 4) return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or 4");
+  x->c.bvh_width = width;
   return SPTR_OK;
 }
 
@@ -345,10 +352,12 @@ int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
   out->num_tris = c.num_tris;
   out->num_spheres = c.num_sph;
   out->num_nodes = c.num_nodes;
-  out->leaf_size = c.leaf_size;
+  out->leaf_size = c.leaf_used;
   out->bvh_depth = c.bvh_depth;
   out->lds_bytes = sv.lds_bytes;
-  out->node_bytes = (uint64_t)c.num_nodes * sizeof(BvhNode);
+  out->bvh_width = sv.width;
+  out->num_nodes = sv.width == 4u ? c.num_nodes4 : c.num_nodes;
+  out->node_bytes = sv.width == 4u ? (uint64_t)c.num_nodes4 * sizeof(Bvh4Node) : (uint64_t)c.num_nodes * sizeof(BvhNode);
   out->tri_bytes = (uint64_t)c.num_tris * 48u;
   out->sphere_bytes = (uint64_t)c.num_sph * 16u;
   out->prim_ref_bytes = ((uint64_t)c.num_tris + c.num_sph) * 4u;

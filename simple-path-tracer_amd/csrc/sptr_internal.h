@@ -50,6 +50,16 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node size");
 
+// BVH4 node, 128 B (one cache line): four child boxes stored SoA so the four slab tests vectorise,
+// four child links (BVH4 node index, leaf range, or kNoHit for an empty slot).  Built by collapsing
+// the LBVH: the BVH2 nodes at even depth become BVH4 nodes whose children are their grandchildren.
+struct Bvh4Node {
+  float4 lox, hix, loy, hiy, loz, hiz;
+  uint4 link;
+  uint4 meta;  // parent (BVH4 index), child count, -, -
+};
+static_assert(sizeof(Bvh4Node) == 128, "node size");
+
 struct DevMaterial {  // == sptr_material
   float albedo[3];
   float metallic;
@@ -70,12 +80,15 @@ struct DevLight {  // host-precomputed per Light::getRadiance (Light.cpp:43-79)
 
 struct SceneView {
   const BvhNode* nodes;
+  const Bvh4Node* nodes4;  // used when width == 4
   const uint32_t* prim_ref;  // sorted primitive refs (leaf ranges index this)
   const float4* tris;  // 3 float4 per sorted triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z Ng.xyz
   const float4* sph;   // sorted spheres: c.xyz r
   const uint32_t* tri_geom;  // geomID per sorted triangle
   const uint32_t* sph_geom;  // geomID per sorted sphere
   uint32_t num_nodes, num_tris, num_sph, root;
+  uint32_t num_nodes4, root4;
+  uint32_t width;      // 2: BVH2 traversal, 4: BVH4 traversal
   uint32_t lds_bytes;  // 0: traverse from global memory
 };
 
@@ -152,8 +165,12 @@ struct Context {
   uint64_t wave_paths = 0;  // 0 = default
   // scene
   DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
-  uint32_t leaf_size = 4;  // max primitives per BVH leaf range (1..32)
+  uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..32); 0 = automatic
+  uint32_t bvh_width = 0;  // traversal width: 2 (LBVH as built), 4 (collapsed), 0 = automatic
+  uint32_t leaf_used = 0;  // leaf size the current BVH was built with
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
+  uint32_t num_nodes4 = 0, root4 = 0;
+  DevBuf nodes4;
   uint32_t num_tri_geoms = 0;
   std::vector<uint32_t> geom_first;     // host copy for primID derivation
   std::vector<uint32_t> geom_material;  // host copy

@@ -82,7 +82,7 @@ class SceneLayout(C.Structure):
     _fields_ = [("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_nodes", C.c_uint32),
                 ("leaf_size", C.c_uint32), ("bvh_depth", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("node_bytes", C.c_uint64), ("tri_bytes", C.c_uint64), ("sphere_bytes", C.c_uint64),
-                ("prim_ref_bytes", C.c_uint64)]
+                ("prim_ref_bytes", C.c_uint64), ("bvh_width", C.c_uint32), ("pad", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -93,7 +93,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_read_rgb8",
     "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
@@ -121,6 +121,7 @@ def lib() -> C.CDLL:
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
+        "sptr_set_bvh_width": (C.c_int, [vp, u32]),
         "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
         "sptr_set_materials": (C.c_int, [vp, C.POINTER(Material), u32]),
         "sptr_set_lights": (C.c_int, [vp, C.POINTER(Light), u32]),
@@ -379,6 +380,9 @@ class Renderer:
 
     def set_leaf_size(self, n: int):
         self._check(self._L.sptr_set_leaf_size(self._h, n), "set_leaf_size")
+
+    def set_bvh_width(self, n: int):
+        self._check(self._L.sptr_set_bvh_width(self._h, n), "set_bvh_width")
 
     def set_debug_mode(self, m: int):
         self._check(self._L.sptr_set_debug_mode(self._h, m), "set_debug_mode")

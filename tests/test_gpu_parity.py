@@ -255,5 +255,30 @@ def test_leaf_size_invariance(renderer, leaf):
         renderer.render(cam, W, H, spp=3)
         acc = renderer.read_accum()
     finally:
-        renderer.set_leaf_size(4)
+        renderer.set_leaf_size(0)
     assert np.array_equal(acc.view(np.uint32), ref_acc.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])
+def test_bvh_width_invariance(renderer, scene, p0, p1):
+    """BVH2 (the LBVH as built) and the collapsed BVH4 return the same hits and the same image."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    rays = _random_rays(20000, 11)
+    out = {}
+    try:
+        for width in (2, 4):
+            renderer.set_bvh_width(width)
+            sptr.setup_default(renderer, scene, p0, p1)
+            info = renderer.scene_layout()
+            assert info["bvh_width"] == width
+            renderer.render(cam, W, H, spp=3)
+            out[width] = (renderer.read_accum().copy(), renderer.intersect(rays), info)
+    finally:
+        renderer.set_bvh_width(0)
+    (a2, (g2, p2, t2, _), i2), (a4, (g4, p4, t4, _), i4) = out[2], out[4]
+    assert i4["num_nodes"] < i2["num_nodes"]
+    assert ((g2 == g4) & (p2 == p4)).mean() >= 0.9999
+    assert np.array_equal(t2[g2 == g4].view(np.uint32), t4[g2 == g4].view(np.uint32))
+    same = (a2 == a4).all(axis=2).mean()
+    assert same >= 0.999
