@@ -1,0 +1,59 @@
+// cr_math.h — correctly rounded f32 sqrt, reciprocal and division by a loop-invariant divisor,
+// for the operand ranges the path tracer uses, without the denormal pre-scaling, VCC scaling and
+// special-case fix-ups of the compiler's general gfx950 expansions.
+//
+// Each helper replays the compiler's own correction sequence (v_sqrt + the +-1 ulp residual test;
+// v_rcp + the Newton/Markstein fma chain of v_div_scale/v_div_fmas/v_div_fixup), so for in-range
+// operands the result is bit-identical to sqrtf(x), 1.0f / x and a / b.  That claim is checked
+// exhaustively on the GPU (every float of the ranges below) by tests/hip/crmath_check.hip, run by
+// tests/test_gpu_crmath.py.  Callers guard the range and fall back to the IEEE operators.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace sptr {
+
+constexpr float kCrLo = 0x1p-96f;  // sqrt_nrm domain: [kCrLo, kCrHi]
+constexpr float kCrHi = 0x1p100f;
+
+// sqrtf(x) for x in [2^-96, FLT_MAX]
+__device__ __forceinline__ float sqrt_nrm(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float em = __builtin_fmaf(-sm, s, x);
+  const float ep = __builtin_fmaf(-sp, s, x);
+  float r = (0.0f >= em) ? sm : s;
+  r = (0.0f < ep) ? sp : r;
+  return r;
+}
+
+// 1.0f / y for y in [2^-100, 2^100]
+__device__ __forceinline__ float rcp_nrm(float y) {
+  const float r0 = __builtin_amdgcn_rcpf(y);
+  const float r1 = __builtin_fmaf(__builtin_fmaf(-y, r0, 1.0f), r0, r0);
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-y, r1, 1.0f), r1, r1);
+  return __builtin_fmaf(__builtin_fmaf(-y, q1, 1.0f), r1, q1);
+}
+
+// Loop-invariant divisor b (|b| in [2^-100, 2^100]): the refined reciprocal is computed once.
+struct DivBy {
+  float b, r;
+};
+__device__ __forceinline__ DivBy div_by(float b) {
+  const float r0 = __builtin_amdgcn_rcpf(b);
+  return DivBy{b, __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0)};
+}
+// a / d.b for a = 0 or |a| in [2^-100, 2^100] with the quotient in the normal range
+__device__ __forceinline__ float div_nrm(float a, const DivBy& d) {
+  const float q0 = a * d.r;
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-d.b, q0, a), d.r, q0);
+  return __builtin_fmaf(__builtin_fmaf(-d.b, q1, a), d.r, q1);
+}
+
+// 1 / sqrt(l2) as glm's normalize evaluates it (two correctly rounded operations)
+__device__ __forceinline__ float inv_len(float l2) {
+  if (l2 >= kCrLo && l2 <= kCrHi) return rcp_nrm(sqrt_nrm(l2));
+  return 1.0f / sqrtf(l2);
+}
+
+}  // namespace sptr

@@ -487,7 +487,13 @@ struct Primary {
   vec3 d;
   uint32_t rng;
 };
-__device__ __forceinline__ bool primary_path(const FrameView& f, uint32_t p, Primary& out) {
+// dW, dH: the image width and height as loop-invariant divisors (cr_math.h; (x + jx) / W stays
+// correctly rounded, with the divisor's reciprocal refined once per thread instead of per path).
+struct ImageDiv {
+  DivBy w, h;
+};
+__device__ __forceinline__ ImageDiv image_div(const FrameView& f) { return ImageDiv{div_by(float(f.W)), div_by(float(f.H))}; }
+__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
   const uint32_t s = fast_div(f.div_P, p), l = p - s * f.P;
   int x, y;
   if (!local_pixel(f, l, x, y)) return false;
@@ -496,7 +502,7 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, uint32_t p, Pri
   uint32_t r = wang_hash(ps ^ acc * 9781u);
   const float jx = rand01(r);
   const float jy = rand01(r);
-  const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
+  const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, dv.w), div_nrm(float(y) + jy, dv.h));
   out.d = safe_normalize(dir);
   out.rng = wang_hash((ps ^ acc) ^ 1u);
   return true;
@@ -631,6 +637,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+  const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
   Visits vc;
   const Sched sd = block_sched(n);
@@ -644,7 +651,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (kPrimary) {
         Primary pr;
         id = pid = i;
-        active = primary_path(f, i, pr);
+        active = primary_path(f, idiv, i, pr);
         o = f.cam_pos;
         d = pr.d;
       } else {
@@ -702,6 +709,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 
   const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
+  const ImageDiv idiv = image_div(f);
   const uint32_t ts = w.tstride, L = w.L;
   const Sched sd = block_sched(n);
   for (uint32_t base = sd.first; base < n; base += sd.step) {
@@ -716,7 +724,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       if (kPrimary) {
         Primary pr;
         p = h.x;
-        primary_path(f, p, pr);
+        primary_path(f, idiv, p, pr);
         ro = f.cam_pos;
         rd = pr.d;
         thr = v3(1.0f, 1.0f, 1.0f);
@@ -1051,6 +1059,7 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
 
 __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, uint32_t* rng) {
   const uint32_t N = (uint32_t)f.W * (uint32_t)f.H;
+  const ImageDiv idiv = image_div(f);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += grid_threads()) {
     const int x = (int)(i % (uint32_t)f.W), y = (int)(i / (uint32_t)f.W);
     const uint32_t acc = f.acc0;
@@ -1058,7 +1067,7 @@ __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, ui
     uint32_t r = wang_hash(ps ^ acc * 9781u);
     const float jx = rand01(r);
     const float jy = rand01(r);
-    const vec3 dir = camera_dir(f, (float(x) + jx) / float(f.W), (float(y) + jy) / float(f.H));
+    const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, idiv.w), div_nrm(float(y) + jy, idiv.h));  // as primary_path
     const vec3 d = safe_normalize(dir);
     dirs[(size_t)i * 3 + 0] = d.x;
     dirs[(size_t)i * 3 + 1] = d.y;

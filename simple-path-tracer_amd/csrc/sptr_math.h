@@ -12,6 +12,8 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
+
+#include "cr_math.h"
 #define SPTR_HD __host__ __device__ __forceinline__
 #else
 #include <cmath>
@@ -50,11 +52,18 @@ SPTR_HD float sq_root(float x) { return sqrtf(x); }
 #else
 inline float sq_root(float x) { return std::sqrt(x); }
 #endif
-SPTR_HD vec3 normalize(vec3 v) { return v * (1.0f / sq_root(dot(v, v))); }
+// 1/sqrt(l2) with both operations correctly rounded.  Device code uses the short correction
+// sequences of cr_math.h (bit-identical in range, verified exhaustively on gfx950).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float inv_length(float l2) { return inv_len(l2); }
+#else
+SPTR_HD float inv_length(float l2) { return 1.0f / sq_root(l2); }
+#endif
+SPTR_HD vec3 normalize(vec3 v) { return v * inv_length(dot(v, v)); }
 SPTR_HD vec3 safe_normalize(vec3 v) {
   const float l2 = dot(v, v);
   if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
-  return v * (1.0f / sq_root(l2));
+  return v * inv_length(l2);
 }
 
 SPTR_HD uint32_t wang_hash(uint32_t a) {
