@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
+    ap.add_argument("--stage-timing", action="store_true",
+                    help="HIP events around every stage (default: around the k_trace launches only, which the "
+                         "roofline needs; events between the other stages would add dispatch gaps)")
     args = ap.parse_args()
     wl = workloads.WORKLOADS[args.workload]
     W, H = wl.width, wl.height
@@ -144,8 +147,17 @@ def main():
     gathered = torch.zeros(world * tiles_per_rank * 1024, dtype=torch.int32, device=dev)
     image = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev)
 
+    # a real stream (torch's default is the legacy null stream, which the library's non-blocking
+    # streams do not order against): render, copy, gather and unpack all run on it
+    torch_stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(torch_stream)
+    stream = torch_stream.cuda_stream
+
     def step(flags=0):
-        st = r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=rank, shard_count=world, flags=flags)
+        # every stage of a step is enqueued on torch's current stream, with no host synchronisation:
+        # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL all-gather -> rank-0 unpack
+        r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=rank, shard_count=world,
+                 flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
         send[: local_tiles.numel()].copy_(local_tiles)
@@ -154,24 +166,27 @@ def main():
         else:
             gathered.copy_(send)
         if rank == 0:
-            torch.cuda.current_stream().synchronize()
-            r.unpack_tiles(gathered.data_ptr(), world, tiles_per_rank, W, H, image.data_ptr())
-        return st
+            r.unpack_tiles(gathered.data_ptr(), world, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
 
     for _ in range(args.warmup):
         step()
+    r.collect_stats()
     # untimed instrumented pass: BVH node / primitive fetch counts for the algorithmic-bytes model
-    cnt = step(sptr.SPTR_FRAME_COUNT_VISITS)
+    step(sptr.SPTR_FRAME_COUNT_VISITS)
+    cnt = r.collect_stats()
 
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step(sptr.SPTR_FRAME_TIMING) for _ in range(args.steps)]
+    timing = sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE
+    for _ in range(args.steps):
+        step(timing)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    stats = [r.collect_stats()]  # the K timed steps' counters and stage events, summed
 
     rays = sum(s.rays_closest + s.rays_shadow for s in stats)
     samples = sum(s.samples for s in stats)
@@ -184,8 +199,9 @@ def main():
         elapsed, rays, samples = float(tmax[0]), float(tsum[1]), float(tsum[2])
 
     if rank == 0:
-        stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / len(stats), 3)
-                    for k in ("trace0", "trace", "shade0", "shade", "shadow", "accum")}
+        stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
+                    for k in (("trace0", "trace", "shade0", "shade", "shadow", "accum") if args.stage_timing
+                              else ("trace0", "trace"))}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),

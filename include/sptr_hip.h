@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 1
+#define SPTR_ABI_VERSION 2
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -105,7 +105,11 @@ typedef struct sptr_camera {
 enum sptr_frame_flags {
   SPTR_FRAME_TIMING = 1u,     /* record per-stage HIP events (adds sync at the end of the call) */
   SPTR_FRAME_NO_RESOLVE = 2u, /* skip the tonemap/resolve pass */
-  SPTR_FRAME_COUNT_VISITS = 4u /* one instrumented trace pass: count BVH node / primitive fetches */
+  SPTR_FRAME_COUNT_VISITS = 4u, /* one instrumented trace pass: count BVH node / primitive fetches */
+  SPTR_FRAME_ASYNC = 8u, /* enqueue only: return without waiting; stats are left zero and the call's
+                            counters and stage times accumulate until sptr_collect_stats */
+  SPTR_FRAME_TIMING_TRACE = 16u /* HIP events around the trace launches only (ms_trace, ms_trace0,
+                                   trace_launches): the other stages run back to back */
 };
 
 /* One render call = `spp` progressive frames (samples per pixel) starting at accumulation index
@@ -169,9 +173,14 @@ typedef struct sptr_scene_layout {
 int sptr_scene_layout_info(const sptr_ctx* ctx, sptr_scene_layout* out);
 
 /* ---- rendering ---------------------------------------------------------------------------------- */
-/* Renders on the context's stream, or on `stream` (a hipStream_t) when not NULL; returns after the
- * work completes. */
+/* Renders on the context's stream, or on `stream` (a hipStream_t) when not NULL.  Returns after the
+ * work completes, with the stats of this call and of any SPTR_FRAME_ASYNC calls still uncollected;
+ * with SPTR_FRAME_ASYNC it only enqueues (consecutive asynchronous calls must use one stream).
+ * OptixBackend::render blocks three times per bounce (OptixBackend.cpp:1678-1789); asynchronous
+ * calls let a caller queue frames, the tile copy and the multi-GPU gather back to back. */
 int sptr_render(sptr_ctx* ctx, const sptr_frame* frame, void* stream, sptr_stats* stats);
+/* Wait for the uncollected render calls and return their summed stats (zero when there are none). */
+int sptr_collect_stats(sptr_ctx* ctx, sptr_stats* stats);
 /* Full image RGB8 (width*height*3; only this shard's tiles are written) and the linear accumulation
  * sums (width*height*3 floats: sum of samples, divide by the sample count for the mean). */
 int sptr_read_rgb8(sptr_ctx* ctx, uint8_t* rgb);
@@ -180,7 +189,8 @@ int sptr_read_accum(sptr_ctx* ctx, float* accum);
  * multi-GPU gather.  *bytes = local_tiles * 4096. */
 int sptr_tiles_device(sptr_ctx* ctx, void** dptr, size_t* bytes);
 /* Scatter gathered tile buffers (rank-major: rank r's local tiles at offset r*tiles_per_rank*4096
- * bytes) into an RGB8 device image width*height*3. */
+ * bytes) into an RGB8 device image width*height*3.  With stream == NULL it runs on the context's
+ * stream and waits; on a caller's stream it only enqueues. */
 int sptr_unpack_tiles(sptr_ctx* ctx, const void* gathered, int32_t shard_count, uint32_t tiles_per_rank,
                       int32_t width, int32_t height, void* rgb8_out, void* stream);
 

@@ -229,24 +229,19 @@ __device__ __forceinline__ float ld_agent(const float* p) {
 }
 
 // Each leaf walks up; at each node the first arriving child stops, the second merges both child
-// boxes (read back through agent-scope loads) and continues.  Also records the leaf depth.
+// boxes (read back through agent-scope loads) and continues.  Subtree heights travel up the same
+// way (the first arriver publishes its height in ht[node]), so the tree height — the deepest leaf,
+// which sizes the traversal stack — is the root's height, without a per-leaf walk to the root.
 __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const float4* bhi, const uint2* kids,
-                        const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* max_depth) {
+                        const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* ht,
+                        uint32_t* max_depth) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
     const uint32_t prim = vals[i];
     const float4 a = blo[prim], b = bhi[prim];
     float lo[3] = {a.x, a.y, a.z}, hi[3] = {b.x, b.y, b.z};
     uint32_t child = kLeafBit | (uint32_t)i;
     uint32_t par = leaf_parent[i];
-    // depth of this leaf (walk the parent chain)
-    {
-      uint32_t dep = 1, q = par;
-      while (q != 0u) {
-        q = nodes[q].link.z;
-        ++dep;
-      }
-      atomicMax(max_depth, dep);
-    }
+    uint32_t h = 0u;  // height of the subtree rooted at `child` (a primitive: 0)
     for (;;) {
       BvhNode* nd = nodes + par;
       const bool left = (kids[par].x == child);
@@ -259,18 +254,23 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
         st_agent(f + 4, lo[0]); st_agent(f + 5, hi[0]); st_agent(f + 6, lo[1]); st_agent(f + 7, hi[1]);
         st_agent(f + 10, lo[2]); st_agent(f + 11, hi[2]);
       }
+      __hip_atomic_fetch_max(ht + par, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t old = __hip_atomic_fetch_add(flags + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == 0u) break;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      h = __hip_atomic_load(ht + par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
       const float l0 = ld_agent(f + 0), l1 = ld_agent(f + 1), l2 = ld_agent(f + 2), l3 = ld_agent(f + 3);
       const float r0 = ld_agent(f + 4), r1 = ld_agent(f + 5), r2 = ld_agent(f + 6), r3 = ld_agent(f + 7);
       const float z0 = ld_agent(f + 8), z1 = ld_agent(f + 9), z2 = ld_agent(f + 10), z3 = ld_agent(f + 11);
       lo[0] = fminf(l0, r0); hi[0] = fmaxf(l1, r1);
       lo[1] = fminf(l2, r2); hi[1] = fmaxf(l3, r3);
       lo[2] = fminf(z0, z2); hi[2] = fmaxf(z1, z3);
-      if (par == 0u) break;
+      if (par == 0u) {
+        *max_depth = h;  // only the second arriver at the root gets here
+        break;
+      }
       child = par;
       par = nd->link.z;
     }
@@ -415,7 +415,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   uint32_t* cb = nullptr;
   uint64_t *keys = nullptr, *keys_s = nullptr;
   uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
-           *rflags = nullptr, *dmax = nullptr;
+           *rflags = nullptr, *dmax = nullptr, *ht = nullptr;
   uint2* kids = nullptr;
   LB_CHECK(tmp.alloc(&blo, N));
   LB_CHECK(tmp.alloc(&bhi, N));
@@ -429,6 +429,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(tmp.alloc(&kids, N));
   LB_CHECK(tmp.alloc(&leaf_parent, N));
   LB_CHECK(tmp.alloc(&rflags, N));
+  LB_CHECK(tmp.alloc(&ht, N));
   LB_CHECK(tmp.alloc(&dmax, 1));
   const uint32_t cb_init[8] = {~0u, ~0u, ~0u, 0u, 0u, 0u, 0u, 0u};
   LB_CHECK(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
@@ -468,10 +469,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
     LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
+    LB_CHECK(hipMemsetAsync(ht, 0, (size_t)N * 4, s));
     hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
                        leaf_parent);
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, kids, leaf_parent,
-                       nodes, rflags, dmax);
+                       nodes, rflags, ht, dmax);
     LB_CHECK(hipGetLastError());
     uint32_t dep = 0;
     LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));

@@ -190,42 +190,101 @@ ShadeView shade_view(const Context& c) {
   return s;
 }
 
-struct StageTimer {  // per-stage HIP events on the render stream (SPTR_FRAME_TIMING)
-  bool on = false;
-  hipStream_t s = nullptr;
-  std::vector<hipEvent_t>* pool = nullptr;
-  std::vector<std::pair<int, size_t>> marks;  // (stage, index of begin event)
-  size_t used = 0;
-  hipEvent_t next() {
-    if (used == pool->size()) {
-      hipEvent_t e;
-      (void)hipEventCreate(&e);
-      pool->push_back(e);
+// Stage events on the render stream, kept in the context's pool until collected.  Stages: 0 whole
+// render call (always recorded), 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum +
+// resolve, 5 trace bounce 0 (raygen fused), 6 shade bounce 0, 7 tail; 1-7 only with
+// SPTR_FRAME_TIMING.
+constexpr int kStages = 8;
+struct StageTimer {
+  Context& c;
+  bool on;                  // SPTR_FRAME_TIMING or SPTR_FRAME_TIMING_TRACE
+  bool trace_only;          // SPTR_FRAME_TIMING_TRACE alone: stages 1 and 5 only
+  hipStream_t s;
+  hipError_t err = hipSuccess;
+  size_t open = SIZE_MAX;   // index in c.marks of the stage being recorded
+  size_t call = SIZE_MAX;   // index in c.marks of this call's stage-0 span
+  size_t next() {
+    if (c.events_used == c.events.size()) {
+      hipEvent_t e = nullptr;
+      const hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) {
+        if (err == hipSuccess) err = r;
+        return SIZE_MAX;
+      }
+      c.events.push_back(e);
     }
-    return (*pool)[used++];
+    const size_t i = c.events_used++;
+    if (err == hipSuccess) err = hipEventRecord(c.events[i], s);
+    return i;
   }
   void begin(int stage) {
-    if (!on) return;
-    marks.push_back({stage, used});
-    (void)hipEventRecord(next(), s);
+    if (!on || (trace_only && stage != 1 && stage != 5)) return;
+    open = c.marks.size();
+    c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
   void end() {
-    if (!on) return;
-    (void)hipEventRecord(next(), s);
+    if (open == SIZE_MAX) return;
+    c.marks[open].e = next();
+    open = SIZE_MAX;
   }
-  // stages: 0 unused, 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum + resolve,
-  //         5 trace bounce 0 (raygen fused), 6 shade bounce 0
-  void collect(double ms[7], uint64_t& trace_launches) {
-    for (auto& m : marks) {
-      float t = 0.0f;
-      (void)hipEventElapsedTime(&t, (*pool)[m.second], (*pool)[m.second + 1]);
-      ms[m.first] += t;
-      if (m.first == 1 || m.first == 5) ++trace_launches;
-    }
-    marks.clear();
-    used = 0;
+  void begin_call() {
+    call = c.marks.size();
+    c.marks.push_back(StageMark{0, next(), SIZE_MAX});
   }
+  void end_call() { c.marks[call].e = next(); }
 };
+
+// Wait for the pending render calls, fold their device counters and stage events into *stats
+// (may be null) and start a new collection window.
+int collect_pending(Context& c, sptr_stats* stats) {
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (c.pending == 0) return SPTR_OK;
+  const hipError_t se = hipStreamSynchronize(c.pending_stream);
+  double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t trace_launches = 0;
+  for (const StageMark& m : c.marks) {
+    float t = 0.0f;
+    if (se == hipSuccess && m.b < c.events.size() && m.e < c.events.size())
+      (void)hipEventElapsedTime(&t, c.events[m.b], c.events[m.e]);
+    ms[m.stage] += t;
+    if (m.stage == 1 || m.stage == 5) ++trace_launches;
+  }
+  c.marks.clear();
+  c.events_used = 0;
+  const uint64_t samples = c.pending_samples, waves = c.pending_waves;
+  c.pending = 0;
+  c.pending_samples = c.pending_waves = 0;
+  if (se != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: ") + hipGetErrorString(se));
+  unsigned long long tot[kTotWords];
+  API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
+  if (tot[kTotOverflow]) return fail(c, SPTR_ERR_HIP, "render: segmented stream overflow (internal error)");
+  if (!stats) return SPTR_OK;
+  stats->ms_total = ms[0];
+  stats->ms_raygen = 0.0;  // raygen is fused into the bounce-0 trace (ms_trace0)
+  stats->ms_trace = ms[1] + ms[5];
+  stats->ms_shade = ms[2] + ms[6];
+  stats->ms_trace0 = ms[5];
+  stats->ms_shade0 = ms[6];
+  stats->ms_shadow = ms[3];
+  stats->ms_accum = ms[4];
+  stats->trace_launches = trace_launches;
+  stats->rays_closest = tot[kTotClosest];
+  stats->rays_shadow = tot[kTotShadow];
+  stats->samples = samples;
+  stats->waves = waves;
+  stats->node_visits = tot[kTotNodes];
+  stats->tri_tests = tot[kTotTris];
+  stats->sphere_tests = tot[kTotSph];
+  stats->shadow_node_visits = tot[kTotShNodes];
+  stats->shadow_prim_tests = tot[kTotShPrims];
+  return SPTR_OK;
+}
+
+// Device work of the pending render calls must be complete before a host read of their results.
+int sync_pending(Context& c) {
+  if (c.pending) API_HIP(hipStreamSynchronize(c.pending_stream));
+  return SPTR_OK;
+}
 
 }  // namespace
 }  // namespace sptr
@@ -263,6 +322,7 @@ int sptr_destroy(sptr_ctx* x) {
   if (!x) return SPTR_ERR_INVALID;
   Context& c = x->c;
   (void)hipSetDevice(c.device);
+  if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
   (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_hrec, &c.w_rad,   &c.w_stask,
@@ -308,6 +368,7 @@ int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
 int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
   if (!x || !s) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
   API_HIP(hipSetDevice(c.device));
   if ((s->num_tris && (!s->indices || !s->positions || !s->tri_geom_first)) || (s->num_spheres && !s->spheres) ||
       ((s->num_tri_geoms + s->num_spheres) && !s->geom_material))
@@ -367,6 +428,7 @@ int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
 int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
   if (!x || (n && !m)) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
   if (n == 0) return fail(c, SPTR_ERR_INVALID, "at least one material is required");
   API_HIP(hipSetDevice(c.device));
   c.mats_host.resize(n);
@@ -402,6 +464,7 @@ int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
 int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
   if (!x) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
   API_HIP(hipSetDevice(c.device));
   if (!e || !e->faces) {
     free_buf(c.env);
@@ -456,21 +519,18 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   if (rc != SPTR_OK) return rc;
 
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  if (c.pending && s != c.pending_stream)
+    return fail(c, SPTR_ERR_INVALID, "render: asynchronous renders must stay on one stream until sptr_collect_stats");
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
   const WaveView w = wave_view(c);
   FrameView fv = frame_view(c, *f);
   const bool timing = (f->flags & SPTR_FRAME_TIMING) != 0;
   const bool count = (f->flags & SPTR_FRAME_COUNT_VISITS) != 0;
-  StageTimer tm;
-  tm.on = timing;
-  tm.s = s;
-  tm.pool = &c.events;
-  hipEvent_t e_begin, e_end;
-  API_HIP(hipEventCreate(&e_begin));
-  API_HIP(hipEventCreate(&e_end));
-  API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
-  API_HIP(hipEventRecord(e_begin, s));
+  const bool trace_timing = (f->flags & SPTR_FRAME_TIMING_TRACE) != 0;
+  StageTimer tm{c, timing || trace_timing, !timing, s};
+  if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+  tm.begin_call();
   uint32_t done = 0, waves = 0;
   const int D = (int)f->max_depth;
   while (done < f->spp) {
@@ -505,49 +565,32 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
                    static_cast<uint8_t*>(c.image.p), s);
     tm.end();
   }
+  tm.end_call();
   API_HIP(hipGetLastError());
-  API_HIP(hipEventRecord(e_end, s));
-  API_HIP(hipEventSynchronize(e_end));
+  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
   c.last_samples = total;
-  unsigned long long tot[kTotWords];
-  API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
-  if (tot[kTotOverflow]) return fail(c, SPTR_ERR_HIP, "render: segmented stream overflow (internal error)");
-  if (stats) {
-    std::memset(stats, 0, sizeof(*stats));
-    float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, e_begin, e_end);
-    stats->ms_total = ms;
-    double st[7] = {0, 0, 0, 0, 0, 0, 0};
-    tm.collect(st, stats->trace_launches);
-    stats->ms_raygen = 0.0;  // raygen is fused into the bounce-0 trace (ms_trace0)
-    stats->ms_trace = st[1] + st[5];
-    stats->ms_shade = st[2] + st[6];
-    stats->ms_trace0 = st[5];
-    stats->ms_shade0 = st[6];
-    stats->ms_shadow = st[3];
-    stats->ms_accum = st[4];
-    stats->rays_closest = tot[kTotClosest];
-    stats->rays_shadow = tot[kTotShadow];
-    stats->samples = (uint64_t)fv.valid * f->spp;
-    stats->waves = waves;
-    stats->node_visits = tot[kTotNodes];
-    stats->tri_tests = tot[kTotTris];
-    stats->sphere_tests = tot[kTotSph];
-    stats->shadow_node_visits = tot[kTotShNodes];
-    stats->shadow_prim_tests = tot[kTotShPrims];
-  } else {
-    double st[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint64_t tl = 0;
-    tm.collect(st, tl);
+  ++c.pending;
+  c.pending_stream = s;
+  c.pending_samples += (uint64_t)fv.valid * f->spp;
+  c.pending_waves += waves;
+  if (f->flags & SPTR_FRAME_ASYNC) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    return SPTR_OK;
   }
-  (void)hipEventDestroy(e_begin);
-  (void)hipEventDestroy(e_end);
-  return SPTR_OK;
+  return collect_pending(c, stats);
+}
+
+int sptr_collect_stats(sptr_ctx* x, sptr_stats* stats) {
+  if (!x) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  return collect_pending(c, stats);
 }
 
 int sptr_read_rgb8(sptr_ctx* x, uint8_t* rgb) {
   if (!x || !rgb) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
   if (!c.image.p) return fail(c, SPTR_ERR_NO_SCENE, "read_rgb8: nothing rendered");
   API_HIP(hipSetDevice(c.device));
   API_HIP(hipMemcpy(rgb, c.image.p, (size_t)c.W * c.H * 3, hipMemcpyDeviceToHost));
@@ -557,6 +600,7 @@ int sptr_read_rgb8(sptr_ctx* x, uint8_t* rgb) {
 int sptr_read_accum(sptr_ctx* x, float* out) {
   if (!x || !out) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
   if (!c.accum.p) return fail(c, SPTR_ERR_NO_SCENE, "read_accum: nothing rendered");
   API_HIP(hipSetDevice(c.device));
   std::vector<float> a((size_t)c.P * 4);
@@ -592,7 +636,7 @@ int sptr_unpack_tiles(sptr_ctx* x, const void* gathered, int32_t G, uint32_t tpr
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
   launch_unpack(static_cast<const uint32_t*>(gathered), G, tpr, W, H, static_cast<uint8_t*>(out), s);
   API_HIP(hipGetLastError());
-  API_HIP(hipStreamSynchronize(s));
+  if (!stream) API_HIP(hipStreamSynchronize(s));  // on a caller's stream the call only enqueues
   return SPTR_OK;
 }
 
@@ -601,6 +645,7 @@ static int run_query(sptr_ctx* x, const float* rays, uint32_t n, bool anyhit, ui
   if (!x || (n && !rays)) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "query: no scene");
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
   if (n == 0) return SPTR_OK;
   API_HIP(hipSetDevice(c.device));
   const size_t rb = (size_t)n * 32, refb = (size_t)n * 4, tb = (size_t)n * 4, nb = (size_t)n * 12, ob = (size_t)n;
@@ -656,6 +701,7 @@ int sptr_primary_rays(sptr_ctx* x, const sptr_camera* cam, int32_t W, int32_t H,
                       uint32_t* rng) {
   if (!x || !cam || W <= 0 || H <= 0 || !dirs || !rng) return SPTR_ERR_INVALID;
   Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
   API_HIP(hipSetDevice(c.device));
   sptr_frame f{};
   f.width = W;

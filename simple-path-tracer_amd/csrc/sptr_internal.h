@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "sptr_hip.h"
@@ -157,6 +158,11 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+struct StageMark {
+  int stage;
+  size_t b, e;  // begin / end event indices in Context::events
+};
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -194,7 +200,14 @@ struct Context {
   uint32_t last_samples = 0;  // accumulation count after the last render
   // query scratch
   DevBuf qbuf;
-  std::vector<hipEvent_t> events;  // timing event pool
+  // Render calls whose counters and events are not yet collected (SPTR_FRAME_ASYNC): the device
+  // totals accumulate across them and the stage events stay in the pool until sptr_collect_stats.
+  std::vector<hipEvent_t> events;               // event pool
+  std::vector<StageMark> marks;                 // recorded stage spans (event pool indices)
+  size_t events_used = 0;
+  uint32_t pending = 0;                         // render calls since the last collection
+  hipStream_t pending_stream = nullptr;
+  uint64_t pending_samples = 0, pending_waves = 0;
 };
 
 // kernels_lbvh.hip

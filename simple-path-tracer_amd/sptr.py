@@ -21,6 +21,8 @@ LIB_PATH = os.environ.get("SPTR_LIB") or os.path.join(HERE, "libsptr_hip.so")  #
 SPTR_FRAME_TIMING = 1
 SPTR_FRAME_NO_RESOLVE = 2
 SPTR_FRAME_COUNT_VISITS = 4
+SPTR_FRAME_ASYNC = 8
+SPTR_FRAME_TIMING_TRACE = 16
 
 
 class SptrError(RuntimeError):
@@ -94,7 +96,8 @@ _lib = None
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
     "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
-    "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_read_rgb8",
+    "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
+    "sptr_read_rgb8",
     "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
     "sptr_host_builtin_scene", "sptr_host_scene_view", "sptr_host_scene_free", "sptr_host_camera_lookat",
@@ -129,6 +132,7 @@ def lib() -> C.CDLL:
         "sptr_scene_info": (C.c_int, [vp, up, up, up, C.POINTER(C.c_double)]),
         "sptr_scene_layout_info": (C.c_int, [vp, C.POINTER(SceneLayout)]),
         "sptr_render": (C.c_int, [vp, C.POINTER(Frame), vp, C.POINTER(Stats)]),
+        "sptr_collect_stats": (C.c_int, [vp, C.POINTER(Stats)]),
         "sptr_read_rgb8": (C.c_int, [vp, bp]),
         "sptr_read_accum": (C.c_int, [vp, fp]),
         "sptr_tiles_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
@@ -395,6 +399,12 @@ class Renderer:
         self._check(self._L.sptr_render(self._h, C.byref(f), C.c_void_p(stream) if stream else None, C.byref(st)),
                     "render")
         self.width, self.height = width, height
+        return st
+
+    def collect_stats(self) -> Stats:
+        """Wait for the SPTR_FRAME_ASYNC renders and return their summed stats."""
+        st = Stats()
+        self._check(self._L.sptr_collect_stats(self._h, C.byref(st)), "collect_stats")
         return st
 
     def read_rgb8(self) -> np.ndarray:

@@ -282,3 +282,22 @@ def test_bvh_width_invariance(renderer, scene, p0, p1):
     assert np.array_equal(t2[g2 == g4].view(np.uint32), t4[g2 == g4].view(np.uint32))
     same = (a2 == a4).all(axis=2).mean()
     assert same >= 0.999
+
+
+def test_async_renders_equal_sync(renderer):
+    """SPTR_FRAME_ASYNC calls only defer the wait: same image, and collected stats = the sum."""
+    sptr.setup_default(renderer, "default_emitter")
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    st1 = renderer.render(cam, W, H, spp=2)
+    st2 = renderer.render(cam, W, H, spp=3, frame_begin=3)
+    ref = renderer.read_accum().copy()
+    for fb, spp in ((1, 2), (3, 3)):
+        z = renderer.render(cam, W, H, spp=spp, frame_begin=fb, flags=sptr.SPTR_FRAME_ASYNC | sptr.SPTR_FRAME_TIMING)
+        assert z.rays_closest == 0  # stats are deferred
+    st = renderer.collect_stats()
+    assert np.array_equal(renderer.read_accum().view(np.uint32), ref.view(np.uint32))
+    assert st.rays_closest == st1.rays_closest + st2.rays_closest
+    assert st.rays_shadow == st1.rays_shadow + st2.rays_shadow
+    assert st.samples == W * H * 5 and st.ms_total > 0 and st.trace_launches > 0
+    assert renderer.collect_stats().rays_closest == 0  # window restarted
