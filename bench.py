@@ -55,7 +55,8 @@ def roofline(cnt, stats, layout, wl_name, steps):
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
     launches_per_step = max(1, launches // max(1, steps))
-    stream = STREAM_BYTES_PER_RAY * cnt.rays_closest
+    traced = cnt.rays_closest - cnt.rays_tail  # closest-hit queries of k_trace (the rest run in k_tail)
+    stream = STREAM_BYTES_PER_RAY * traced
     node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0  # 64 BVH2, 128 BVH4
     scene = node_b * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
     lds = layout["lds_bytes"] > 0
@@ -76,9 +77,9 @@ def roofline(cnt, stats, layout, wl_name, steps):
             "launches_per_step": launches_per_step,
             "scene_in_lds": lds,
             "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
-            "per_ray": {"nodes": round(cnt.node_visits / max(1, cnt.rays_closest), 3),
-                        "tris": round(cnt.tri_tests / max(1, cnt.rays_closest), 3),
-                        "spheres": round(cnt.sphere_tests / max(1, cnt.rays_closest), 3)}}
+            "per_ray": {"nodes": round(cnt.node_visits / max(1, traced), 3),
+                        "tris": round(cnt.tri_tests / max(1, traced), 3),
+                        "spheres": round(cnt.sphere_tests / max(1, traced), 3)}}
 
 
 def cpu_baseline(wl, flat, cam):
@@ -116,6 +117,10 @@ def main():
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
+    ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
+    ap.add_argument("--emulate-shards", type=int, default=0,
+                    help="timing experiment on one GPU: render only shard 0 of G (the per-rank work of a G-GPU run); "
+                         "the line is marked emulated and is not a G-GPU measurement")
     ap.add_argument("--stage-timing", action="store_true",
                     help="HIP events around every stage (default: around the k_trace launches only, which the "
                          "roofline needs; events between the other stages would add dispatch gaps)")
@@ -139,12 +144,16 @@ def main():
         r.set_leaf_size(args.leaf_size)
     if args.bvh_width:
         r.set_bvh_width(args.bvh_width)
+    if args.tail_depth:
+        r.set_tail_depth(args.tail_depth)
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
     cam = workloads.camera(wl)
-    tiles_per_rank = sptr.tiles_per_rank(W, H, world)
+    shards = args.emulate_shards if (args.emulate_shards and not distributed) else world
+    shard = 0 if args.emulate_shards else rank
+    tiles_per_rank = sptr.tiles_per_rank(W, H, shards)
     send = torch.zeros(tiles_per_rank * 1024, dtype=torch.int32, device=dev)
-    gathered = torch.zeros(world * tiles_per_rank * 1024, dtype=torch.int32, device=dev)
+    gathered = torch.zeros(shards * tiles_per_rank * 1024, dtype=torch.int32, device=dev)
     image = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev)
 
     # a real stream (torch's default is the legacy null stream, which the library's non-blocking
@@ -156,7 +165,7 @@ def main():
     def step(flags=0):
         # every stage of a step is enqueued on torch's current stream, with no host synchronisation:
         # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL all-gather -> rank-0 unpack
-        r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=rank, shard_count=world,
+        r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
                  flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
@@ -164,9 +173,9 @@ def main():
         if distributed:
             dist.all_gather_into_tensor(gathered, send)
         else:
-            gathered.copy_(send)
+            gathered[: send.numel()].copy_(send)
         if rank == 0:
-            r.unpack_tiles(gathered.data_ptr(), world, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
+            r.unpack_tiles(gathered.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -200,7 +209,7 @@ def main():
 
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
-                    for k in (("trace0", "trace", "shade0", "shade", "shadow", "accum") if args.stage_timing
+                    for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum") if args.stage_timing
                               else ("trace0", "trace"))}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
@@ -221,12 +230,15 @@ def main():
                        "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL all-gather"},
             "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
             "stage_ms_per_step": stage_ms,
+            "tail_rays_per_step": int(sum(s.rays_tail for s in stats) / args.steps),
             "rays_per_step": int(rays / args.steps),
             "scene": {"prims": info["prims"], "lbvh_nodes": info["nodes"], "bvh_depth": info["depth"],
                       "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"],
                       "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},
             "cpu_baseline": None,
         }
+        if args.emulate_shards:
+            line["emulated"] = f"shard 0 of {shards} on one GPU: per-rank work of a {shards}-GPU run (not a multi-GPU value)"
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, flat, cam)
         print(json.dumps(line), flush=True)

@@ -138,6 +138,8 @@ typedef struct sptr_stats {
   uint64_t node_visits, tri_tests, sphere_tests; /* SPTR_FRAME_COUNT_VISITS only */
   uint64_t shadow_node_visits, shadow_prim_tests;
   double ms_trace0, ms_shade0; /* SPTR_FRAME_TIMING: bounce-0 parts of ms_trace / ms_shade */
+  uint64_t rays_tail;          /* closest-hit queries (of rays_closest) traced by the path-per-thread tail */
+  double ms_tail;              /* SPTR_FRAME_TIMING: the tail launch */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */
@@ -149,6 +151,9 @@ int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
 /* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default 2^27,
  * at most 2^30). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
+/* First bounce traced path-per-thread (one launch carries every surviving path to its end; earlier
+ * bounces run as trace/shade/shadow wavefront stages).  0 = automatic (2); >= max_depth = none. */
+int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 2 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);

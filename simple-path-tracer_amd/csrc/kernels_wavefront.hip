@@ -664,12 +664,15 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     if (active) {
       const Ray r = make_ray(o, d);
-      hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-      if (!hit) {
+      // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
+      // 1 = constant environment, 4 = primary misses write no radiance
+      if (!(kPrimary && (f.ablate & 2u))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+      if (kPrimary && !hit && (f.ablate & 4u)) {
+      } else if (!hit) {
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = env_color(sh, safe_normalize(d));
+          const vec3 e = (f.ablate & 1u) ? d : env_color(sh, safe_normalize(d));
           vec3 rv;
           if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -687,6 +690,152 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
+// --------------------------------------------------------------------------------- shading steps
+// The per-hit steps of WavefrontPathTracerCPU::traceRay (wf_pt_cpu.cpp:106-247), shared by the
+// wavefront k_shade and the path-per-thread k_tail so both evaluate every path identically.
+struct Surface {
+  vec3 P, n;      // hit point, face-forwarded normal
+  DevMaterial m;  // MaterialManager::getMaterialFromHit
+};
+__device__ __forceinline__ Surface surface_at(const SceneView& sv, const ShadeView& sh, const DevMaterial* smat,
+                                              uint32_t nm, vec3 ro, vec3 rd, float t, uint32_t ref) {
+  Surface s;
+  s.P = ro + t * rd;
+  const uint32_t idx = ref & kIndexMask;
+  vec3 ng;
+  uint32_t mid;
+  if (ref & kSphereBit) {
+    const float4 c = sv.sph[idx];
+    ng = v3((s.P.x - c.x) / c.w, (s.P.y - c.y) / c.w, (s.P.z - c.z) / c.w);
+    mid = sh.geom_mat[sv.sph_geom[idx]];
+  } else {
+    const float4 c = sv.tris[3 * idx + 2];
+    ng = v3(c.y, c.z, c.w);
+    mid = sh.geom_mat[sv.tri_geom[idx]];
+  }
+  s.n = safe_normalize(ng);
+  if (dot(s.n, rd) > 0.0f) s.n = -s.n;
+  s.m = (mid < nm) ? smat[mid] : sh.mats[mid];
+  return s;
+}
+
+// Light::getRadiance + direction/distance (Light.cpp:43-79)
+__device__ __forceinline__ void light_at(const DevLight& Lt, vec3 P, vec3& ldir, float& ldist, vec3& Li) {
+  if (Lt.type == 0) {
+    ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
+    ldist = __builtin_huge_valf();
+    Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+  } else {
+    const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - P;
+    ldist = sqrtf(dot(lv, lv));
+    ldir = lv / ldist;
+    const float att = 1.0f + 0.09f * ldist + 0.032f * ldist * ldist;
+    Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]) / att;
+  }
+}
+__device__ __forceinline__ bool light_faces(const DevLight& Lt, const Surface& s) {
+  vec3 ldir;
+  if (Lt.type == 0) {
+    ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
+  } else {
+    const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - s.P;
+    ldir = lv / sqrtf(dot(lv, lv));
+  }
+  return fmax_g(dot(s.n, ldir), 0.0f) > 0.0f;
+}
+// Direct-light term of one light (wf_pt_cpu.cpp:127-147 with Light::isOccluded's shadow ray,
+// Light.cpp:21-33): false when the light is behind the surface; else the shadow ray {so, ldir,
+// [1e-4, tfar]} and the contribution added when it is unoccluded.
+__device__ __forceinline__ bool light_term(const DevLight& Lt, const Surface& s, vec3 view, vec3 thr, vec3& so,
+                                           vec3& ldir, float& tfar, vec3& contrib) {
+  float ldist;
+  vec3 Li;
+  light_at(Lt, s.P, ldir, ldist, Li);
+  const float cs = fmax_g(dot(s.n, ldir), 0.0f);
+  if (cs <= 0.0f) return false;
+  const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(s.P.x), fabsf(s.P.y)), fabsf(s.P.z)));
+  so = s.P + s.n * eps;
+  tfar = ldist - 1e-4f;
+  const vec3 fr = eval_brdf(s.m, s.n, view, ldir);
+  contrib = thr * (fr * Li * cs);
+  return true;
+}
+
+// Continuation: metal mirror, glass Fresnel/refraction, diffuse cosine sample + Russian roulette
+// (wf_pt_cpu.cpp:151-247).  Updates thr and rng; false when the path is terminated.
+__device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_t depth, vec3& thr, uint32_t& rng,
+                                              vec3& no, vec3& nd) {
+  const DevMaterial& m = s.m;
+  const vec3 P = s.P, nrm = s.n;
+  const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  if (m.metallic > 0.5f) {
+    no = P + nrm * 1e-4f;
+    nd = safe_normalize(reflect(rd, nrm));
+    thr = thr * (albedo * m.metallic);
+    return true;
+  }
+  if (m.metallic < 0.1f && m.ior > 1.3f) {
+    const float ior = m.ior;
+    const float cosine = -dot(rd, nrm);
+    const float eta = (cosine >= 0.0f) ? (1.0f / ior) : ior;
+    const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
+    float r0 = (1.0f - ior) / (1.0f + ior);
+    r0 = r0 * r0;
+    const float xc = 1.0f - clamp_std(fabsf(cosine), 0.0f, 1.0f);
+    const float F = r0 + (1.0f - r0) * xc * xc * xc * xc * xc;
+    const float xi = rand01(rng);
+    if (xi < F) {
+      no = P + nrm * 1e-4f;
+      nd = safe_normalize(reflect(rd, nrm));
+      thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
+    } else {
+      const float ci = -dot(nrm, rd);
+      const float kk = 1.0f - eta * eta * (1.0f - ci * ci);
+      vec3 refr = v3(0.0f, 0.0f, 0.0f);
+      if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
+      if (dot(refr, refr) > 0.0f) {
+        no = P - nrm * 1e-4f;
+        nd = safe_normalize(refr);
+        thr = thr * v3(tr, tr, tr);
+      } else {
+        no = P + nrm * 1e-4f;
+        nd = safe_normalize(reflect(rd, nrm));
+      }
+    }
+    return true;
+  }
+  const float r1 = rand01(rng);
+  const float r2 = rand01(rng);
+  const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
+  const float rr = sqrtf(r2);
+  const float lx = rr * cosf(phi), ly = rr * sinf(phi);
+  const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
+  const vec3 nn = safe_normalize(nrm);
+  const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
+                                         : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
+  const vec3 bt = cross(tg, nn);
+  const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
+  no = P + nrm * 1e-4f;
+  const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
+  const float xi = rand01(rng);
+  bool cont = true;
+  if (depth > 2u) {
+    if (xi >= surv) cont = false;
+    else thr = thr * (albedo / fmax_g(surv, 1e-6f));
+  } else {
+    thr = thr * albedo;
+  }
+  nd = safe_normalize(sdir);
+  return cont;
+}
+
+__device__ __forceinline__ uint32_t stage_materials(const ShadeView& sh, DevMaterial* smat) {
+  const uint32_t nm = sh.num_mats < 32u ? sh.num_mats : 32u;
+  for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
+    reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
+  return nm;
+}
+
 // --------------------------------------------------------------------------------- k_shade
 // One thread per hit record of this bounce.  Radiance is read lazily (only when something is
 // added) and written back once; bounce 0 starts from zero radiance and unit throughput in
@@ -700,9 +849,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   extern __shared__ uint32_t s_off[];
   __shared__ DevMaterial smat[32];
   __shared__ uint32_t s_cnt_n, s_cnt_s;
-  const uint32_t nm = sh.num_mats < 32u ? sh.num_mats : 32u;
-  for (uint32_t i = threadIdx.x; i < nm * 12u; i += blockDim.x)
-    reinterpret_cast<float*>(smat)[i] = reinterpret_cast<const float*>(sh.mats)[i];
+  const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x == 0) s_cnt_n = s_cnt_s = 0u;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segH, nseg_in, s_off, per_in);
@@ -717,10 +864,11 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     const bool active = i < n;
     bool cont = false, shadow = false, dirty = kPrimary;
     uint32_t p = 0u, rng = 0u;
-    vec3 ro, rd, thr, radv = v3(0.0f, 0.0f, 0.0f), P, nrm, no, nd;
-    DevMaterial m;
+    vec3 rd, thr, radv = v3(0.0f, 0.0f, 0.0f), no, nd;
+    Surface sf;
     if (active) {
       const uint4 h = w.hrec[seg_slot(s_off, nseg_in, per_in, i)];
+      vec3 ro;
       if (kPrimary) {
         Primary pr;
         p = h.x;
@@ -741,41 +889,16 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
         radv = v3(1.0f, 1.0f, 1.0f);
         dirty = true;
       } else {
-        const float t = __uint_as_float(h.y);
-        P = ro + t * rd;
-        const uint32_t idx = h.z & kIndexMask;
-        vec3 ng;
-        uint32_t mid;
-        if (h.z & kSphereBit) {
-          const float4 s = sv.sph[idx];
-          ng = v3((P.x - s.x) / s.w, (P.y - s.y) / s.w, (P.z - s.z) / s.w);
-          mid = sh.geom_mat[sv.sph_geom[idx]];
-        } else {
-          const float4 c = sv.tris[3 * idx + 2];
-          ng = v3(c.y, c.z, c.w);
-          mid = sh.geom_mat[sv.tri_geom[idx]];
-        }
-        nrm = safe_normalize(ng);
-        if (dot(nrm, rd) > 0.0f) nrm = -nrm;
-        m = (mid < nm) ? smat[mid] : sh.mats[mid];
-        const vec3 emission = v3(m.emission[0], m.emission[1], m.emission[2]);
+        sf = surface_at(sv, sh, smat, nm, ro, rd, __uint_as_float(h.y), h.z);
+        const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
         if (dot(emission, emission) > 0.0f) {
           if (!kPrimary) radv = xyz(w.rad[p]);
           radv = radv + thr * emission;
           dirty = true;
         }
         // any light facing the surface -> this path gets a shadow record
-        for (uint32_t li = 0; li < sh.num_lights; ++li) {
-          const DevLight& Lt = sh.lights[li];
-          vec3 ldir;
-          if (Lt.type == 0) {
-            ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
-          } else {
-            const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - P;
-            ldir = lv / sqrtf(dot(lv, lv));
-          }
-          if (fmax_g(dot(nrm, ldir), 0.0f) > 0.0f) shadow = true;
-        }
+        for (uint32_t li = 0; li < sh.num_lights; ++li)
+          if (light_faces(sh.lights[li], sf)) shadow = true;
       }
     }
     const uint32_t js = block_append(&s_cnt_s, shadow);
@@ -788,97 +911,18 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       float4* task = w.stask + (size_t)(sd.seg0 + js) * L * ts;
       const vec3 view = -rd;
       for (uint32_t li = 0; li < L; ++li, task += ts) {
-        const DevLight& Lt = sh.lights[li];
-        vec3 ldir, Li;
-        float ldist;
-        if (Lt.type == 0) {
-          ldir = v3(Lt.v[0], Lt.v[1], Lt.v[2]);
-          ldist = __builtin_huge_valf();
-          Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
-        } else {
-          const vec3 lv = v3(Lt.v[0], Lt.v[1], Lt.v[2]) - P;
-          ldist = sqrtf(dot(lv, lv));
-          ldir = lv / ldist;
-          const float att = 1.0f + 0.09f * ldist + 0.032f * ldist * ldist;
-          Li = v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]) / att;
-        }
-        const float cs = fmax_g(dot(nrm, ldir), 0.0f);
-        if (cs <= 0.0f) {
+        vec3 so, ldir, contrib;
+        float tfar;
+        if (!light_term(sh.lights[li], sf, view, thr, so, ldir, tfar, contrib)) {
           task[1] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0u));
           continue;
         }
-        const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
-        const vec3 so = P + nrm * eps;
-        const vec3 fr = eval_brdf(m, nrm, view, ldir);
-        const vec3 contrib = thr * (fr * Li * cs);
-        task[0] = f4(so, ldist - 1e-4f);
+        task[0] = f4(so, tfar);
         task[1] = f4(contrib, __uint_as_float(p + 1u));
         if (ts > 2u) task[2] = f4(ldir, 0.0f);
       }
     }
-    if (active && sh.debug_mode != 1) {
-      // continuation
-      const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
-      if (m.metallic > 0.5f) {
-        no = P + nrm * 1e-4f;
-        nd = safe_normalize(reflect(rd, nrm));
-        thr = thr * (albedo * m.metallic);
-        cont = true;
-      } else if (m.metallic < 0.1f && m.ior > 1.3f) {
-        const float ior = m.ior;
-        const float cosine = -dot(rd, nrm);
-        const float eta = (cosine >= 0.0f) ? (1.0f / ior) : ior;
-        const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
-        float r0 = (1.0f - ior) / (1.0f + ior);
-        r0 = r0 * r0;
-        const float xc = 1.0f - clamp_std(fabsf(cosine), 0.0f, 1.0f);
-        const float F = r0 + (1.0f - r0) * xc * xc * xc * xc * xc;
-        const float xi = rand01(rng);
-        if (xi < F) {
-          no = P + nrm * 1e-4f;
-          nd = safe_normalize(reflect(rd, nrm));
-          thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
-        } else {
-          const float ci = -dot(nrm, rd);
-          const float kk = 1.0f - eta * eta * (1.0f - ci * ci);
-          vec3 refr = v3(0.0f, 0.0f, 0.0f);
-          if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
-          if (dot(refr, refr) > 0.0f) {
-            no = P - nrm * 1e-4f;
-            nd = safe_normalize(refr);
-            thr = thr * v3(tr, tr, tr);
-          } else {
-            no = P + nrm * 1e-4f;
-            nd = safe_normalize(reflect(rd, nrm));
-          }
-        }
-        cont = true;
-      } else {
-        const float r1 = rand01(rng);
-        const float r2 = rand01(rng);
-        const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
-        const float rr = sqrtf(r2);
-        const float lx = rr * cosf(phi), ly = rr * sinf(phi);
-        const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
-        const vec3 nn = safe_normalize(nrm);
-        const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
-                                               : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
-        const vec3 bt = cross(tg, nn);
-        const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
-        no = P + nrm * 1e-4f;
-        const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
-        const float xi = rand01(rng);
-        cont = true;
-        if ((uint32_t)depth > 2u) {
-          if (xi >= surv) cont = false;
-          else thr = thr * (albedo / fmax_g(surv, 1e-6f));
-        } else {
-          thr = thr * albedo;
-        }
-        nd = safe_normalize(sdir);
-      }
-      cont = cont && !last;
-    }
+    if (active && sh.debug_mode != 1) cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
     if (active && dirty) w.rad[p] = f4(radv, 0.0f);
     const uint32_t jn = block_append(&s_cnt_n, cont);
     if (cont && sd.seg0 + jn >= w.seg_cap) {
@@ -954,6 +998,94 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
   if (kCount) flush_visits(vc, w.tot, kTotShNodes);
 }
 
+// --------------------------------------------------------------------------------- k_tail
+// The last bounces (depth0 .. max_depth-1), one thread per surviving path carried to its end in
+// registers: closest hit -> miss/env, or emission + the shadow rays of the lit lights traced in
+// place + continuation -> next bounce.  Late bounces hold few, incoherent rays; as wavefront
+// stages they cost three dependent launches per bounce, a path-state round trip through HBM and a
+// shadow-task stream.  Per path the operations and the order of the radiance updates are those of
+// k_trace + k_shade + k_shadow (wf_pt_cpu.cpp:94-248), so the image does not depend on where the
+// wavefront hands over (test_tail_depth_invariance).  Closest-hit and any-hit queries are tallied
+// per block (bstat_closest / bstat) and folded by k_accum.
+template <bool kLds, bool kW4>
+__global__ void __launch_bounds__(kBlock) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
+                                                 uint32_t nseg_in) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ DevMaterial smat[32];
+  __shared__ uint32_t s_rays[2];
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
+  const uint32_t nm = stage_materials(sh, smat);
+  if (threadIdx.x < 2u) s_rays[threadIdx.x] = 0u;
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
+  const RayStream rin = w.rs[depth0 & 1];
+  const uint32_t L = w.L, D = f.max_depth;
+  Visits vc;
+  uint32_t n_closest = 0u, n_shadow = 0u;
+  const Sched sd = block_sched(n);
+  for (uint32_t i = sd.first + threadIdx.x; i < n; i += sd.step) {
+    const uint32_t id = seg_slot(s_off, nseg_in, per_in, i);
+    const float4 o4 = rin.o[id], d4 = rin.d[id];
+    vec3 ro = xyz(o4), rd = xyz(d4), thr = xyz(rin.thr[id]);
+    uint32_t rng = __float_as_uint(o4.w);
+    const uint32_t p = __float_as_uint(d4.w);
+    vec3 radv = v3(0.0f, 0.0f, 0.0f);
+    bool loaded = false;  // rad[p] is read at the first update
+    for (uint32_t depth = (uint32_t)depth0; depth < D; ++depth) {
+      ++n_closest;
+      float tfar = __builtin_huge_valf();
+      uint32_t ref = kNoHit;
+      const bool hit = traverse_w<kW4, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
+      if (sh.debug_mode == 1) {  // hit/miss visualisation (never continues past bounce 0)
+        radv = hit ? v3(1.0f, 1.0f, 1.0f) : v3(0.0f, 0.0f, 0.0f);
+        loaded = true;
+        break;
+      }
+      if (!loaded) {
+        radv = xyz(w.rad[p]);
+        loaded = true;
+      }
+      if (!hit) {
+        radv = radv + thr * env_color(sh.env, safe_normalize(rd));
+        break;
+      }
+      const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
+      const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
+      if (dot(emission, emission) > 0.0f) radv = radv + thr * emission;
+      const vec3 view = -rd;
+      for (uint32_t li = 0; li < L; ++li) {
+        vec3 so, ldir, contrib;
+        float st;
+        if (!light_term(sh.lights[li], sf, view, thr, so, ldir, st, contrib)) continue;
+        ++n_shadow;
+        uint32_t sref = kNoHit;
+        if (!traverse_w<kW4, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
+          radv = radv + contrib;
+      }
+      vec3 no, nd;
+      if (!continue_path(sf, rd, depth, thr, rng, no, nd)) break;
+      ro = no;
+      rd = nd;
+    }
+    if (loaded) w.rad[p] = f4(radv, 0.0f);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    n_closest += __shfl_xor(n_closest, off);
+    n_shadow += __shfl_xor(n_shadow, off);
+  }
+  if (lane_id() == 0u) {
+    atomicAdd(&s_rays[0], n_closest);
+    atomicAdd(&s_rays[1], n_shadow);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    w.bstat_closest[blockIdx.x] += s_rays[0];
+    w.bstat[blockIdx.x] += s_rays[1];
+  }
+}
+
 // --------------------------------------------------------------------------------- k_accum / resolve
 __global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset) {
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
@@ -961,14 +1093,23 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float
     for (uint32_t s = 0; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
     accum[l] = f4(a, 0.0f);
   }
-  if (blockIdx.x == 0) {  // fold the per-block any-hit tallies of this batch into the totals
-    unsigned long long s = 0ull;
+  if (blockIdx.x == 0) {  // fold the per-block query tallies of this batch into the totals
+    unsigned long long s = 0ull, c = 0ull;
     for (uint32_t b = threadIdx.x; b < kMaxSegs; b += kBlock) {
       s += w.bstat[b];
+      c += w.bstat_closest[b];
       w.bstat[b] = 0ull;
+      w.bstat_closest[b] = 0ull;
     }
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane_id() == 0u) atomicAdd(&w.tot[kTotShadow], s);
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off);
+      c += __shfl_xor(c, off);
+    }
+    if (lane_id() == 0u) {
+      atomicAdd(&w.tot[kTotShadow], s);
+      atomicAdd(&w.tot[kTotClosest], c);
+      atomicAdd(&w.tot[kTotTail], c);
+    }
   }
 }
 
@@ -1214,6 +1355,22 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   else   { if (count) SPTR_SHADOW_W(false, true); else SPTR_SHADOW_W(false, false); }
 #undef SPTR_SHADOW_W
 #undef SPTR_SHADOW
+  return g;
+}
+
+unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth0,
+                     uint32_t nseg, hipStream_t s) {
+  const bool L = sv.lds_bytes != 0;
+  const unsigned lb = trace_lds(sv, L, false, nseg);
+  unsigned g = 0;
+#define SPTR_TAIL(Lc, Wc)                                                                            \
+  do {                                                                                               \
+    g = resident_grid((const void*)&k_tail<Lc, Wc>, lb);                                             \
+    hipLaunchKernelGGL((k_tail<Lc, Wc>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth0, nseg);  \
+  } while (0)
+  if (L) { if (sv.width == 4u) SPTR_TAIL(true, true); else SPTR_TAIL(true, false); }
+  else   { if (sv.width == 4u) SPTR_TAIL(false, true); else SPTR_TAIL(false, false); }
+#undef SPTR_TAIL
   return g;
 }
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -52,6 +53,9 @@ void free_buf(DevBuf& b) {
 // a 1080p frame in one batch.  Measured on MI355X: 2.1M-path batches 5.2 Grays/s, 16.8M 17.7,
 // 134M 27.6 — per-launch fixed costs dominate small batches, and HBM capacity is not a constraint.
 constexpr uint64_t kDefaultWavePaths = 1ull << 27;
+// Bounces 0 .. T-1 run as wavefront stages (trace, shade, shadow launches over dense queues); from
+// bounce T on, k_tail carries each surviving path to its end in one launch.
+constexpr uint32_t kDefaultTailDepth = kMaxDepth;  // measured slower than the wavefront
 
 // MaterialManager::getMaterialFromHit (src/MaterialManager.cpp:91-103): the geomID's mapped
 // material when it is in range, else MaterialManager::getMaterialByID(geomID) (:79-89).
@@ -135,6 +139,7 @@ WaveView wave_view(Context& c) {
   w.segH = SegTable{seg + (kMaxSegs + 4), seg + (kMaxSegs + 4) + kMaxSegs};
   w.segS = SegTable{seg + 2 * (kMaxSegs + 4), seg + 2 * (kMaxSegs + 4) + kMaxSegs};
   w.bstat = reinterpret_cast<unsigned long long*>(seg + 3 * (kMaxSegs + 4));
+  w.bstat_closest = w.bstat + kMaxSegs;
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
@@ -171,6 +176,8 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.cam_u = v3(k.up[0], k.up[1], k.up[2]);
   v.half_w = k.half_width;
   v.half_h = k.half_height;
+  static const uint32_t ablate = getenv("SPTR_ABLATE") ? (uint32_t)atoi(getenv("SPTR_ABLATE")) : 0u;
+  v.ablate = ablate;
   return v;
 }
 
@@ -270,6 +277,8 @@ int collect_pending(Context& c, sptr_stats* stats) {
   stats->trace_launches = trace_launches;
   stats->rays_closest = tot[kTotClosest];
   stats->rays_shadow = tot[kTotShadow];
+  stats->rays_tail = tot[kTotTail];
+  stats->ms_tail = ms[7];
   stats->samples = samples;
   stats->waves = waves;
   stats->node_visits = tot[kTotNodes];
@@ -308,7 +317,7 @@ int sptr_create(int device, sptr_ctx** out) {
     delete x;
     return SPTR_ERR_HIP;
   }
-  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + kMaxSegs * 8;
+  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8;
   if (ensure_buf(c.w_seg, seg_bytes) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
       hipMemset(c.w_seg.p, 0, seg_bytes) != hipSuccess) {
     delete x;
@@ -355,6 +364,13 @@ int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
   if (!x) return SPTR_ERR_INVALID;
   if (width != 0 && width != 2 && width != 4) return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or 4");
   x->c.bvh_width = width;
+  return SPTR_OK;
+}
+
+int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (depth > (uint32_t)kMaxDepth) return fail(x->c, SPTR_ERR_INVALID, "tail depth must be 0 (automatic) or 1..32");
+  x->c.tail_depth = depth;
   return SPTR_OK;
 }
 
@@ -533,6 +549,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   tm.begin_call();
   uint32_t done = 0, waves = 0;
   const int D = (int)f->max_depth;
+  const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : kDefaultTailDepth));
   while (done < f->spp) {
     const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
     fv.k = kk;
@@ -541,6 +558,12 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
     for (int d = 0; d < D; ++d) {
+      if (d >= T) {  // the remaining bounces, path per thread
+        tm.begin(7);
+        launch_tail(sv, sh, fv, w, d, g_shade, s);
+        tm.end();
+        break;
+      }
       tm.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();

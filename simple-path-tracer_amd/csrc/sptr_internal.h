@@ -120,12 +120,21 @@ struct FrameView {
   uint32_t valid;  // pixels of this shard inside the image
   vec3 cam_pos, cam_f, cam_r, cam_u;
   float half_w, half_h;
+  uint32_t ablate;  // SPTR_ABLATE environment variable: timing experiments only (0 in normal use)
 };
 
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 
 // 64-bit totals block
-enum : int { kTotClosest = 0, kTotShadow, kTotNodes, kTotTris, kTotSph, kTotShNodes, kTotShPrims, kTotOverflow, kTotWords };
+enum : int {
+  kTotClosest = 0,  // closest-hit queries (k_trace + k_tail)
+  kTotShadow,       // any-hit queries
+  kTotNodes, kTotTris, kTotSph,  // k_trace visit counts (SPTR_FRAME_COUNT_VISITS)
+  kTotShNodes, kTotShPrims,      // k_shadow visit counts
+  kTotOverflow,
+  kTotTail,         // closest-hit queries traced by k_tail
+  kTotWords
+};
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
@@ -147,7 +156,8 @@ struct WaveView {
   float4* stask;    // per shade slot: L tasks of tstride float4
   SegTable segN, segH, segS;  // next rays, hits, shadow tasks
   unsigned long long* tot;
-  unsigned long long* bstat;  // [kMaxSegs] per-block any-hit tallies (k_shadow), folded by k_accum
+  unsigned long long* bstat;          // [kMaxSegs] per-block any-hit tallies (k_shadow, k_tail), folded by k_accum
+  unsigned long long* bstat_closest;  // [kMaxSegs] per-block closest-hit tallies of k_tail
   uint32_t seg_cap;  // records allocated per segmented stream (bounds guard)
   uint32_t L;        // lights (tasks per shaded path)
   uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
@@ -169,6 +179,7 @@ struct Context {
   std::string err;
   int debug_mode = 0;
   uint64_t wave_paths = 0;  // 0 = default
+  uint32_t tail_depth = 0;  // first bounce traced path-per-thread by k_tail (0 = automatic)
   // scene
   DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
   uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..32); 0 = automatic
@@ -221,6 +232,8 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
                   uint32_t nseg_in, hipStream_t s);
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   uint32_t nseg_in, hipStream_t s);
+unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth0,
+                     uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
                    hipStream_t s);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, hipStream_t s);

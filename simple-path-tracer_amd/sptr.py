@@ -74,7 +74,8 @@ class Stats(C.Structure):
                 ("ms_trace", C.c_double), ("ms_shade", C.c_double), ("ms_shadow", C.c_double),
                 ("ms_accum", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("shadow_node_visits", C.c_uint64),
-                ("shadow_prim_tests", C.c_uint64), ("ms_trace0", C.c_double), ("ms_shade0", C.c_double)]
+                ("shadow_prim_tests", C.c_uint64), ("ms_trace0", C.c_double), ("ms_shade0", C.c_double),
+                ("rays_tail", C.c_uint64), ("ms_tail", C.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -95,7 +96,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -123,6 +124,7 @@ def lib() -> C.CDLL:
         "sptr_last_error": (C.c_char_p, [vp]),
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
+        "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
         "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
@@ -381,6 +383,9 @@ class Renderer:
 
     def set_wave_paths(self, n: int):
         self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
+
+    def set_tail_depth(self, n: int):
+        self._check(self._L.sptr_set_tail_depth(self._h, n), "set_tail_depth")
 
     def set_leaf_size(self, n: int):
         self._check(self._L.sptr_set_leaf_size(self._h, n), "set_leaf_size")

@@ -301,3 +301,27 @@ def test_async_renders_equal_sync(renderer):
     assert st.rays_shadow == st1.rays_shadow + st2.rays_shadow
     assert st.samples == W * H * 5 and st.ms_total > 0 and st.trace_launches > 0
     assert renderer.collect_stats().rays_closest == 0  # window restarted
+
+
+@pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])
+def test_tail_depth_invariance(renderer, scene, p0, p1):
+    """Where the wavefront stages hand over to the path-per-thread tail changes only the schedule:
+    the image and the closest/any-hit query counts are identical for every split depth."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, scene, p0, p1)
+    out = {}
+    try:
+        for t in (1, 2, 3, 6):
+            renderer.set_tail_depth(t)
+            st = renderer.render(cam, W, H, spp=4)
+            out[t] = (renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, st.rays_tail)
+    finally:
+        renderer.set_tail_depth(0)
+    ref = out[6]
+    assert ref[3] == 0  # tail at max_depth: all bounces are wavefront stages
+    for t in (1, 2, 3):
+        acc, rc, rs, rt = out[t]
+        assert np.array_equal(acc.view(np.uint32), ref[0].view(np.uint32)), t
+        assert (rc, rs) == (ref[1], ref[2]), t
+        assert 0 < rt < rc
