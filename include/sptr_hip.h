@@ -152,7 +152,9 @@ int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
  * at most 2^30). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
 /* First bounce traced path-per-thread (one launch carries every surviving path to its end; earlier
- * bounces run as trace/shade/shadow wavefront stages).  0 = automatic (2); >= max_depth = none. */
+ * bounces run as trace/shade/shadow wavefront stages).  0 = automatic: 4 for batches of at most
+ * 2^25 paths (e.g. the per-rank share of a sharded 1080p frame), none for larger batches;
+ * >= max_depth = none.  The image and the query counts do not depend on it. */
 int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 2 otherwise); applies to the next sptr_upload_scene. */

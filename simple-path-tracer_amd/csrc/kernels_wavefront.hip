@@ -83,11 +83,19 @@ __device__ __forceinline__ Sched block_sched(uint32_t n) {
 // (s_off[0..nseg]); returns the total.  Contains block barriers: call from every thread.
 __device__ uint32_t seg_scan(const SegTable& t, uint32_t nseg, uint32_t* s_off, uint32_t& per) {
   __shared__ uint32_t s_wave[kBlock / 64];
+  // every count load is issued before the first use (unrolled, predicated), so the prologue costs
+  // one memory round trip instead of one per segment: it bounds the duration of the short launches
+  // of the deep bounces (and of every launch in a small, e.g. 8-way sharded, batch)
+  constexpr uint32_t kChunk = kMaxSegs / kBlock;
   const uint32_t chunk = (nseg + kBlock - 1) / kBlock;
   const uint32_t b0 = threadIdx.x * chunk;
+  const uint32_t per_v = *t.per;
+  uint32_t v[kChunk];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunk; ++j) v[j] = (j < chunk && b0 + j < nseg) ? t.cnt[b0 + j] : 0u;
   uint32_t sum = 0u;
-  for (uint32_t j = 0; j < chunk; ++j)
-    if (b0 + j < nseg) sum += t.cnt[b0 + j];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunk; ++j) sum += v[j];
   uint32_t incl = sum;
   const uint32_t lane = lane_id();
   for (int off = 1; off < 64; off <<= 1) {
@@ -98,17 +106,18 @@ __device__ uint32_t seg_scan(const SegTable& t, uint32_t nseg, uint32_t* s_off, 
   __syncthreads();
   uint32_t run = incl - sum;
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += s_wave[w];
-  for (uint32_t j = 0; j < chunk; ++j)
-    if (b0 + j < nseg) {
+#pragma unroll
+  for (uint32_t j = 0; j < kChunk; ++j)
+    if (j < chunk && b0 + j < nseg) {
       s_off[b0 + j] = run;
-      run += t.cnt[b0 + j];
+      run += v[j];
     }
   if (threadIdx.x == 0) {
     uint32_t tot = 0u;
     for (uint32_t w = 0; w < kBlock / 64; ++w) tot += s_wave[w];
     s_off[nseg] = tot;
   }
-  per = *t.per;
+  per = per_v;
   __syncthreads();
   return s_off[nseg];
 }

@@ -49,13 +49,26 @@ void free_buf(DevBuf& b) {
   b.bytes = 0;
 }
 
-// One wavefront batch holds up to 2^27 paths (~17.7 GB of path state at 132 B/path): all 64 spp of
-// a 1080p frame in one batch.  Measured on MI355X: 2.1M-path batches 5.2 Grays/s, 16.8M 17.7,
-// 134M 27.6 — per-launch fixed costs dominate small batches, and HBM capacity is not a constraint.
-constexpr uint64_t kDefaultWavePaths = 1ull << 27;
+// One wavefront batch holds up to 2^29 paths (160 B of path state each with one light: 86 GB, under
+// a third of the 288 GB of HBM).  Every batch pays the secondary bounces' latency floor once: their
+// queues are short (C3: ~1% of the primary rays survive) and each launch lasts as long as its
+// longest traversal (~0.2-0.3 ms in the rattan chair), so fewer, larger batches win.  Measured on
+// MI355X (C3, 1080p x 256 spp; profiles/r01d_wave_sweep.txt): 2^24 paths/batch 9.8 Grays/s, 2^25
+// 15.2, 2^26 22.1, 2^27 29.4, 2^28 37.1, 2^29 42.8.  The default is further capped by free memory.
+constexpr uint64_t kDefaultWavePaths = 1ull << 29;
+constexpr double kWaveMemFraction = 0.5;  // at most this share of the free HBM for the default batch
 // Bounces 0 .. T-1 run as wavefront stages (trace, shade, shadow launches over dense queues); from
 // bounce T on, k_tail carries each surviving path to its end in one launch.
-constexpr uint32_t kDefaultTailDepth = kMaxDepth;  // measured slower than the wavefront
+// Automatic policy (tail_depth 0), measured on MI355X (C2, profiles/r01d_shards_c2.txt): with a
+// full 2^27-path batch the deep-bounce launches are large enough to pay for themselves and the
+// wavefront wins (no tail: 4.20 ms vs 4.34 ms with a tail from bounce 4); in the small per-rank
+// batches of a sharded frame the fixed cost of the 3 launches per deep bounce dominates, and the
+// tail from bounce 4 wins (8-way shard: 0.723 ms vs 0.794; 4-way: 1.208 vs 1.238).
+constexpr uint32_t kSmallBatchTailDepth = 4;
+constexpr uint64_t kSmallBatchPaths = 1ull << 25;  // batches up to this many paths take the tail
+uint32_t auto_tail_depth(uint64_t batch_paths) {
+  return batch_paths <= kSmallBatchPaths ? kSmallBatchTailDepth : (uint32_t)kMaxDepth;
+}
 
 // MaterialManager::getMaterialFromHit (src/MaterialManager.cpp:91-103): the geomID's mapped
 // material when it is in range, else MaterialManager::getMaterialByID(geomID) (:79-89).
@@ -99,6 +112,10 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
   resized = true;
   return SPTR_OK;
 }
+
+// device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
+// L shadow tasks of ts float4s (the segment slack is excluded)
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 16 + 16 + (uint64_t)L * ts * 16; }
 
 int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts) {
   L = L ? L : 1u;
@@ -528,7 +545,19 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const bool reset = f->frame_begin == 1;
   if (!reset && f->frame_begin != c.last_samples + 1)
     return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
-  const uint64_t wave_paths = c.wave_paths ? c.wave_paths : kDefaultWavePaths;
+  uint64_t wave_paths = c.wave_paths;
+  if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
+    wave_paths = kDefaultWavePaths;
+    if (c.wave_cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
+        const uint64_t held = c.wave_cap ? c.wave_cap * wave_path_bytes(c.wave_L, c.wave_ts) : 0ull;
+        const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
+        const uint64_t fit = (uint64_t)(((double)free_b + (double)held) * kWaveMemFraction) / wave_path_bytes(L, task_stride(c));
+        wave_paths = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(wave_paths, fit));
+      }
+    }
+  }
   uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
   k = std::min<uint32_t>(k, f->spp);
   rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c));
@@ -549,7 +578,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   tm.begin_call();
   uint32_t done = 0, waves = 0;
   const int D = (int)f->max_depth;
-  const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : kDefaultTailDepth));
+  const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P)));
   while (done < f->spp) {
     const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
     fv.k = kk;

@@ -312,7 +312,7 @@ def test_tail_depth_invariance(renderer, scene, p0, p1):
     sptr.setup_default(renderer, scene, p0, p1)
     out = {}
     try:
-        for t in (1, 2, 3, 6):
+        for t in (1, 2, 3, 4, 5, 6, 0):
             renderer.set_tail_depth(t)
             st = renderer.render(cam, W, H, spp=4)
             out[t] = (renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, st.rays_tail)
@@ -320,7 +320,9 @@ def test_tail_depth_invariance(renderer, scene, p0, p1):
         renderer.set_tail_depth(0)
     ref = out[6]
     assert ref[3] == 0  # tail at max_depth: all bounces are wavefront stages
-    for t in (1, 2, 3):
+    # automatic policy: a small batch (96x64x4 paths) hands over to the tail at bounce 4
+    assert out[0][3] == out[4][3] > 0
+    for t in (1, 2, 3, 4, 5, 0):
         acc, rc, rs, rt = out[t]
         assert np.array_equal(acc.view(np.uint32), ref[0].view(np.uint32)), t
         assert (rc, rs) == (ref[1], ref[2]), t
