@@ -34,6 +34,8 @@ import workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 STREAM_BYTES_PER_RAY = 36.0  # path id 4 + origin 12 + dir 12 in, t 4 + prim 4 out
+L2_BYTES_PER_XCD = 4 << 20  # MI355X: 4 MB L2 per XCD (MI355X_MICROARCH.md)
+XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 8, "c4": 4, "c5": 1}
 
 
@@ -49,9 +51,15 @@ def roofline(cnt, stats, layout, wl_name, steps):
     """Roofline of the dominant kernel, k_trace (all bounces; one template).
 
     Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 + 64 n_node + 48 n_tri + 16 n_sph with the
-    visit counts taken from an instrumented pass over the same rays.  When the scene is staged in
-    LDS (lds_bytes > 0), node and primitive fetches never reach HBM, so the HBM-algorithmic bytes
-    are the 36-byte ray stream only; the full B_ray figure is reported beside it."""
+    visit counts taken from an instrumented pass over the same rays.  Which of those bytes are HBM
+    bytes depends on where the scene lives:
+      lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU, so only
+           the 36-byte ray stream counts;
+      l2   scene (nodes + triangles + spheres + refs) fits one XCD's 4 MB L2: the compulsory
+           traffic is one scene copy per XCD per launch (8 x footprint) plus the ray stream —
+           counting every visit as HBM bytes would report more than the peak (C3: 1.15);
+      hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in §8(d).
+    The full B_ray figure is reported beside it (b_ray_full_gbs)."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
     launches_per_step = max(1, launches // max(1, steps))
@@ -60,7 +68,9 @@ def roofline(cnt, stats, layout, wl_name, steps):
     node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0  # 64 BVH2, 128 BVH4
     scene = node_b * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
     lds = layout["lds_bytes"] > 0
-    hbm_alg = stream + (0.0 if lds else scene)
+    footprint = sum(layout[k] for k in ("node_bytes", "tri_bytes", "sphere_bytes", "prim_ref_bytes"))
+    residency = "lds" if lds else ("l2" if footprint <= L2_BYTES_PER_XCD else "hbm")
+    hbm_alg = stream + {"lds": 0.0, "l2": XCDS * footprint * launches_per_step, "hbm": scene}[residency]
     per_launch = hbm_alg / launches_per_step
     achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic, src = None, None
@@ -75,7 +85,7 @@ def roofline(cnt, stats, layout, wl_name, steps):
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
             "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
             "launches_per_step": launches_per_step,
-            "scene_in_lds": lds,
+            "scene_in_lds": lds, "scene_residency": residency, "scene_bytes": int(footprint),
             "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
             "per_ray": {"nodes": round(cnt.node_visits / max(1, traced), 3),
                         "tris": round(cnt.tri_tests / max(1, traced), 3),

@@ -148,8 +148,8 @@ int sptr_create(int device, sptr_ctx** out);
 int sptr_destroy(sptr_ctx* ctx);
 const char* sptr_last_error(const sptr_ctx* ctx);
 int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
-/* Largest number of paths (pixels x samples) processed per wavefront batch (0 = default 2^27,
- * at most 2^30). */
+/* Largest number of paths (pixels x samples) processed per wavefront batch (at most 2^30).
+ * 0 = default: 2^29, capped by what half of the device's free memory holds (at least 2^24). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
 /* First bounce traced path-per-thread (one launch carries every surviving path to its end; earlier
  * bounces run as trace/shade/shadow wavefront stages).  0 = automatic: 4 for batches of at most

@@ -1099,7 +1099,18 @@ __global__ void __launch_bounds__(kBlock) k_tail(SceneView sv, ShadeView sh, Fra
 __global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset) {
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     vec3 a = reset ? v3(0.0f, 0.0f, 0.0f) : xyz(accum[l]);
-    for (uint32_t s = 0; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
+    // sample order is the reference's accumulation order (one add per frame); the unroll only
+    // lets eight sample loads be in flight per thread before the first add
+    const float4* src = w.rad + l;
+    uint32_t s = 0;
+    for (; s + 8u <= f.k; s += 8u) {
+      float4 v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8u; ++j) v[j] = src[(size_t)(s + j) * f.P];
+#pragma unroll
+      for (uint32_t j = 0; j < 8u; ++j) a = a + xyz(v[j]);
+    }
+    for (; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
     accum[l] = f4(a, 0.0f);
   }
   if (blockIdx.x == 0) {  // fold the per-block query tallies of this batch into the totals
