@@ -31,8 +31,14 @@
                              // (bounce 0 stays at 7: coherent rays gain more from occupancy, 8.4 -> 5.4)
 #endif
 #ifndef SPTR_SHADE_WAVES
-#define SPTR_SHADE_WAVES 1
+#define SPTR_SHADE_WAVES 5  // 111 -> 96 VGPRs, 4 -> 5 waves, no spills: C2 shade 0.971 -> 0.907 ms
+#endif                      // (6 waves spills 48-76 B/lane; profiles/r01f_variants.txt)
+#ifndef SPTR_TAIL_WAVES
+#define SPTR_TAIL_WAVES 1
 #endif
+#ifndef SPTR_SHADOW_WAVES
+#define SPTR_SHADOW_WAVES 6  // C5 (BVH4 from HBM): 5 -> 6 waves, shadow 8.34 -> 7.19 ms/step; 7 waves
+#endif                       // spills more and loses it again (8.06)
 
 namespace sptr {
 
@@ -960,7 +966,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount, bool kW4>
-__global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
+__global__ void __launch_bounds__(kBlock, SPTR_SHADOW_WAVES) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
@@ -1017,7 +1023,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(SceneView sv, ShadeView sh, W
 // wavefront hands over (test_tail_depth_invariance).  Closest-hit and any-hit queries are tallied
 // per block (bstat_closest / bstat) and folded by k_accum.
 template <bool kLds, bool kW4>
-__global__ void __launch_bounds__(kBlock) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
                                                  uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
