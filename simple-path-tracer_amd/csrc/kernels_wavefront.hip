@@ -508,18 +508,21 @@ struct ImageDiv {
   DivBy w, h;
 };
 __device__ __forceinline__ ImageDiv image_div(const FrameView& f) { return ImageDiv{div_by(float(f.W)), div_by(float(f.H))}; }
-__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
-  const uint32_t s = fast_div(f.div_P, p), l = p - s * f.P;
-  int x, y;
-  if (!local_pixel(f, l, x, y)) return false;
-  const uint32_t acc = f.acc0 + s;
-  const uint32_t ps = (uint32_t)(y * f.W + x);
+// pixel (x, y) with pixel_seed ps = y*W + x, accumulation index acc
+__device__ __forceinline__ void primary_at(const FrameView& f, const ImageDiv& dv, int x, int y, uint32_t ps,
+                                           uint32_t acc, Primary& out) {
   uint32_t r = wang_hash(ps ^ acc * 9781u);
   const float jx = rand01(r);
   const float jy = rand01(r);
   const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, dv.w), div_nrm(float(y) + jy, dv.h));
   out.d = safe_normalize(dir);
   out.rng = wang_hash((ps ^ acc) ^ 1u);
+}
+__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
+  const uint32_t s = fast_div(f.div_P, p), l = p - s * f.P;
+  int x, y;
+  if (!local_pixel(f, l, x, y)) return false;
+  primary_at(f, dv, x, y, (uint32_t)(y * f.W + x), f.acc0 + s, out);
   return true;
 }
 
@@ -644,6 +647,66 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
+  if constexpr (kPrimary && kLds) {
+    // Bounce 0, pixel-major (LDS-staged scenes, where every primary ray costs about the same): thread <- local pixel l, looping over the batch's k sample slots in
+    // sample order (path p = s*P + l, as everywhere else).  Misses before the pixel's first hit
+    // are summed straight into the accumulator — the same adds, in the same order, that k_accum
+    // would do — so an all-sky pixel (most of C2) writes no radiance at all and k_accum skips it;
+    // from the first hit on, misses go to rad[p] and k_accum resumes there (accum.w = resume slot).
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+    const ImageDiv idiv = image_div(f);
+    Visits vc;
+    const Sched sd = block_sched(f.P);
+    const uint32_t per = sd.per * f.k;  // hit-record segment stride: all samples of the block's pixels
+    const uint32_t seg0 = sd.seg0 * f.k;
+    for (uint32_t base = sd.first; base < f.P; base += sd.step) {
+      const uint32_t l = base + threadIdx.x;
+      int x = 0, y = 0;
+      const bool valid = l < f.P && local_pixel(f, l, x, y);
+      const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
+      vec3 a = v3(0.0f, 0.0f, 0.0f);
+      if (valid && !f.reset) a = xyz(f.accum[l]);
+      uint32_t resume = f.k;
+      for (uint32_t smp = 0; smp < f.k; ++smp) {
+        bool hit = false;
+        uint32_t ref = kNoHit;
+        float tfar = __builtin_huge_valf();
+        const uint32_t p = smp * f.P + l;
+        if (valid) {
+          Primary pr;
+          primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
+          const Ray r = make_ray(f.cam_pos, pr.d);
+          // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
+          // 1 = constant environment, 4 = primary misses add no radiance
+          if (!(f.ablate & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+          if (!hit) {
+            vec3 rv = v3(0.0f, 0.0f, 0.0f);
+            if (sh.debug_mode != 1) {
+              const vec3 e = (f.ablate & 1u) ? pr.d : env_color(sh, safe_normalize(pr.d));
+              rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+            }
+            if (resume != f.k) w.rad[p] = f4(rv, 0.0f);
+            else if (!(f.ablate & 4u)) a = a + rv;
+          } else if (resume == f.k) {
+            resume = smp;
+          }
+        }
+        const uint32_t j = block_append(&s_cnt, hit);
+        if (hit) {
+          if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
+          else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
+        }
+      }
+      if (l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
+    }
+    seg_publish(w.segH, &s_cnt, per);
+    if (kCount) flush_visits(vc, w.tot, kTotNodes);
+    return;
+  }
+  // bounce 0 of scenes traversed from L2/HBM stays path-major: per-pixel cost varies by orders of
+  // magnitude there (sky vs a 10M-triangle mesh), and a thread looping over all k samples of one
+  // pixel leaves the launch waiting on the blocks that drew the mesh (C5 measured 22.9 -> 67.9 ms)
   uint32_t n, per_in = 0u;
   if (kPrimary) {
     n = f.P * f.k;
@@ -697,7 +760,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     const uint32_t j = block_append(&s_cnt, hit);
     if (hit) {
-      if (sd.seg0 + j < w.seg_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
       else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
     }
   }
@@ -1102,13 +1165,26 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
 }
 
 // --------------------------------------------------------------------------------- k_accum / resolve
-__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum, int reset) {
+// Per-pixel sample sums in sample order.  Pixel-major bounce 0 (f.pixel_major) began them:
+// accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
+// batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
+// slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
+__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum) {
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
-    vec3 a = reset ? v3(0.0f, 0.0f, 0.0f) : xyz(accum[l]);
+    uint32_t s0 = 0u;
+    vec3 a = v3(0.0f, 0.0f, 0.0f);
+    if (f.pixel_major) {
+      const float4 a4 = accum[l];
+      s0 = __float_as_uint(a4.w);
+      if (s0 >= f.k) continue;
+      a = xyz(a4);
+    } else if (!f.reset) {
+      a = xyz(accum[l]);
+    }
     // sample order is the reference's accumulation order (one add per frame); the unroll only
     // lets eight sample loads be in flight per thread before the first add
     const float4* src = w.rad + l;
-    uint32_t s = 0;
+    uint32_t s = s0;
     for (; s + 8u <= f.k; s += 8u) {
       float4 v[8];
 #pragma unroll
@@ -1117,7 +1193,7 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float
       for (uint32_t j = 0; j < 8u; ++j) a = a + xyz(v[j]);
     }
     for (; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
-    accum[l] = f4(a, 0.0f);
+    accum[l] = f4(a, __uint_as_float(f.k));
   }
   if (blockIdx.x == 0) {  // fold the per-block query tallies of this batch into the totals
     unsigned long long s = 0ull, c = 0ull;
@@ -1400,8 +1476,8 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
   return g;
 }
 
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, hipStream_t s) {
-  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, reset ? 1 : 0);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s) {
+  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum);
 }
 
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,

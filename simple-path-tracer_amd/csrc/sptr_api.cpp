@@ -117,8 +117,11 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
 // L shadow tasks of ts float4s (the segment slack is excluded)
 uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 16 + 16 + (uint64_t)L * ts * 16; }
 
-int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts) {
+int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k) {
   L = L ? L : 1u;
+  // hit records: the pixel-major bounce-0 trace gives each block a segment of k records per pixel
+  // slot it owns, so the segment slack is kMaxSegs * kBlock * k records
+  API_HIP(ensure_buf(c.w_hrec, ((size_t)cap + (size_t)kMaxSegs * kBlock * k) * 16));
   if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
   // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
   // with per = ceil(n / (G*kBlock)) * kBlock, so the segment space G*per can exceed n by up to
@@ -126,7 +129,6 @@ int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts) {
   const size_t n = (size_t)cap, ns = n + (size_t)kMaxSegs * kBlock;
   for (auto& b : c.w_rs)
     for (DevBuf& x : b) API_HIP(ensure_buf(x, ns * 16));
-  API_HIP(ensure_buf(c.w_hrec, ns * 16));
   API_HIP(ensure_buf(c.w_rad, n * 16));
   API_HIP(ensure_buf(c.w_stask, ns * L * ts * 16));
   c.wave_cap = cap;
@@ -161,6 +163,7 @@ WaveView wave_view(Context& c) {
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
   w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
+  w.hrec_cap = (uint32_t)std::min<uint64_t>(c.w_hrec.bytes / 16, 0xFFFFFFFFull);
   return w;
 }
 
@@ -195,6 +198,9 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.half_h = k.half_height;
   static const uint32_t ablate = getenv("SPTR_ABLATE") ? (uint32_t)atoi(getenv("SPTR_ABLATE")) : 0u;
   v.ablate = ablate;
+  v.accum = static_cast<float4*>(c.accum.p);
+  v.reset = 0;
+  v.pixel_major = 0;
   return v;
 }
 
@@ -560,7 +566,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   }
   uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
   k = std::min<uint32_t>(k, f->spp);
-  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c));
+  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k);
   if (rc != SPTR_OK) return rc;
 
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
@@ -583,6 +589,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
     fv.k = kk;
     fv.acc0 = f->frame_begin + done;
+    fv.reset = (reset && done == 0) ? 1u : 0u;
+    fv.pixel_major = sv.lds_bytes != 0 ? 1u : 0u;  // must match k_trace's kLds dispatch
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
@@ -604,7 +612,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       tm.end();
     }
     tm.begin(4);
-    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), reset && done == 0, s);
+    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), s);
     tm.end();
     API_HIP(hipGetLastError());
     done += kk;

@@ -121,6 +121,9 @@ struct FrameView {
   vec3 cam_pos, cam_f, cam_r, cam_u;
   float half_w, half_h;
   uint32_t ablate;  // SPTR_ABLATE environment variable: timing experiments only (0 in normal use)
+  float4* accum;    // per local pixel: running sample sum (xyz) + resume slot (w bits), see k_accum
+  uint32_t reset;   // this batch starts the accumulation (frame_begin == 1, first batch)
+  uint32_t pixel_major;  // bounce 0 runs pixel-major and folds leading misses into accum (LDS scenes)
 };
 
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
@@ -159,6 +162,7 @@ struct WaveView {
   unsigned long long* bstat;          // [kMaxSegs] per-block any-hit tallies (k_shadow, k_tail), folded by k_accum
   unsigned long long* bstat_closest;  // [kMaxSegs] per-block closest-hit tallies of k_tail
   uint32_t seg_cap;  // records allocated per segmented stream (bounds guard)
+  uint32_t hrec_cap;  // hit records allocated (bounce 0 segments span k samples per pixel slot)
   uint32_t L;        // lights (tasks per shaded path)
   uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
 };
@@ -236,7 +240,7 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
                      uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
                    hipStream_t s);
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, bool reset, hipStream_t s);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
