@@ -647,12 +647,14 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
-  if constexpr (kPrimary && kLds) {
-    // Bounce 0, pixel-major (LDS-staged scenes, where every primary ray costs about the same): thread <- local pixel l, looping over the batch's k sample slots in
-    // sample order (path p = s*P + l, as everywhere else).  Misses before the pixel's first hit
-    // are summed straight into the accumulator — the same adds, in the same order, that k_accum
-    // would do — so an all-sky pixel (most of C2) writes no radiance at all and k_accum skips it;
-    // from the first hit on, misses go to rad[p] and k_accum resumes there (accum.w = resume slot).
+  if (kPrimary && kLds && f.pixel_major) {
+    // Bounce 0, pixel-major (f.pixel_major: LDS-staged scenes, where every primary ray costs
+    // about the same, in batches with >= kPixelMajorItems pixels per resident thread): thread <-
+    // local pixel l, looping over the batch's k sample slots in sample order (path p = s*P + l,
+    // as everywhere else).  Misses before the pixel's first hit are summed straight into the
+    // accumulator — the same adds, in the same order, that k_accum would do — so an all-sky pixel
+    // writes no radiance at all and k_accum skips it; from the first hit on, misses go to rad[p]
+    // and k_accum resumes there (accum.w = resume slot).
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
     const ImageDiv idiv = image_div(f);
@@ -667,6 +669,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
       vec3 a = v3(0.0f, 0.0f, 0.0f);
       if (valid && !f.reset) a = xyz(f.accum[l]);
+      bool fold = true;
       uint32_t resume = f.k;
       for (uint32_t smp = 0; smp < f.k; ++smp) {
         bool hit = false;
@@ -686,9 +689,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
               const vec3 e = (f.ablate & 1u) ? pr.d : env_color(sh, safe_normalize(pr.d));
               rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
             }
-            if (resume != f.k) w.rad[p] = f4(rv, 0.0f);
+            if (!fold) w.rad[p] = f4(rv, 0.0f);
             else if (!(f.ablate & 4u)) a = a + rv;
-          } else if (resume == f.k) {
+          } else if (fold) {
+            fold = false;
             resume = smp;
           }
         }
@@ -704,9 +708,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     if (kCount) flush_visits(vc, w.tot, kTotNodes);
     return;
   }
-  // bounce 0 of scenes traversed from L2/HBM stays path-major: per-pixel cost varies by orders of
-  // magnitude there (sky vs a 10M-triangle mesh), and a thread looping over all k samples of one
-  // pixel leaves the launch waiting on the blocks that drew the mesh (C5 measured 22.9 -> 67.9 ms)
+  // Bounce 0 path-major (thread <- path slot).  Scenes traversed from L2/HBM always: per-pixel
+  // cost varies by orders of magnitude there (sky vs a 10M-triangle mesh), and a thread looping
+  // over all k samples of one pixel leaves the launch waiting on the blocks that drew the mesh (C5
+  // measured 22.9 -> 67.9 ms).  LDS scenes when the batch has too few pixels (sharded frames).
   uint32_t n, per_in = 0u;
   if (kPrimary) {
     n = f.P * f.k;
@@ -1391,6 +1396,20 @@ SceneView scene_view(const Context& c) {
 
 static unsigned trace_lds(const SceneView& sv, bool lds, bool primary, uint32_t nseg) {
   return (lds ? sv.lds_bytes : 0u) + (primary ? 0u : (4u * (nseg + 1u) + 15u) / 16u * 16u);
+}
+
+// Pixel-major bounce 0 needs enough pixels to keep every resident thread busy: with fewer than
+// kPixelMajorItems pixels per thread of the resident grid, the per-thread quantisation (a thread
+// holds all k samples of its pixel) costs more than the radiance round trip it saves.  Measured
+// on C2 (profiles/r01h_pixel_major.txt): 1 GPU, 4.5 pixels/thread: 4.17 -> 3.74 ms; 2-way shard,
+// 2.3: 2.26 -> 2.24-2.28; 4-way, 1.1: 1.20 -> 1.28-1.29; 8-way: 0.72 -> 0.99.
+constexpr uint32_t kPixelMajorItems = 4;
+uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
+  if (sv.lds_bytes == 0) return 0u;
+  const unsigned lb = trace_lds(sv, true, true, 0);
+  const unsigned g = sv.width == 4u ? resident_grid((const void*)&k_trace<true, false, true, true>, lb)
+                                    : resident_grid((const void*)&k_trace<true, false, true, false>, lb);
+  return (uint64_t)f.P >= (uint64_t)g * kBlock * kPixelMajorItems ? 1u : 0u;
 }
 
 unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,

@@ -590,7 +590,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     fv.k = kk;
     fv.acc0 = f->frame_begin + done;
     fv.reset = (reset && done == 0) ? 1u : 0u;
-    fv.pixel_major = sv.lds_bytes != 0 ? 1u : 0u;  // must match k_trace's kLds dispatch
+    fv.pixel_major = bounce0_pixel_major(sv, fv);
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;

@@ -123,7 +123,7 @@ struct FrameView {
   uint32_t ablate;  // SPTR_ABLATE environment variable: timing experiments only (0 in normal use)
   float4* accum;    // per local pixel: running sample sum (xyz) + resume slot (w bits), see k_accum
   uint32_t reset;   // this batch starts the accumulation (frame_begin == 1, first batch)
-  uint32_t pixel_major;  // bounce 0 runs pixel-major and folds leading misses into accum (LDS scenes)
+  uint32_t pixel_major;  // bounce 0 runs pixel-major and folds leading misses into accum (bounce0_pixel_major)
 };
 
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
@@ -240,6 +240,7 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
                      uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
                    hipStream_t s);
+uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
