@@ -7,11 +7,18 @@ Inputs are synthetic (the reference's own procedural scene; no datasets).  --wor
 selects the other configurations (simple-path-tracer_amd/workloads.py); c5 is the HBM roofline run.
 
 One "step" = one complete render of the frame at the workload's spp: every rank renders its
-interleaved 32x32 tiles and resolves them; the resolved RGBA8 tiles are all-gathered over RCCL and
-rank 0 unpacks them into the W x H RGB8 image.
+interleaved 32x32 tiles (the reference's tile schedule, src/GLRenderer.cpp:335-350) and resolves
+them; the resolved RGBA8 tiles are all-gathered over RCCL and rank 0 unpacks them into the W x H
+RGB8 image.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+`--gpus N` without a torch.distributed environment launches the N ranks itself: a child
+`torch.distributed.run` of a fresh interpreter, started before this process touches the GPU (this
+process only waits for it and exits with its code).  `--dry-run` runs the same rank launch, tile
+schedule, all-gather and unpack on the CPU over gloo with a synthetic per-pixel pattern instead of
+the renderer (a check of the multi-rank plumbing that needs no GPU).
 
 value = all ranks' rays (closest-hit + any-hit queries, = the reference's rtcIntersect1 +
 rtcOccluded1 calls) / max-over-ranks wall time of the K timed steps.  Work per rank shrinks as N
@@ -20,7 +27,10 @@ grows (fixed frame), so scaling is "strong".
 import argparse
 import glob
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,10 +43,18 @@ import sptr  # noqa: E402
 import workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-STREAM_BYTES_PER_RAY = 36.0  # path id 4 + origin 12 + dir 12 in, t 4 + prim 4 out
+# VALU issue peak: a wave issues one VALU instruction per 2 cycles on its SIMD (MI355X_MICROARCH.md),
+# 256 CUs x 4 SIMDs x 0.5 x 2.4 GHz = 1.2288e12 wave-instructions/s
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 0.5 * 2.4e9
+# SURVEY.md §8(d) ray stream: path id 4 + origin 12 + dir 12 read, t 4 + prim 4 written.  A primary
+# ray reads nothing (raygen is fused into the bounce-0 trace), so it is charged the 8 B it writes.
+STREAM_READ_BYTES, STREAM_WRITE_BYTES = 28.0, 8.0
 L2_BYTES_PER_XCD = 4 << 20  # MI355X: 4 MB L2 per XCD (MI355X_MICROARCH.md)
 XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 8, "c4": 4, "c5": 1}
+# experiment knobs of the library and the build (timing studies only); a bench line records any that
+# is set, so a stray variable cannot silently change a measured number
+KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU")
 
 
 class _DevArray:
@@ -47,25 +65,35 @@ class _DevArray:
                                          "version": 3}
 
 
-def roofline(cnt, stats, layout, wl_name, steps):
-    """Roofline of the dominant kernel, k_trace (all bounces; one template, see DESIGN.md §Kernels).
+def _latest_profile(pattern):
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not found:
+        return None, None
+    with open(found[-1]) as f:
+        return json.load(f), os.path.relpath(found[-1], ROOT)
+
+
+def roofline(cnt, stats, layout, wl_name, steps, samples):
+    """Roofline of the dominant kernel, k_trace (all bounces; one template, see DESIGN.md §4).
 
     Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 + 64 n_node + 48 n_tri + 16 n_sph with the
-    visit counts taken from an instrumented pass over the same rays.  Which of those bytes are HBM
+    visit counts taken from an instrumented pass over the same rays; primary rays (raygen fused, no
+    input stream) are charged their 8 written bytes only.  Which of the node/primitive bytes are HBM
     bytes depends on where the scene lives:
-      lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU, so only
-           the 36-byte ray stream counts;
-      l2   scene (nodes + triangles + spheres + refs) fits one XCD's 4 MB L2: the compulsory
-           traffic is one scene copy per XCD per launch (8 x footprint) plus the ray stream —
-           counting every visit as HBM bytes would report more than the peak (C3: 1.15);
+      lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU;
+      l2   scene fits one XCD's 4 MB L2: one scene copy per XCD per launch (counting every visit as
+           HBM bytes would report more than the peak on C3);
       hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in §8(d).
-    The full B_ray figure is reported beside it (b_ray_full_gbs)."""
+    Beside the modelled fraction: counter_frac = FETCH_SIZE x2 + WRITE_SIZE per launch (the latest
+    profiles/r*_pmc_<wl>_trace.json) over the live launch time, and valu_issue_frac = SQ_INSTS_VALU per
+    launch (profiles/r*_sq_<wl>_trace.json) over the live launch time and the 1.23e12/s issue peak."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
     launches_per_step = max(1, launches // max(1, steps))
     traced = cnt.rays_closest - cnt.rays_tail  # closest-hit queries of k_trace (the rest run in k_tail)
-    stream = STREAM_BYTES_PER_RAY * traced
-    node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0  # 64 BVH2, 128 BVH4
+    primary = min(traced, samples)  # one primary ray per pixel sample, all traced by k_trace
+    stream = (STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (traced - primary) + STREAM_WRITE_BYTES * primary
+    node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0
     scene = node_b * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
     lds = layout["lds_bytes"] > 0
     footprint = sum(layout[k] for k in ("node_bytes", "tri_bytes", "sphere_bytes", "prim_ref_bytes"))
@@ -73,48 +101,149 @@ def roofline(cnt, stats, layout, wl_name, steps):
     hbm_alg = stream + {"lds": 0.0, "l2": XCDS * footprint * launches_per_step, "hbm": scene}[residency]
     per_launch = hbm_alg / launches_per_step
     achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic, src = None, None
-    # latest round's PMC pass (tools/gpu_profile.sh): FETCH_SIZE x2 + WRITE_SIZE per k_trace launch
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{wl_name}_trace.json")))
-    if found:
-        pmc = found[-1]
-        with open(pmc) as f:
-            d = json.load(f)
-        traffic, src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
-    return {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
-            "launches_per_step": launches_per_step,
-            "scene_in_lds": lds, "scene_residency": residency, "scene_bytes": int(footprint),
-            "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
-            "per_ray": {"nodes": round(cnt.node_visits / max(1, traced), 3),
-                        "tris": round(cnt.tri_tests / max(1, traced), 3),
-                        "spheres": round(cnt.sphere_tests / max(1, traced), 3)}}
+    pmc, pmc_src = _latest_profile(f"r*_pmc_{wl_name}_trace.json")
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    sq, sq_src = _latest_profile(f"r*_sq_{wl_name}_trace.json")
+    valu = sq.get("valu_per_launch") if sq else None
+    out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": pmc_src,
+           "counter_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s else None,
+           "valu_issue_frac": round(valu / avg_launch_s / VALU_PEAK_WAVE_INSTR_PER_S, 4) if valu and avg_launch_s else None,
+           "valu_source": sq_src,
+           "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+           "launches_per_step": launches_per_step,
+           "scene_in_lds": lds, "scene_residency": residency, "scene_bytes": int(footprint),
+           "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
+           "per_ray": {"nodes": round(cnt.node_visits / max(1, traced), 3),
+                       "tris": round(cnt.tri_tests / max(1, traced), 3),
+                       "spheres": round(cnt.sphere_tests / max(1, traced), 3)}}
+    fr = {"hbm_model": out["frac"], "hbm_counters": out["counter_frac"], "valu_issue": out["valu_issue_frac"]}
+    known = {k: v for k, v in fr.items() if v is not None}
+    out["binding"] = max(known, key=known.get) if known else None
+    return out
+
+
+def host_cpus():
+    """What this process may use: hardware threads, the affinity mask, the cgroup CPU quota."""
+    hw = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = hw
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    granted = min(aff, quota) if quota else aff
+    return {"hardware_concurrency": hw, "affinity": aff, "cgroup_quota_cpus": quota, "granted": granted,
+            "model": model}
 
 
 def cpu_baseline(wl, flat, cam):
     """The oracle (C++ restatement of the reference's CPU wavefront integrator, Embree semantics with
-    its own median-split BVH) on the host cores, on the same scene and camera: a reported baseline."""
+    its own binned-SAH BVH) on the host cores, on the same scene and camera: a reported baseline.
+    Two runs: every CPU this process is granted, and one fewer (the reference's TBB policy,
+    src/main.cpp:127-135)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure, used here only as the timed CPU baseline
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
     spp = min(wl.spp, CPU_SAMPLE_SPP.get(wl.name, 1))
     scene = {k: getattr(flat, k) for k in ("positions", "indices", "tri_geom_first", "spheres", "geom_material")}
     t0 = time.perf_counter()
     P = oracle.Prepared(scene, bvh=True)
     t_build = time.perf_counter() - t0
     faces = workloads.hdr_env_faces() if wl.hdr_env else None
-    t0 = time.perf_counter()
-    _, _, cnt = P.render(cam.as_array(), wl.width, wl.height, oracle.preset_materials(wl.scene == "default_emitter"),
-                         oracle.default_lights(), frames=spp, max_depth=wl.max_depth, threads=threads, env_faces=faces)
-    dt = time.perf_counter() - t0
-    rays = cnt["rays_closest"] + cnt["rays_shadow"]
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{wl.width}x{wl.height} x {spp} spp of {wl.spp} ({'full workload' if spp == wl.spp else 'first spp'})"
-                      f", {rays} rays in {dt:.2f} s (+{t_build:.2f} s BVH build); oracle/wf_oracle.cpp with a"
-                      f" median-split BVH, std::thread over 32x32 tiles",
-            "msamples_per_s": round(cnt["samples"] / dt / 1e6, 3)}
+    mats = oracle.preset_materials(wl.scene == "default_emitter")
+
+    def run(threads):
+        t0 = time.perf_counter()
+        _, _, cnt = P.render(cam.as_array(), wl.width, wl.height, mats, oracle.default_lights(), frames=spp,
+                             max_depth=wl.max_depth, threads=threads, env_faces=faces)
+        dt = time.perf_counter() - t0
+        rays = cnt["rays_closest"] + cnt["rays_shadow"]
+        return rays, cnt["samples"], dt
+
+    n_all = cpus["granted"]
+    rays, samples, dt = run(n_all)
+    res = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": n_all, "kind": "port",
+           "sample": f"{wl.width}x{wl.height} x {spp} spp of {wl.spp} ({'full workload' if spp == wl.spp else 'first spp'})"
+                     f", {rays} rays in {dt:.2f} s (+{t_build:.2f} s BVH build); oracle/wf_oracle.cpp with a"
+                     f" binned-SAH BVH, std::thread over 32x32 tiles with a dynamic tile counter",
+           "msamples_per_s": round(samples / dt / 1e6, 3), "cpu": cpus}
+    if n_all > 1:
+        r1, s1, d1 = run(n_all - 1)
+        res["cores_minus_1"] = {"cores": n_all - 1, "value": round(r1 / d1 / 1e6, 3),
+                                "msamples_per_s": round(s1 / d1 / 1e6, 3),
+                                "policy": "reference TBB policy: hardware_concurrency - 1 (src/main.cpp:127-135)"}
+    return res
+
+
+def interactive(steps):
+    """The reference's own usage: 1 spp per render() call, progressive accumulation, RGB8 read back
+    every frame, as GLRenderer::renderLoop drives a backend (src/GLRenderer.cpp:161-176).  Runs the C++
+    harness (backends::HipBackend through the C ABI) as a child process."""
+    cli = os.path.join(ROOT, "simple-path-tracer_amd", "sptr_cli")
+    out = []
+    for w, h in ((800, 600), (1920, 1080)):
+        r = subprocess.run([cli, "--scene", "default", "--w", str(w), "--h", str(h), "--spp", str(steps),
+                            "--warmup", "10", "--json", "--out", "/dev/null"], capture_output=True, text=True,
+                           timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"sptr_cli failed: {r.stderr[-2000:]}")
+        out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    return out
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """One process per GPU: run this script under torch.distributed.run in a child process (this
+    process has not touched the GPU and never does; it waits and returns the child's exit code)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def dry_run(args, wl, world, rank):
+    """CPU plumbing check of the multi-rank step (gloo): each rank packs its interleaved tiles of a
+    synthetic per-pixel pattern with the product's host tile packing (the twin of the device
+    resolve's tile layout), one all-gather, rank 0 unpacks and compares with the whole pattern."""
+    import numpy as np
+
+    W, H = wl.width, wl.height
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.uint32)
+    pattern = np.stack([(xx * 7 + yy) & 255, (xx ^ yy) & 255, (xx * 13 + yy * 5) & 255], -1).astype(np.uint8)
+    tiles = sptr.pack_tiles(pattern, world, rank)
+    gathered = torch.zeros(world * tiles.size, dtype=torch.int32)
+    dist.all_gather_into_tensor(gathered, torch.from_numpy(tiles.view(np.int32)))
+    mine = torch.tensor([float(((tiles >> 24) == 255).sum())], dtype=torch.float64)  # pixels inside the image
+    dist.all_reduce(mine)
+    if rank == 0:
+        img = sptr.unpack_tiles(gathered.numpy().view(np.uint32), world, W, H)
+        ok = bool(np.array_equal(img, pattern)) and int(mine.item()) == W * H
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": dist.get_world_size(),
+                          "backend": dist.get_backend(), "workload": wl.name, "tiles_per_rank": int(tiles.size // 1024),
+                          "pixels_covered": int(mine.item()), "gather_ok": ok}), flush=True)
+        if not ok:
+            sys.exit(1)
 
 
 def main():
@@ -124,6 +253,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c2", choices=sorted(workloads.WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-interactive", action="store_true", help="skip the 1-spp progressive-frame leg")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo check of the rank launch + tile gather")
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
@@ -138,13 +269,34 @@ def main():
     wl = workloads.WORKLOADS[args.workload]
     W, H = wl.width, wl.height
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     distributed = world > 1
+    if distributed and args.emulate_shards:
+        print("bench.py: --emulate-shards is a one-GPU timing experiment; not allowed with several ranks",
+              file=sys.stderr)
+        sys.exit(2)
+
+    if args.dry_run:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dry_run(args, wl, world, rank)
+        dist.destroy_process_group()
+        return
+
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     dev = torch.device("cuda", local)
 
     r = sptr.Renderer(local)
@@ -159,7 +311,7 @@ def main():
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
     cam = workloads.camera(wl)
-    shards = args.emulate_shards if (args.emulate_shards and not distributed) else world
+    shards = args.emulate_shards if args.emulate_shards else world
     shard = 0 if args.emulate_shards else rank
     tiles_per_rank = sptr.tiles_per_rank(W, H, shards)
     send = torch.zeros(tiles_per_rank * 1024, dtype=torch.int32, device=dev)
@@ -216,17 +368,20 @@ def main():
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, rays, samples = float(tmax[0]), float(tsum[1]), float(tsum[2])
+        # the gathered frame is the same bytes a 1-GPU render gives (tests/test_gpu_parity.py shard union)
+        assert int(tsum[2]) == W * H * wl.spp * args.steps, (int(tsum[2]), W * H * wl.spp * args.steps)
 
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
                     for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum") if args.stage_timing
                               else ("trace0", "trace"))}
+        knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),
             "unit": "Mrays/s",
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if distributed else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -238,7 +393,10 @@ def main():
             "config": {"workload": wl.description, "scene": os.path.basename(wl.scene), "width": W, "height": H,
                        "spp": wl.spp, "max_depth": wl.max_depth,
                        "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL all-gather"},
-            "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
+            "world_size": world,
+            "collective": ("RCCL all_gather_into_tensor of the RGBA8 tiles, once per step" if distributed
+                           else "none (1 rank)"),
+            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, samples),
             "stage_ms_per_step": stage_ms,
             "tail_rays_per_step": int(sum(s.rays_tail for s in stats) / args.steps),
             "rays_per_step": int(rays / args.steps),
@@ -247,8 +405,12 @@ def main():
                       "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},
             "cpu_baseline": None,
         }
+        if knobs:
+            line["experiment_knobs"] = knobs
         if args.emulate_shards:
             line["emulated"] = f"shard 0 of {shards} on one GPU: per-rank work of a {shards}-GPU run (not a multi-GPU value)"
+        if world == 1 and not args.no_interactive and not args.emulate_shards:
+            line["interactive"] = interactive(200)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(wl, flat, cam)
         print(json.dumps(line), flush=True)

@@ -393,6 +393,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     c.root = kNoHit;
     c.root4 = kNoHit;
     c.num_nodes4 = 0;
+    c.stack_need2 = c.stack_need4 = 0;
     return SPTR_OK;
   }
   Tmp tmp;
@@ -465,6 +466,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     c.root4 = c.root;
     c.num_nodes4 = 0;
     c.bvh_depth = 0;
+    c.stack_need2 = c.stack_need4 = 0;
   } else {
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
@@ -480,7 +482,12 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     LB_CHECK(hipStreamSynchronize(s));
     c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;
-    if (dep >= (uint32_t)kStack) {
+    // a BVH2 node at depth d holds at most d pushed entries and pushes one more; a BVH4 node (BVH2
+    // depth 2*d4) holds at most 3*d4 and pushes up to three more; internal nodes lie at BVH2 depth
+    // <= dep - 1
+    c.stack_need2 = dep;
+    c.stack_need4 = 3u * ((dep > 0u ? dep - 1u : 0u) / 2u + 1u);
+    if (c.stack_need2 > (uint32_t)kStack) {
       c.err = "lbvh: tree depth " + std::to_string(dep) + " exceeds the traversal stack";
       return SPTR_ERR_INVALID;
     }

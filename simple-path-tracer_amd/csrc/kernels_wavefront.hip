@@ -265,6 +265,7 @@ __device__ __forceinline__ bool sphere_occ(float4 s, const Ray& r, float tnear, 
 
 struct Visits {
   uint32_t nodes = 0, tris = 0, sph = 0;
+  uint32_t stack_overflow = 0;  // a push was dropped (reported through kTotStackOverflow)
 };
 
 // Leaf = contiguous range of sorted primitive references (LBVH subtrees cover contiguous ranges):
@@ -373,6 +374,7 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
         R = s;
       }
       if (sp < kStack) stack.put(sp++, R);
+      else vc.stack_overflow = 1u;
       cur = L;
     } else if (hl) {
       cur = L;
@@ -430,6 +432,8 @@ __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t*
       if (h1 && (!h0 || t1 < tn)) { tn = t1; cn = c1; kn = 1u; }
       if (h2 && ((!h0 && !h1) || t2 < tn)) { tn = t2; cn = c2; kn = 2u; }
       if (h3 && ((!h0 && !h1 && !h2) || t3 < tn)) { tn = t3; cn = c3; kn = 3u; }
+      const uint32_t npush = (h0 && kn != 0u) + (h1 && kn != 1u) + (h2 && kn != 2u) + (h3 && kn != 3u);
+      if (sp + (int)npush > kStack) vc.stack_overflow = 1u;
       if (h3 && kn != 3u && sp < kStack) stack.put(sp++, c3);
       if (h2 && kn != 2u && sp < kStack) stack.put(sp++, c2);
       if (h1 && kn != 1u && sp < kStack) stack.put(sp++, c1);
@@ -479,6 +483,11 @@ __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv
                                            uint32_t& ref, Visits& vc, LdsStack& ls) {
   if (kW4) return traverse4<kAny, kCount>(sc.nodes4, sc.prim_ref, sc.tris, sc.sph, sv.root4, r, tnear, tfar, ref, vc, ls);
   return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
+}
+
+// Sticky stack-overflow report (one store per wave that saw a dropped push).
+__device__ __forceinline__ void report_stack(const Visits& vc, unsigned long long* tot) {
+  if (__ballot(vc.stack_overflow != 0u) && lane_id() == 0u) tot[kTotStackOverflow] = 1ull;
 }
 
 __device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long long* tot, int base) {
@@ -705,6 +714,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
     }
     seg_publish(w.segH, &s_cnt, per);
+    report_stack(vc, w.tot);
     if (kCount) flush_visits(vc, w.tot, kTotNodes);
     return;
   }
@@ -770,6 +780,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
   }
   seg_publish(w.segH, &s_cnt, sd.per);
+  report_stack(vc, w.tot);
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
@@ -1078,6 +1089,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW_WAVES) k_shadow(SceneView 
   if (lane_id() == 0u) atomicAdd(&s_rays, rays);
   __syncthreads();
   if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
+  report_stack(vc, w.tot);
   if (kCount) flush_visits(vc, w.tot, kTotShNodes);
 }
 
@@ -1167,6 +1179,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
     w.bstat_closest[blockIdx.x] += s_rays[0];
     w.bstat[blockIdx.x] += s_rays[1];
   }
+  report_stack(vc, w.tot);
 }
 
 // --------------------------------------------------------------------------------- k_accum / resolve
@@ -1265,7 +1278,7 @@ __global__ void __launch_bounds__(kBlock) k_unpack(const uint32_t* g, int G, uin
 // --------------------------------------------------------------------------------- query kernels
 __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* tri_orig, const uint32_t* sph_orig,
                                                   const float* rays, uint32_t n, int anyhit, uint32_t* ref_out,
-                                                  float* t_out, float* ng_out, uint8_t* occ) {
+                                                  float* t_out, float* ng_out, uint8_t* occ, uint32_t* stack_overflow) {
   __shared__ LdsStack s_stack;
   const Staged sg{sv.nodes, sv.nodes4, sv.prim_ref, sv.tris, sv.sph};
   Visits vc;
@@ -1303,6 +1316,7 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
     ng_out[(size_t)i * 3 + 1] = ng.y;
     ng_out[(size_t)i * 3 + 2] = ng.z;
   }
+  if (__ballot(vc.stack_overflow != 0u) && lane_id() == 0u) *stack_overflow = 1u;
 }
 
 __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, uint32_t* rng) {
@@ -1342,6 +1356,7 @@ struct GridCache {
 static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
   static GridCache cache[32];
   static int cus = 0;
+  int per = 0;
   for (GridCache& g : cache)
     if (g.fn == fn && g.lds == lds_bytes) return g.blocks;
   if (cus == 0) {
@@ -1349,14 +1364,15 @@ static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
-  int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, lds_bytes) != hipSuccess || per <= 0) per = 4;
-  static int cap = -1;  // SPTR_MAX_BLOCKS_PER_CU: experiment knob (resident blocks per CU)
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static int cap = -1;  // SPTR_MAX_BLOCKS_PER_CU: experiment knob (resident blocks per CU), experiment builds only
   if (cap < 0) {
     const char* e = getenv("SPTR_MAX_BLOCKS_PER_CU");
     cap = e ? atoi(e) : 0;
   }
   if (cap > 0 && per > cap) per = cap;
+#endif
   unsigned blocks = (unsigned)(cus * per);
   if (blocks > kMaxSegs) blocks = kMaxSegs;  // producer grids index the segment tables
   for (GridCache& g : cache)
@@ -1386,6 +1402,9 @@ SceneView scene_view(const Context& c) {
   const uint64_t bytes2 = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
                           ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.width = c.bvh_width ? c.bvh_width : (bytes2 <= kLdsSceneBytes ? 2u : 4u);
+  // never a width whose worst-case traversal stack exceeds kStack (build_lbvh rejects trees that
+  // even BVH2 cannot traverse)
+  if (s.width == 4u && c.stack_need4 > (uint32_t)kStack) s.width = 2u;
   s.prim_ref = static_cast<const uint32_t*>(c.prim_ref.p);
   const uint64_t node_bytes = s.width == 4u ? (uint64_t)c.num_nodes4 * sizeof(Bvh4Node) : (uint64_t)c.num_nodes * 64;
   const uint64_t bytes = node_bytes + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
@@ -1512,9 +1531,9 @@ void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int
 }
 
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
-                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, hipStream_t s) {
+                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, uint32_t* stack_overflow, hipStream_t s) {
   hipLaunchKernelGGL(k_query, dim3(grid_for(n)), dim3(kBlock), 0, s, sv, tri_orig, sph_orig, rays, n, anyhit ? 1 : 0,
-                     ref, t, ng, occ);
+                     ref, t, ng, occ, stack_overflow);
 }
 
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s) {

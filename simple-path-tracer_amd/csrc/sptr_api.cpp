@@ -26,6 +26,7 @@ int fail(Context& c, int code, const std::string& msg) {
   c.err = msg;
   return code;
 }
+int sync_pending(Context& c);
 
 #define API_HIP(x)                                                                          \
   do {                                                                                      \
@@ -92,36 +93,24 @@ inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
   return shard_pixel(c.W, c.H, c.G, c.R, l, x, y);
 }
 
-int ensure_pixels(Context& c, int W, int H, int G, int R, bool& resized) {
-  resized = false;
-  if (c.W == W && c.H == H && c.G == G && c.R == R && c.accum.p) return SPTR_OK;
-  const uint32_t local_tiles = shard_tiles(W, H, G, R);
-  c.W = W;
-  c.H = H;
-  c.G = G;
-  c.R = R;
-  c.local_tiles = local_tiles;
-  c.P = local_tiles * (uint32_t)kTilePixels;
-  API_HIP(ensure_buf(c.accum, (size_t)c.P * 16));
-  API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
-  API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
-  API_HIP(hipMemset(c.accum.p, 0, (size_t)c.P * 16));
-  API_HIP(hipMemset(c.tiles.p, 0, (size_t)c.P * 4));
-  API_HIP(hipMemset(c.image.p, 0, (size_t)W * H * 3));
-  c.last_samples = 0;
-  resized = true;
-  return SPTR_OK;
+// device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
+// L shadow tasks of ts float4s
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 16 + 16 + (uint64_t)L * ts * 16; }
+// fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
+uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
+  const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * 16;
 }
 
-// device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
-// L shadow tasks of ts float4s (the segment slack is excluded)
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 16 + 16 + (uint64_t)L * ts * 16; }
-
-int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k) {
+// k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
+// pixel slot it owns, so its segment slack is kMaxSegs * kBlock * k records (k_slack = k); every
+// other producer needs kMaxSegs * kBlock (k_slack = 1).
+int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
   L = L ? L : 1u;
-  // hit records: the pixel-major bounce-0 trace gives each block a segment of k records per pixel
-  // slot it owns, so the segment slack is kMaxSegs * kBlock * k records
-  API_HIP(ensure_buf(c.w_hrec, ((size_t)cap + (size_t)kMaxSegs * kBlock * k) * 16));
+  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * 16;
+  const bool grow = c.w_hrec.bytes < hrec_bytes || !(c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p);
+  if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
+  API_HIP(ensure_buf(c.w_hrec, hrec_bytes));
   if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
   // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
   // with per = ceil(n / (G*kBlock)) * kBlock, so the segment space G*per can exceed n by up to
@@ -196,8 +185,13 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.cam_u = v3(k.up[0], k.up[1], k.up[2]);
   v.half_w = k.half_width;
   v.half_h = k.half_height;
+#ifdef SPTR_EXPERIMENT_KNOBS
+  // SPTR_ABLATE (timing experiments only: wrong images by design); experiment builds only
   static const uint32_t ablate = getenv("SPTR_ABLATE") ? (uint32_t)atoi(getenv("SPTR_ABLATE")) : 0u;
   v.ablate = ablate;
+#else
+  v.ablate = 0u;
+#endif
   v.accum = static_cast<float4*>(c.accum.p);
   v.reset = 0;
   v.pixel_major = 0;
@@ -288,6 +282,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   unsigned long long tot[kTotWords];
   API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
   if (tot[kTotOverflow]) return fail(c, SPTR_ERR_HIP, "render: segmented stream overflow (internal error)");
+  if (tot[kTotStackOverflow]) return fail(c, SPTR_ERR_HIP, "render: BVH traversal stack overflow (internal error)");
   if (!stats) return SPTR_OK;
   stats->ms_total = ms[0];
   stats->ms_raygen = 0.0;  // raygen is fused into the bounce-0 trace (ms_trace0)
@@ -315,6 +310,31 @@ int collect_pending(Context& c, sptr_stats* stats) {
 // Device work of the pending render calls must be complete before a host read of their results.
 int sync_pending(Context& c) {
   if (c.pending) API_HIP(hipStreamSynchronize(c.pending_stream));
+  return SPTR_OK;
+}
+
+// Pixel buffers of a (W, H, shard) configuration.  A pending asynchronous render may still use the
+// old buffers, so it is waited for before they are reallocated, and the clears are enqueued on the
+// render stream (ordered before this call's kernels).
+int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& resized) {
+  resized = false;
+  if (c.W == W && c.H == H && c.G == G && c.R == R && c.accum.p) return SPTR_OK;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  const uint32_t local_tiles = shard_tiles(W, H, G, R);
+  c.W = W;
+  c.H = H;
+  c.G = G;
+  c.R = R;
+  c.local_tiles = local_tiles;
+  c.P = local_tiles * (uint32_t)kTilePixels;
+  API_HIP(ensure_buf(c.accum, (size_t)c.P * 16));
+  API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
+  API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
+  API_HIP(hipMemsetAsync(c.accum.p, 0, (size_t)c.P * 16, s));
+  API_HIP(hipMemsetAsync(c.tiles.p, 0, (size_t)c.P * 4, s));
+  API_HIP(hipMemsetAsync(c.image.p, 0, (size_t)W * H * 3, s));
+  c.last_samples = 0;
+  resized = true;
   return SPTR_OK;
 }
 
@@ -545,8 +565,11 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const int ntiles = ((f->width + kTile - 1) / kTile) * ((f->height + kTile - 1) / kTile);
   if (R >= ntiles) return fail(c, SPTR_ERR_INVALID, "render: more shards than tiles");
   if ((uint64_t)f->width * f->height > (1ull << 28)) return fail(c, SPTR_ERR_INVALID, "render: image too large");
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  if (c.pending && s != c.pending_stream)
+    return fail(c, SPTR_ERR_INVALID, "render: asynchronous renders must stay on one stream until sptr_collect_stats");
   bool resized = false;
-  int rc = ensure_pixels(c, f->width, f->height, G, R, resized);
+  int rc = ensure_pixels(c, f->width, f->height, G, R, s, resized);
   if (rc != SPTR_OK) return rc;
   const bool reset = f->frame_begin == 1;
   if (!reset && f->frame_begin != c.last_samples + 1)
@@ -559,20 +582,26 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
         const uint64_t held = c.wave_cap ? c.wave_cap * wave_path_bytes(c.wave_L, c.wave_ts) : 0ull;
         const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
-        const uint64_t fit = (uint64_t)(((double)free_b + (double)held) * kWaveMemFraction) / wave_path_bytes(L, task_stride(c));
+        // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
+        const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
+                              (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u));
+        const uint64_t fit = budget > 0.0 ? (uint64_t)budget / wave_path_bytes(L, task_stride(c)) : 0ull;
         wave_paths = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(wave_paths, fit));
       }
     }
   }
   uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
   k = std::min<uint32_t>(k, f->spp);
-  rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k);
-  if (rc != SPTR_OK) return rc;
-
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
-  if (c.pending && s != c.pending_stream)
-    return fail(c, SPTR_ERR_INVALID, "render: asynchronous renders must stay on one stream until sptr_collect_stats");
   const SceneView sv = scene_view(c);
+  {
+    // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
+    FrameView probe = frame_view(c, *f);
+    probe.k = k;
+    const uint32_t k_slack = bounce0_pixel_major(sv, probe) ? k : 1u;
+    rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
+    if (rc != SPTR_OK) return rc;
+  }
+
   const ShadeView sh = shade_view(c);
   const WaveView w = wave_view(c);
   FrameView fv = frame_view(c, *f);
@@ -711,16 +740,21 @@ static int run_query(sptr_ctx* x, const float* rays, uint32_t n, bool anyhit, ui
   const size_t rb = (size_t)n * 32, refb = (size_t)n * 4, tb = (size_t)n * 4, nb = (size_t)n * 12, ob = (size_t)n;
   API_HIP(ensure_buf(c.qbuf, rb + refb + tb + nb + ob + 64));
   char* base = static_cast<char*>(c.qbuf.p);
+  uint32_t* d_sflag = reinterpret_cast<uint32_t*>(base + (rb + refb + tb + nb + ob + 15) / 16 * 16);
   float* d_rays = reinterpret_cast<float*>(base);
   uint32_t* d_ref = reinterpret_cast<uint32_t*>(base + rb);
   float* d_t = reinterpret_cast<float*>(base + rb + refb);
   float* d_ng = reinterpret_cast<float*>(base + rb + refb + tb);
   uint8_t* d_occ = reinterpret_cast<uint8_t*>(base + rb + refb + tb + nb);
   API_HIP(hipMemcpy(d_rays, rays, rb, hipMemcpyHostToDevice));
+  API_HIP(hipMemset(d_sflag, 0, 4));
   launch_query(scene_view(c), static_cast<const uint32_t*>(c.tri_orig.p), static_cast<const uint32_t*>(c.sph_orig.p),
-               d_rays, n, anyhit, d_ref, d_t, d_ng, d_occ, c.stream);
+               d_rays, n, anyhit, d_ref, d_t, d_ng, d_occ, d_sflag, c.stream);
   API_HIP(hipGetLastError());
   API_HIP(hipStreamSynchronize(c.stream));
+  uint32_t sflag = 0;
+  API_HIP(hipMemcpy(&sflag, d_sflag, 4, hipMemcpyDeviceToHost));
+  if (sflag) return fail(c, SPTR_ERR_HIP, "query: BVH traversal stack overflow (internal error)");
   if (anyhit) {
     API_HIP(hipMemcpy(occ, d_occ, ob, hipMemcpyDeviceToHost));
     return SPTR_OK;

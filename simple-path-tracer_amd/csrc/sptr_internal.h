@@ -38,7 +38,11 @@ constexpr int kTile = 32;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kMaxLights = 8;
 constexpr int kMaxDepth = 32;
-constexpr int kStack = 64;
+// Traversal stack entries.  BVH2 pushes at most one entry per internal level, BVH4 at most three,
+// so a tree of height h needs h (BVH2) or 3 * ((h - 1) / 2 + 1) (BVH4) entries; build_lbvh records
+// both bounds, scene_view never picks a width whose bound exceeds kStack, and a push that would
+// still overflow is dropped and reported (kTotStackOverflow), never silent.
+constexpr int kStack = 96;
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;  // scenes up to this size are staged whole into LDS
 
@@ -136,6 +140,7 @@ enum : int {
   kTotShNodes, kTotShPrims,      // k_shadow visit counts
   kTotOverflow,
   kTotTail,         // closest-hit queries traced by k_tail
+  kTotStackOverflow,  // a traversal push was dropped (cannot happen within the build's stack bound)         // closest-hit queries traced by k_tail
   kTotWords
 };
 
@@ -191,6 +196,7 @@ struct Context {
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_nodes4 = 0, root4 = 0;
+  uint32_t stack_need2 = 0, stack_need4 = 0;  // traversal stack entries the BVH2 / BVH4 can need
   DevBuf nodes4;
   uint32_t num_tri_geoms = 0;
   std::vector<uint32_t> geom_first;     // host copy for primID derivation
@@ -247,7 +253,7 @@ void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
                    hipStream_t s);
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
-                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, hipStream_t s);
+                  bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, uint32_t* stack_overflow, hipStream_t s);
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s);
 
 }  // namespace sptr

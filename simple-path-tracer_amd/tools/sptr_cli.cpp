@@ -4,6 +4,12 @@
 // one render() per frame, progressive accumulation.
 //   sptr_cli [--scene default|default_emitter|test_triangle|sphere_mesh:STACKS:SLICES|gltf:PATH]
 //            [--w 800] [--h 600] [--spp 4] [--depth 6] [--env sky|FILE.hdr] [--out image.ppm]
+//            [--warmup N] [--json]
+// --spp N renders N progressive frames of 1 spp each (GLRenderer's m_accumulated_samples loop);
+// --warmup N renders N untimed frames first (then restarts the accumulation by a camera change);
+// --json prints one line with per-frame wall-clock statistics (render + RGB8 read back, as the
+// window loop pays them) for bench.py's interactive leg.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -34,7 +40,8 @@ static bool build_scene(const std::string& s, scene::SceneDesc& sd, MaterialMana
 
 int main(int argc, char** argv) {
   std::string scene_name = "default", env = "sky", out = "image.ppm";
-  int w = 800, h = 600, spp = 4, depth = 6;
+  int w = 800, h = 600, spp = 4, depth = 6, warmup = 0;
+  bool json = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -45,8 +52,10 @@ int main(int argc, char** argv) {
     else if (a == "--depth") depth = std::atoi(next());
     else if (a == "--env") env = next();
     else if (a == "--out") out = next();
+    else if (a == "--warmup") warmup = std::atoi(next());
+    else if (a == "--json") json = true;
     else {
-      std::fprintf(stderr, "usage: %s [--scene S] [--w W] [--h H] [--spp N] [--depth D] [--env sky|F.hdr] [--out F]\n",
+      std::fprintf(stderr, "usage: %s [--scene S] [--w W] [--h H] [--spp N] [--depth D] [--env sky|F.hdr] [--out F] [--warmup N] [--json]\n",
                    argv[0]);
       return 2;
     }
@@ -77,17 +86,37 @@ int main(int argc, char** argv) {
     return 1;
   }
   std::vector<unsigned char> img(size_t(w) * h * 3);
+  if (warmup > 0) {
+    Camera wcam(vec3{0.0f, 3.0f, 8.5f}, vec3{0.0f, 1.0f, 0.0f}, vec3{0.0f, 1.0f, 0.0f}, 60.0f, float(w) / float(h));
+    for (int f = 0; f < warmup; ++f) be.render(img.data(), w, h, wcam);  // the camera change below resets
+  }
   uint64_t rays = 0;
   double ms = 0.0;
+  std::vector<double> frame_ms;
+  frame_ms.reserve(size_t(spp));
   const auto t0 = std::chrono::steady_clock::now();
   for (int f = 0; f < spp; ++f) {
+    const auto f0 = std::chrono::steady_clock::now();
     be.render(img.data(), w, h, cam);
+    frame_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
     rays += be.stats().rays_closest + be.stats().rays_shadow;
     ms += be.stats().ms_total;
   }
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  std::printf("scene=%s %dx%d spp=%d depth=%d: %.2f ms device, %.2f ms wall, %.1f Mrays/s (device)\n",
-              scene_name.c_str(), w, h, spp, depth, ms, wall, ms > 0 ? rays / (ms * 1e3) : 0.0);
+  if (json) {
+    std::vector<double> s = frame_ms;
+    std::sort(s.begin(), s.end());
+    auto pct = [&](double q) { return s.empty() ? 0.0 : s[std::min(s.size() - 1, size_t(q * double(s.size())))]; };
+    std::printf("{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"frames\": %d, \"spp_per_frame\": 1, "
+                "\"depth\": %d, \"ms_per_frame_wall\": %.4f, \"ms_per_frame_p50\": %.4f, \"ms_per_frame_p99\": %.4f, "
+                "\"ms_per_frame_device\": %.4f, \"fps\": %.1f, \"mrays_per_s_wall\": %.1f, "
+                "\"path\": \"backends::HipBackend::render (sptr_render + sptr_read_rgb8 per frame)\"}\n",
+                scene_name.c_str(), w, h, spp, depth, wall / spp, pct(0.5), pct(0.99), ms / spp,
+                wall > 0 ? 1e3 * spp / wall : 0.0, wall > 0 ? rays / (wall * 1e3) : 0.0);
+  } else {
+    std::printf("scene=%s %dx%d spp=%d depth=%d: %.2f ms device, %.2f ms wall, %.1f Mrays/s (device)\n",
+                scene_name.c_str(), w, h, spp, depth, ms, wall, ms > 0 ? rays / (ms * 1e3) : 0.0);
+  }
   FILE* fp = std::fopen(out.c_str(), "wb");
   if (!fp) return 1;
   std::fprintf(fp, "P6\n%d %d\n255\n", w, h);

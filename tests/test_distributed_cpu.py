@@ -61,3 +61,37 @@ def test_two_rank_tile_gather(tmp_path):
     assert np.array_equal(np.load(tmp_path / "img.npy"), full)
     # rays are partitioned, not duplicated: the sum over ranks equals the single-rank count
     assert float(np.load(tmp_path / "rays.npy")[0]) == cnt["rays_closest"] + cnt["rays_shadow"]
+
+
+def _bench(args, env=None, timeout=240):
+    import json
+    import subprocess
+
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=ROOT)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`bench.py --gpus 2` with no torch.distributed environment launches 2 ranks itself (a child
+    torch.distributed.run); --dry-run runs the tile schedule + all-gather + unpack over gloo."""
+    rc, line, err = _bench(["--gpus", "2", "--dry-run", "--workload", "c1"])
+    assert rc == 0, err[-3000:]
+    assert line["dry_run"] and line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["gather_ok"] and line["pixels_covered"] == 256 * 256
+
+
+def test_bench_gpus_1_stays_single_rank():
+    rc, line, err = _bench(["--gpus", "1", "--dry-run", "--workload", "c2"])
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == 1 and line["gather_ok"] and line["pixels_covered"] == 1920 * 1080
+
+
+def test_bench_rejects_inconsistent_world():
+    rc, line, err = _bench(["--gpus", "1", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and line is None and "WORLD_SIZE=2" in err

@@ -1,0 +1,188 @@
+"""GPU parity on the BASELINE configurations the other suites only cover at reduced shape:
+
+  C3  rattan chair glTF (6116 tris) + the synthetic HDR environment (written as Radiance .hdr, read
+      back through the product's reader, equirect -> 512^2 cube faces), rendered vs the oracle fed
+      the same flat scene and faces;
+  C4  3840x2160: pixel/tile indexing and the 8-way interleaved shard union at full 4K size, and the
+      whole 4K frame (2 spp) vs the oracle;
+  C5  the 10M-triangle sphere mesh at full tessellation (1250 x 4000; BVH height ~45, BVH4 traversed
+      from HBM): first hits on camera + random rays and a small render vs the oracle with its own BVH.
+
+Tolerances as in test_gpu_parity.py's docstring (bit-exact first hits >= 99.99 %, images >= 99.9 %
+exact RGB8 pixels and relative L1 <= 1e-3; the 10M-triangle mesh allows the grazing-ray residue of
+its degenerate pole triangles, 99.95 % hits and 99.5 % pixels)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import sptr
+import workloads
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _image_close(rgb, orgb, acc, oacc, exact_frac=0.999, rel_l1=1e-3):
+    frac = float((rgb == orgb).all(axis=2).mean())
+    fin, ofin = np.isfinite(acc), np.isfinite(oacc)
+    assert (fin != ofin).sum() <= max(3, 1e-6 * fin.size), "non-finite pixels differ"
+    m = fin & ofin
+    rel = float(np.abs(acc[m] - oacc[m]).sum() / max(1e-12, np.abs(oacc[m]).sum()))
+    assert frac >= exact_frac, f"exact-pixel fraction {frac}"
+    assert rel <= rel_l1, f"relative L1 {rel}"
+    return frac, rel
+
+
+def _camera_rays(cam, W, H, acc=1):
+    d, _ = oracle.primary(cam.as_array(), W, H, acc)
+    rays = np.zeros((W * H, 8), np.float32)
+    rays[:, 0:3] = np.broadcast_to(cam.as_array()[:3], d.shape).reshape(-1, 3)
+    rays[:, 3:6] = d.reshape(-1, 3)
+    rays[:, 7] = np.inf
+    return rays
+
+
+def _random_rays(n, seed, lo, hi):
+    g = np.random.default_rng(seed)
+    d = g.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = g.uniform(lo, hi, size=(n, 3))
+    rays[:, 3:6] = d
+    rays[:, 7] = np.inf
+    return rays
+
+
+def _flat_dict(flat):
+    return {k: getattr(flat, k) for k in ("positions", "indices", "tri_geom_first", "spheres", "geom_material")}
+
+
+# --------------------------------------------------------------------------------------------- C3
+def test_c3_chair_hdr_vs_oracle(renderer):
+    wl = workloads.WORKLOADS["c3"]
+    import tempfile
+
+    faces = workloads.hdr_env_faces()  # synthetic sky -> .hdr -> product reader -> product cube faces
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "sky.hdr")
+        workloads.write_hdr(p, workloads.synthetic_sky_equirect())
+        e = sptr.load_hdr(p)
+    assert np.array_equal(oracle.equirect_to_faces(e, 512), faces)  # the oracle's own equirect mapping agrees
+    flat = sptr.setup_default(renderer, wl.scene, wl.p0, wl.p1, env_faces=faces)
+    assert len(flat.indices) == 6116 and list(flat.geom_material) == [7]  # one chair mesh, Wood
+    P = oracle.Prepared(_flat_dict(flat), bvh=True)
+    # first hits: camera rays and random rays from around the chair
+    cam = sptr.camera_lookat(aspect=1.0)
+    lo, hi = flat.positions.min(0), flat.positions.max(0)
+    rays = np.concatenate([_camera_rays(cam, 160, 160), _random_rays(60000, 3, lo - 0.3, hi + 0.3)])
+    g, pr, t, ng = renderer.intersect(rays)
+    og, opr, ot, ong = P.intersect(rays)
+    same = (g == og) & (pr == opr)
+    assert same.mean() >= 0.9999, same.mean()
+    h = same & (og != 0xFFFFFFFF)
+    assert h.sum() > 3000
+    assert np.array_equal(t[h].view(np.uint32), ot[h].view(np.uint32))
+    # the C3 render path (HDR cubemap miss shading, Wood material, one sun) at 128x72 x 4 spp
+    W, H, S = 128, 72, 4
+    cam = sptr.camera_lookat(aspect=W / H)
+    st = renderer.render(cam, W, H, spp=S)
+    rgb, acc = renderer.read_rgb8(), renderer.read_accum()
+    oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
+                                frames=S, env_faces=faces, threads=THREADS)
+    _image_close(rgb, orgb, acc, oacc)
+    assert st.samples == ocnt["samples"] == W * H * S
+    assert abs(int(st.rays_closest) - ocnt["rays_closest"]) <= 1e-3 * ocnt["rays_closest"]
+    renderer.set_environment(None)
+
+
+# --------------------------------------------------------------------------------------------- C4
+@pytest.fixture(scope="module")
+def c4_frame(renderer):
+    W, H, S = 3840, 2160, 2
+    sptr.setup_default(renderer, "default")
+    cam = sptr.camera_lookat(aspect=W / H)
+    st = renderer.render(cam, W, H, spp=S)
+    return cam, st, renderer.read_rgb8().copy(), renderer.read_accum().copy()
+
+
+def test_c4_4k_vs_oracle(renderer, c4_frame):
+    cam, st, rgb, acc = c4_frame
+    P = oracle.Prepared(oracle.builtin_scene("default"), bvh=True)
+    oacc, orgb, ocnt = P.render(cam.as_array(), 3840, 2160, oracle.preset_materials(False), oracle.default_lights(),
+                                frames=2, threads=THREADS)
+    _image_close(rgb, orgb, acc, oacc)
+    assert st.samples == ocnt["samples"] == 3840 * 2160 * 2
+    assert abs(int(st.rays_closest) - ocnt["rays_closest"]) <= 1e-4 * ocnt["rays_closest"]
+
+
+def test_c4_4k_pixel_indexing(renderer, c4_frame):
+    """Raygen at 4K: directions and RNG states of every pixel bit-exact (pixel_seed = y*W + x spans
+    8.3M values; the camera's (x + jx) / W divisions at W = 3840)."""
+    cam, _, _, _ = c4_frame
+    d, r = renderer.primary_rays(cam, 3840, 2160, 1024)
+    od, orr = oracle.primary(cam.as_array(), 3840, 2160, 1024)
+    assert np.array_equal(r, orr)
+    assert np.array_equal(d.view(np.uint32), od.view(np.uint32))
+
+
+def test_c4_8way_shard_union(renderer, c4_frame):
+    """The C4 multi-GPU schedule at full size: 8 interleaved tile shards, each rank's resolved tiles
+    packed as the all-gather sends them, unpacked on rank 0 == the one-GPU frame, byte for byte."""
+    cam, st0, rgb0, _ = c4_frame
+    G, W, H = 8, 3840, 2160
+    tpr = sptr.tiles_per_rank(W, H, G)
+    gathered = np.zeros(G * tpr * 1024, np.uint32)
+    samples = rays = 0
+    for r in range(G):
+        s = renderer.render(cam, W, H, spp=2, shard_rank=r, shard_count=G)
+        samples += s.samples
+        rays += s.rays_closest + s.rays_shadow
+        gathered[r * tpr * 1024:(r + 1) * tpr * 1024] = sptr.pack_tiles(renderer.read_rgb8(), G, r)
+    assert samples == W * H * 2
+    assert rays == st0.rays_closest + st0.rays_shadow
+    assert np.array_equal(sptr.unpack_tiles(gathered, G, W, H), rgb0)
+
+
+# --------------------------------------------------------------------------------------------- C5
+@pytest.fixture(scope="module")
+def c5_scene(renderer):
+    wl = workloads.WORKLOADS["c5"]
+    flat = sptr.setup_default(renderer, wl.scene, wl.p0, wl.p1)
+    P = oracle.Prepared(oracle.builtin_scene("sphere_mesh", wl.p0, wl.p1), bvh=True)
+    return flat, P
+
+
+def test_c5_deep_bvh_first_hits(renderer, c5_scene):
+    flat, P = c5_scene
+    lay, info = renderer.scene_layout(), renderer.scene_info()
+    assert lay["num_tris"] == 10_000_000 and info["prims"] == 10_000_000 + 8
+    assert lay["bvh_width"] == 4 and lay["lds_bytes"] == 0  # BVH4 from HBM
+    assert info["depth"] >= 40  # the deep-BVH stress this config exists for
+    assert 3 * ((info["depth"] - 1) // 2 + 1) <= 96  # within the BVH4 stack bound (sptr_internal.h kStack)
+    cam = sptr.camera_lookat(aspect=16 / 9)
+    rays = np.concatenate([_camera_rays(cam, 384, 216), _random_rays(120000, 9, (-1.5, 0.2, 0.5), (1.5, 3.0, 3.5))])
+    g, pr, t, ng = renderer.intersect(rays)
+    og, opr, ot, ong = P.intersect(rays)
+    same = (g == og) & (pr == opr)
+    assert same.mean() >= 0.9995, same.mean()
+    h = same & (og != 0xFFFFFFFF)
+    assert h.sum() > 30000
+    assert (t[h].view(np.uint32) == ot[h].view(np.uint32)).mean() >= 0.9999
+    # any-hit shadow queries through the same deep tree
+    sh = rays[::4].copy()
+    sh[:, 6] = 1e-4
+    assert (renderer.occluded(sh) == P.occluded(sh)).mean() >= 0.9995
+
+
+def test_c5_render_vs_oracle(renderer, c5_scene):
+    flat, P = c5_scene
+    W, H, S = 128, 72, 2
+    cam = sptr.camera_lookat(aspect=W / H)
+    st = renderer.render(cam, W, H, spp=S)
+    rgb, acc = renderer.read_rgb8(), renderer.read_accum()
+    oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
+                                frames=S, threads=THREADS)
+    _image_close(rgb, orgb, acc, oacc, exact_frac=0.995, rel_l1=5e-3)
+    assert st.samples == W * H * S

@@ -2,6 +2,9 @@
 # Timing experiments on one GPU (images of the ablated runs are wrong): SPTR_ABLATE bits of the
 # bounce-0 trace (see k_trace), leaf size / BVH width, and emulated multi-GPU shards.
 set -euo pipefail
+# the SPTR_ABLATE / SPTR_MAX_BLOCKS_PER_CU knobs exist only in experiment builds:
+#   tools/build_variants.sh "knobs:-DSPTR_EXPERIMENT_KNOBS"   (on the CPU, before the GPU call)
+export SPTR_LIB=${SPTR_LIB:-$GRAFT_REPO_ROOT/variants/knobs/libsptr_hip.so}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 o=gpurun_out/${1:-exp}
 mkdir -p $o

@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT"
 tag=$1; shift
 out=gpurun_out/$tag
 mkdir -p "$out"
-tests=0; sq=0
+tests=0; sq=0; benchflags=${BENCHFLAGS:-}
 while [ $# -gt 0 ] && [ "${1#--}" != "$1" ]; do
   case $1 in --tests) tests=1 ;; --sq) sq=1 ;; esac
   shift
@@ -22,18 +22,18 @@ if [ $tests = 1 ]; then
 fi
 for wl in "$@"; do
   echo "[$(date +%T)] bench $wl"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
+  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
   tail -1 "$out/bench_$wl.json"
   echo "[$(date +%T)] bench $wl --stage-timing"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 --stage-timing --no-cpu-baseline \
+  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 --stage-timing --no-cpu-baseline --no-interactive \
     > "$out/bench_${wl}_stages.json" 2> "$out/bench_${wl}_stages.err"
   echo "[$(date +%T)] rocprof kernel trace + stats $wl"
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_$wl" -o run -- \
-    python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline > "$out/stats_$wl.log" 2>&1
+    python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive > "$out/stats_$wl.log" 2>&1
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "[$(date +%T)] pmc $c $wl"
     timeout -s KILL 300 rocprofv3 --pmc "$c" --output-format csv -d "$out/pmc_${c}_$wl" -o run -- \
-      python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline > "$out/pmc_${c}_$wl.log" 2>&1
+      python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_${c}_$wl.log" 2>&1
   done
   python3 tools/prof_summary.py "$out/stats_$wl" "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" > "$out/summary_$wl.txt"
   python3 tools/prof_summary.py "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" --emit "$out/pmc_${wl}_trace.json" \
@@ -42,8 +42,9 @@ for wl in "$@"; do
     echo "[$(date +%T)] pmc SQ $wl"
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
       SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d "$out/pmc_SQ_$wl" -o run -- \
-      python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline > "$out/pmc_SQ_$wl.log" 2>&1
+      python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_SQ_$wl.log" 2>&1
     python3 tools/prof_summary.py "$out/pmc_SQ_$wl" > "$out/sq_$wl.txt"
+    python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_trace.json" --kernel k_trace --workload "$wl" > /dev/null
   fi
 done
 echo "[$(date +%T)] done"

@@ -1,6 +1,9 @@
 #!/usr/bin/env bash
 # Sweep resident blocks per CU (SPTR_MAX_BLOCKS_PER_CU) for the given workloads.
 set -euo pipefail
+# the SPTR_ABLATE / SPTR_MAX_BLOCKS_PER_CU knobs exist only in experiment builds:
+#   tools/build_variants.sh "knobs:-DSPTR_EXPERIMENT_KNOBS"   (on the CPU, before the GPU call)
+export SPTR_LIB=${SPTR_LIB:-$GRAFT_REPO_ROOT/variants/knobs/libsptr_hip.so}
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/occ
 for wl in "$@"; do

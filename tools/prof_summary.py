@@ -21,25 +21,51 @@ def short(n):
     return n.split("(")[0][:48]
 
 
+def _is_count_variant(name):
+    """k_trace<L, C, P, W> / k_shadow<L, C, W>: the instrumented (C = true) visit-count instantiation
+    runs only in bench.py's untimed counting pass and is left out of the per-launch means."""
+    if "<" not in name:
+        return False
+    args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
+    return len(args) >= 3 and args[1] == "true"
+
+
 def emit(dirs, kernel, out_path, workload):
     per = collections.defaultdict(list)  # counter -> per-dispatch values for matching kernels
+    dur = []
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             vals = collections.defaultdict(float)
             for r in csv.DictReader(open(f)):
-                if kernel in r["Kernel_Name"]:
+                if kernel in r["Kernel_Name"] and not _is_count_variant(r["Kernel_Name"]):
                     vals[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+                    if r["Counter_Name"] == "SQ_INSTS_VALU":
+                        dur.append((r["Dispatch_Id"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
             for (_, c), v in vals.items():
                 per[c].append(v)
     mean = {c: sum(v) / len(v) for c, v in per.items() if v}
+    if "SQ_INSTS_VALU" in mean:  # SQ pass: VALU wave-instructions per launch (bench.py valu_issue_frac)
+        d = dict(dur)
+        t = sum(d.values()) / max(1, len(d))
+        res = {"workload": workload, "kernel": kernel, "dispatches": len(per["SQ_INSTS_VALU"]),
+               "valu_per_launch": mean["SQ_INSTS_VALU"], "counters_per_launch": mean,
+               "profiled_launch_us": t * 1e6,
+               "valu_issue_frac_profiled": mean["SQ_INSTS_VALU"] / t / (256 * 4 * 0.5 * 2.4e9) if t else None,
+               "note": "SQ_INSTS_VALU counts wave-instructions; peak issue 256 CU x 4 SIMD x 0.5/cycle x 2.4 GHz "
+                       "(MI355X_MICROARCH.md: a wave issues a VALU instruction over 2 cycles); the visit-count "
+                       "instantiation of the untimed pass is excluded"}
+        with open(out_path, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+        return
     fetch = 2.0 * mean.get("FETCH_SIZE", 0.0) * 1024.0
     write = mean.get("WRITE_SIZE", 0.0) * 1024.0
     res = {"workload": workload, "kernel": kernel, "dispatches": {c: len(v) for c, v in per.items()},
            "fetch_bytes_per_launch_x2": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (calibrated for 16-B/lane streams only); "
-                   "Infinity-Cache hits are counted by these memory-side counters; mean over all dispatches of "
-                   "every instantiation of the kernel"}
+                   "Infinity-Cache hits are counted by these memory-side counters; mean over the dispatches of "
+                   "every instantiation of the kernel except the visit-count one of the untimed pass"}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
