@@ -459,11 +459,13 @@ static inline bool sphere_occludes(const float* s, V3 O, V3 D, float tnear, floa
   return (t1 > tnear && t1 < tfar) || (t2 > tnear && t2 < tfar);
 }
 
-// Prepared scene: flattened arrays + a simple CPU BVH (median split).  The BVH only prunes work:
-// the closest hit equals the brute-force result (exact ties excepted), which tests check.
+// Prepared scene: flattened arrays + a CPU BVH (binned SAH, as Embree's builders are SAH-based).
+// The BVH only prunes work: the closest hit equals the brute-force result (exact ties excepted),
+// which tests check.  Children of an internal node are adjacent (left, left + 1).
 struct Node {
   float lo[3], hi[3];
   uint32_t left, count;  // count>0: leaf over refs[left .. left+count)
+  uint32_t axis, pad;    // split axis of an internal node (front-to-back order)
 };
 struct Prepared {
   std::vector<float> pos;
@@ -488,6 +490,13 @@ static void ref_bounds(const Prepared& P, uint32_t r, float lo[3], float hi[3]) 
   }
 }
 
+static inline float half_area(const float lo[3], const float hi[3]) {
+  const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+// Binned SAH (16 bins per axis over the centroid bounds; leaf when splitting does not pay or at
+// <= 2 primitives; traversal cost 1, intersection cost 1).
 static void build_bvh(Prepared& P) {
   const uint32_t n = P.ntri + P.nsph;
   P.refs.resize(n);
@@ -498,18 +507,19 @@ static void build_bvh(Prepared& P) {
     ref_bounds(P, P.refs[i], &blo[size_t(i) * 3], &bhi[size_t(i) * 3]);
     for (int k = 0; k < 3; ++k) cen[size_t(i) * 3 + k] = 0.5f * (blo[size_t(i) * 3 + k] + bhi[size_t(i) * 3 + k]);
   }
-  // refs are permuted; keep a parallel "slot -> original i" index to find bounds/centroids
-  std::vector<uint32_t> ord(n);
+  std::vector<uint32_t> ord(n);  // slot -> original primitive i
   for (uint32_t i = 0; i < n; ++i) ord[i] = i;
   P.nodes.clear();
   if (n == 0) return;
   P.nodes.reserve(2 * size_t(n));
+  constexpr int kBins = 16;
+  constexpr uint32_t kMaxLeaf = 4;
   struct Task { uint32_t node, begin, end; };
   std::vector<Task> st;
   P.nodes.push_back(Node{});
   st.push_back({0, 0, n});
   while (!st.empty()) {
-    Task t = st.back();
+    const Task t = st.back();
     st.pop_back();
     Node nd{};
     for (int k = 0; k < 3; ++k) { nd.lo[k] = INFINITY; nd.hi[k] = -INFINITY; }
@@ -524,22 +534,79 @@ static void build_bvh(Prepared& P) {
       }
     }
     const uint32_t cnt = t.end - t.begin;
-    int ax = 0;
-    for (int k = 1; k < 3; ++k) if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
-    if (cnt <= 4 || !(chi[ax] > clo[ax])) {
+    int best_ax = -1, best_bin = 0;
+    float best_cost = INFINITY;
+    if (cnt > 2) {
+      for (int ax = 0; ax < 3; ++ax) {
+        const float ext = chi[ax] - clo[ax];
+        if (!(ext > 0.0f)) continue;
+        float bl[kBins][3], bh[kBins][3];
+        uint32_t bc[kBins] = {};
+        for (int b = 0; b < kBins; ++b)
+          for (int k = 0; k < 3; ++k) { bl[b][k] = INFINITY; bh[b][k] = -INFINITY; }
+        const float scale = float(kBins) / ext;
+        for (uint32_t i = t.begin; i < t.end; ++i) {
+          const uint32_t o = ord[i];
+          const int b = std::min(kBins - 1, int((cen[size_t(o) * 3 + ax] - clo[ax]) * scale));
+          ++bc[b];
+          for (int k = 0; k < 3; ++k) {
+            bl[b][k] = std::min(bl[b][k], blo[size_t(o) * 3 + k]);
+            bh[b][k] = std::max(bh[b][k], bhi[size_t(o) * 3 + k]);
+          }
+        }
+        float ra[kBins];
+        uint32_t rc[kBins];
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t c = 0;
+        for (int b = kBins - 1; b > 0; --b) {
+          c += bc[b];
+          for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], bl[b][k]); hi[k] = std::max(hi[k], bh[b][k]); }
+          ra[b] = c ? half_area(lo, hi) : 0.0f;
+          rc[b] = c;
+        }
+        for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+        c = 0;
+        for (int b = 0; b < kBins - 1; ++b) {
+          c += bc[b];
+          for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], bl[b][k]); hi[k] = std::max(hi[k], bh[b][k]); }
+          if (c == 0 || rc[b + 1] == 0) continue;
+          const float cost = half_area(lo, hi) * float(c) + ra[b + 1] * float(rc[b + 1]);
+          if (cost < best_cost) { best_cost = cost; best_ax = ax; best_bin = b; }
+        }
+      }
+    }
+    const float leaf_cost = half_area(nd.lo, nd.hi) * float(cnt);
+    const float split_cost = half_area(nd.lo, nd.hi) + best_cost;  // traversal + both children
+    if (cnt <= 2 || best_ax < 0 || (cnt <= kMaxLeaf && split_cost >= leaf_cost)) {
+      if (cnt > kMaxLeaf && best_ax < 0) {  // coincident centroids: split the range in half
+        const uint32_t mid = t.begin + cnt / 2;
+        const uint32_t l = uint32_t(P.nodes.size());
+        P.nodes.push_back(Node{});
+        P.nodes.push_back(Node{});
+        nd.left = l;
+        nd.count = 0;
+        nd.axis = 0;
+        P.nodes[t.node] = nd;
+        st.push_back({l + 1, mid, t.end});
+        st.push_back({l, t.begin, mid});
+        continue;
+      }
       nd.left = t.begin;
       nd.count = cnt;
       P.nodes[t.node] = nd;
       continue;
     }
-    const uint32_t mid = t.begin + cnt / 2;
-    std::nth_element(ord.begin() + t.begin, ord.begin() + mid, ord.begin() + t.end,
-                     [&](uint32_t a, uint32_t b) { return cen[size_t(a) * 3 + ax] < cen[size_t(b) * 3 + ax]; });
+    const float scale = float(kBins) / (chi[best_ax] - clo[best_ax]);
+    const auto it = std::partition(ord.begin() + t.begin, ord.begin() + t.end, [&](uint32_t o) {
+      return std::min(kBins - 1, int((cen[size_t(o) * 3 + best_ax] - clo[best_ax]) * scale)) <= best_bin;
+    });
+    const uint32_t mid = uint32_t(it - ord.begin());
     const uint32_t l = uint32_t(P.nodes.size());
     P.nodes.push_back(Node{});
     P.nodes.push_back(Node{});
     nd.left = l;
     nd.count = 0;
+    nd.axis = uint32_t(best_ax);
     P.nodes[t.node] = nd;
     st.push_back({l + 1, mid, t.end});
     st.push_back({l, t.begin, mid});
@@ -549,17 +616,32 @@ static void build_bvh(Prepared& P) {
   P.refs.swap(r2);
 }
 
-// conservative slab test (per-axis branches; padded exit distance)
-static inline bool box_hit(const Node& nd, V3 O, V3 D, float tnear, float tfar) {
+// Ray with its per-axis reciprocal, computed once per query (the slab test prunes only).
+struct RayInv {
+  float o[3], inv[3];
+  bool zero[3];
+  int neg[3];
+};
+static inline RayInv ray_inv(V3 O, V3 D) {
+  RayInv r;
   const float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
+  for (int k = 0; k < 3; ++k) {
+    r.o[k] = o[k];
+    r.zero[k] = d[k] == 0.0f;
+    r.inv[k] = r.zero[k] ? 0.0f : 1.0f / d[k];
+    r.neg[k] = d[k] < 0.0f;
+  }
+  return r;
+}
+// conservative slab test (padded exit distance); returns the entry distance in *tent
+static inline bool box_hit(const Node& nd, const RayInv& r, float tnear, float tfar, float* tent = nullptr) {
   float t0 = tnear, t1 = tfar;
   for (int k = 0; k < 3; ++k) {
-    if (d[k] == 0.0f) {
-      if (o[k] < nd.lo[k] || o[k] > nd.hi[k]) return false;
+    if (r.zero[k]) {
+      if (r.o[k] < nd.lo[k] || r.o[k] > nd.hi[k]) return false;
       continue;
     }
-    const float inv = 1.0f / d[k];
-    float a = (nd.lo[k] - o[k]) * inv, b = (nd.hi[k] - o[k]) * inv;
+    float a = (nd.lo[k] - r.o[k]) * r.inv[k], b = (nd.hi[k] - r.o[k]) * r.inv[k];
     if (a > b) std::swap(a, b);
     b *= 1.0f + 8.0f * std::numeric_limits<float>::epsilon();
     a *= 1.0f - 8.0f * std::numeric_limits<float>::epsilon();
@@ -567,6 +649,7 @@ static inline bool box_hit(const Node& nd, V3 O, V3 D, float tnear, float tfar) 
     if (b < t1) t1 = b;
     if (t0 > t1) return false;
   }
+  if (tent) *tent = t0;
   return true;
 }
 
@@ -607,17 +690,21 @@ static bool closest_hit(const Prepared& P, V3 O, V3 D, float tnear, float tfar, 
     for (uint32_t i = 0; i < P.nsph; ++i) test_ref(P, 0x80000000u | i, O, D, tnear, tfar, h, any);
     return any;
   }
-  uint32_t stack[128];
+  // front-to-back: the child on the ray's near side of the split axis first; a popped node is
+  // re-tested against the shrunk tfar
+  const RayInv ri = ray_inv(O, D);
+  uint32_t stack[256];
   int sp = 0;
   stack[sp++] = 0;
   while (sp) {
     const Node& nd = P.nodes[stack[--sp]];
-    if (!box_hit(nd, O, D, tnear, tfar)) continue;
+    if (!box_hit(nd, ri, tnear, tfar)) continue;
     if (nd.count) {
       for (uint32_t i = 0; i < nd.count; ++i) test_ref(P, P.refs[nd.left + i], O, D, tnear, tfar, h, any);
     } else {
-      stack[sp++] = nd.left + 1;
-      stack[sp++] = nd.left;
+      const uint32_t near = nd.left + uint32_t(ri.neg[nd.axis]), far = nd.left + 1u - uint32_t(ri.neg[nd.axis]);
+      stack[sp++] = far;
+      stack[sp++] = near;
     }
   }
   return any;
@@ -640,12 +727,13 @@ static bool occluded(const Prepared& P, V3 O, V3 D, float tnear, float tfar, boo
     for (uint32_t i = 0; i < P.nsph; ++i) if (ref_occludes(P, 0x80000000u | i, O, D, tnear, tfar)) return true;
     return false;
   }
-  uint32_t stack[128];
+  const RayInv ri = ray_inv(O, D);
+  uint32_t stack[256];
   int sp = 0;
   stack[sp++] = 0;
   while (sp) {
     const Node& nd = P.nodes[stack[--sp]];
-    if (!box_hit(nd, O, D, tnear, tfar)) continue;
+    if (!box_hit(nd, ri, tnear, tfar)) continue;
     if (nd.count) {
       for (uint32_t i = 0; i < nd.count; ++i) if (ref_occludes(P, P.refs[nd.left + i], O, D, tnear, tfar)) return true;
     } else {
