@@ -558,7 +558,7 @@ __device__ __forceinline__ vec3 sky_color(vec3 d) {
     t = u * u * (3.0f - 2.0f * u);
   }
   vec3 c = mix(v3(0.7f, 0.8f, 0.9f), v3(0.2f, 0.4f, 0.8f), t);
-  const vec3 sd = normalize(v3(0.3f, 0.6f, -0.8f));
+  const vec3 sd = v3(kSunDirX, kSunDirY, kSunDirZ);  // normalize(vec3(0.3, 0.6, -0.8)), precomputed
   const float sdot = fmax_g(dot(d, sd), 0.0f);
   float p8, p64;
   pow8_64(sdot, p8, p64);
@@ -573,8 +573,11 @@ __device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, i
   const float4 t = env[((size_t)face * S + y) * S + x];
   return v3(t.x, t.y, t.z);
 }
-__device__ vec3 env_color(const EnvView& sh, vec3 dir) {
-  if (!sh.env) return sky_color(dir);
+// kCube: the environment is a cubemap (sh.env != null), else the procedural sky; a template
+// parameter so that the kernels of the common sky case carry no cubemap code or registers
+template <bool kCube>
+__device__ __forceinline__ vec3 env_color(const EnvView& sh, vec3 dir) {
+  if (!kCube) return sky_color(dir);
   const vec3 d = normalize(dir);
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
   float ma, uc, vc;
@@ -642,12 +645,170 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 }
 
 // --------------------------------------------------------------------------------- k_trace
+template <bool kLds, bool kCount, bool kPrimary, bool kW4>
+__global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
+    k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_cnt;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
+  if (threadIdx.x == 0) s_cn// Bounce 0, pixel-major (f.pixel_major == kFoldThread: LDS-staged scenes, where every primary ray
+// costs about the same, in batches with >= kPixelMajorItems pixels per resident thread): thread <-
+// local pixel l, looping over the batch's k sample slots in sample order (path p = s*P + l, as
+// everywhere else).  Misses before the pixel's first hit are summed straight into the accumulator
+// — the same adds, in the same order, that k_accum would do — so an all-sky pixel writes no
+// radiance at all and k_accum skips it; from the first hit on, misses go to rad[p] and k_accum
+// resumes there (accum.w = resume slot).  A kernel of its own (not a branch of k_trace), so that
+// its registers are allocated for this loop alone.
+template <bool kCount, bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
+    k_trace_pm(SceneView sv, EnvView sh, FrameView f, WaveView w) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0u;
+  const Staged sc = stage_scene<true>(sv, lds);
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+  const ImageDiv idiv = image_div(f);
+  Visits vc;
+  const Sched sd = block_sched(f.P);
+  const uint32_t per = sd.per * f.k;  // hit-record segment stride: all samples of the block's pixels
+  const uint32_t seg0 = sd.seg0 * f.k;
+  for (uint32_t base = sd.first; base < f.P; base += sd.step) {
+    const uint32_t l = base + threadIdx.x;
+    int x = 0, y = 0;
+    const bool valid = l < f.P && local_pixel(f, l, x, y);
+    const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
+    vec3 a = v3(0.0f, 0.0f, 0.0f);
+    if (valid && !f.reset) a = xyz(f.accum[l]);
+    bool fold = true;
+    uint32_t resume = f.k;
+    for (uint32_t smp = 0; smp < f.k; ++smp) {
+      bool hit = false;
+      uint32_t ref = kNoHit;
+      float tfar = __builtin_huge_valf();
+      const uint32_t p = smp * f.P + l;
+      if (valid) {
+        Primary pr;
+        primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
+        const Ray r = make_ray(f.cam_pos, pr.d);
+        // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
+        // 1 = constant environment, 4 = primary misses add no radiance
+        if (!(f.ablate & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!hit) {
+          vec3 rv = v3(0.0f, 0.0f, 0.0f);
+          if (sh.debug_mode != 1) {
+            const vec3 e = (f.ablate & 1u) ? pr.d : env_color<kCube>(sh, safe_normalize(pr.d));
+            rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+          }
+          if (!fold) w.rad[p] = f4(rv, 0.0f);
+          else if (!(f.ablate & 4u)) a = a + rv;
+        } else if (fold) {
+          fold = false;
+          resume = smp;
+        }
+      }
+      const uint32_t j = block_append(&s_cnt, hit);
+      if (hit) {
+        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
+        else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
+      }
+    }
+    if (l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
+  }
+  seg_publish(w.segH, &s_cnt, per);
+  report_stack(vc, w.tot);
+  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+}
+
+// Bounce 0, lane groups per pixel (f.pixel_major == kFoldWave: batches of >= kWaveFoldMinK samples
+// where the thread-per-pixel loop above would leave resident threads idle (sharded frames) or be
+// unbalanced (scenes traversed from L2/HBM, where per-pixel cost varies by orders of magnitude)).
+// A wave owns 8 local pixels; the 8 lanes of pixel g trace its samples 8 at a time (lane q takes
+// sample r*8 + q of round r), so a wave's rays come from 8 neighbouring pixels.  A pixel's leading
+// misses (the samples before its first hit) are summed into the accumulator in sample order — an
+// 8-step shuffle loop per round, the same adds in the same order as k_accum; later misses go to
+// rad[p] and accum.w records where k_accum resumes.  Blocks take 32-pixel chunks round-robin.
+// (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts 289 us, 8 lanes
+// 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
+constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
+template <bool kLds, bool kCount, bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
+    k_trace_wp(SceneView sv, EnvView sh, FrameView f, WaveView w) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0u;
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+  const ImageDiv idiv = image_div(f);
+  Visits vc;
+  constexpr uint32_t kPix = kBlock / kFoldLanes;  // pixels per block chunk
+  const uint32_t lane = lane_id(), q = lane & (kFoldLanes - 1u), g0 = lane & ~(kFoldLanes - 1u);
+  const uint32_t lb = logical_block();
+  const uint32_t first = lb * kPix, step = gridDim.x * kPix;
+  const uint32_t per_pix = (f.P + step - 1u) / step * kPix;  // pixels per block at most
+  const uint32_t per = per_pix * f.k;                         // hit-record segment stride
+  const uint32_t seg0 = lb * per;
+  const uint32_t rounds = (f.k + kFoldLanes - 1u) / kFoldLanes;
+  for (uint32_t base = first; base < f.P; base += step) {
+    const uint32_t l = base + threadIdx.x / kFoldLanes;
+    int x = 0, y = 0;
+    const bool valid = l < f.P && local_pixel(f, l, x, y);
+    const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
+    vec3 a = v3(0.0f, 0.0f, 0.0f);
+    if (valid && !f.reset) a = xyz(f.accum[l]);
+    bool fold = true;
+    uint32_t resume = f.k;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      const uint32_t smp = r * kFoldLanes + q;
+      const bool act = valid && smp < f.k;
+      bool hit = false;
+      uint32_t ref = kNoHit;
+      float tfar = __builtin_huge_valf();
+      const uint32_t p = smp * f.P + l;
+      vec3 rv = v3(0.0f, 0.0f, 0.0f);
+      if (act) {
+        Primary pr;
+        primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
+        const Ray r = make_ray(f.cam_pos, pr.d);
+        hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_normalize(pr.d));
+      }
+      // this pixel group's hits of the round -> number of leading misses still to fold
+      const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
+      const uint32_t nact = f.k - r * kFoldLanes < kFoldLanes ? f.k - r * kFoldLanes : kFoldLanes;
+      const uint32_t nfold = fold ? (hm ? (uint32_t)__builtin_ctz(hm) : nact) : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < kFoldLanes; ++j) {
+        const float vx = __shfl(rv.x, (int)(g0 + j)), vy = __shfl(rv.y, (int)(g0 + j)), vz = __shfl(rv.z, (int)(g0 + j));
+        if (j < nfold) a = v3(a.x + vx, a.y + vy, a.z + vz);
+      }
+      if (fold && hm) {
+        fold = false;
+        resume = r * kFoldLanes + nfold;
+      }
+      if (act && !hit && q >= nfold) w.rad[p] = f4(rv, 0.0f);
+      const uint32_t j = block_append(&s_cnt, hit);
+      if (hit) {
+        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
+        else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
+      }
+    }
+    if (q == 0u && l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(valid ? resume : f.k));
+  }
+  seg_publish(w.segH, &s_cnt, per);
+  report_stack(vc, w.tot);
+  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+}
 // Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
 // (wf_pt_cpu.cpp:98-103) is added to rad[p] in place, so only hits go on to k_shade, as dense hit
 // records in this block's segment.  kPrimary: bounce 0, one thread per path slot, camera ray
 // computed in place (no input stream at all).  Input of later bounces: the dense ray stream
 // rs[depth&1] written by the previous k_shade, addressed through its segment table.
-template <bool kLds, bool kCount, bool kPrimary, bool kW4>
+template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
@@ -656,76 +817,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
-  if (kPrimary && kLds && f.pixel_major) {
-    // Bounce 0, pixel-major (f.pixel_major: LDS-staged scenes, where every primary ray costs
-    // about the same, in batches with >= kPixelMajorItems pixels per resident thread): thread <-
-    // local pixel l, looping over the batch's k sample slots in sample order (path p = s*P + l,
-    // as everywhere else).  Misses before the pixel's first hit are summed straight into the
-    // accumulator — the same adds, in the same order, that k_accum would do — so an all-sky pixel
-    // writes no radiance at all and k_accum skips it; from the first hit on, misses go to rad[p]
-    // and k_accum resumes there (accum.w = resume slot).
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
-    const ImageDiv idiv = image_div(f);
-    Visits vc;
-    const Sched sd = block_sched(f.P);
-    const uint32_t per = sd.per * f.k;  // hit-record segment stride: all samples of the block's pixels
-    const uint32_t seg0 = sd.seg0 * f.k;
-    for (uint32_t base = sd.first; base < f.P; base += sd.step) {
-      const uint32_t l = base + threadIdx.x;
-      int x = 0, y = 0;
-      const bool valid = l < f.P && local_pixel(f, l, x, y);
-      const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
-      vec3 a = v3(0.0f, 0.0f, 0.0f);
-      if (valid && !f.reset) a = xyz(f.accum[l]);
-      bool fold = true;
-      uint32_t resume = f.k;
-      for (uint32_t smp = 0; smp < f.k; ++smp) {
-        bool hit = false;
-        uint32_t ref = kNoHit;
-        float tfar = __builtin_huge_valf();
-        const uint32_t p = smp * f.P + l;
-        if (valid) {
-          Primary pr;
-          primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
-          const Ray r = make_ray(f.cam_pos, pr.d);
-          // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
-          // 1 = constant environment, 4 = primary misses add no radiance
-          if (!(f.ablate & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-          if (!hit) {
-            vec3 rv = v3(0.0f, 0.0f, 0.0f);
-            if (sh.debug_mode != 1) {
-              const vec3 e = (f.ablate & 1u) ? pr.d : env_color(sh, safe_normalize(pr.d));
-              rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
-            }
-            if (!fold) w.rad[p] = f4(rv, 0.0f);
-            else if (!(f.ablate & 4u)) a = a + rv;
-          } else if (fold) {
-            fold = false;
-            resume = smp;
-          }
-        }
-        const uint32_t j = block_append(&s_cnt, hit);
-        if (hit) {
-          if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
-          else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
-        }
-      }
-      if (l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
-    }
-    seg_publish(w.segH, &s_cnt, per);
-    report_stack(vc, w.tot);
-    if (kCount) flush_visits(vc, w.tot, kTotNodes);
-    return;
-  }
-  // Bounce 0 path-major (thread <- path slot).  Scenes traversed from L2/HBM always: per-pixel
-  // cost varies by orders of magnitude there (sky vs a 10M-triangle mesh), and a thread looping
-  // over all k samples of one pixel leaves the launch waiting on the blocks that drew the mesh (C5
-  // measured 22.9 -> 67.9 ms).  LDS scenes when the batch has too few pixels (sharded frames).
-  uint32_t n, per_in = 0u;
-  if (kPrimary) {
-    n = f.P * f.k;
-    __syncthreads();
+reads();
   } else {
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
@@ -765,7 +857,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = (f.ablate & 1u) ? d : env_color(sh, safe_normalize(d));
+          const vec3 e = (f.ablate & 1u) ? d : env_color<kCube>(sh, safe_normalize(d));
           vec3 rv;
           if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -1102,7 +1194,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW_WAVES) k_shadow(SceneView 
 // k_trace + k_shade + k_shadow (wf_pt_cpu.cpp:94-248), so the image does not depend on where the
 // wavefront hands over (test_tail_depth_invariance).  Closest-hit and any-hit queries are tallied
 // per block (bstat_closest / bstat) and folded by k_accum.
-template <bool kLds, bool kW4>
+template <bool kLds, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
                                                  uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
@@ -1143,7 +1235,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
         loaded = true;
       }
       if (!hit) {
-        radv = radv + thr * env_color(sh.env, safe_normalize(rd));
+        radv = radv + thr * env_color<kCube>(sh.env, safe_normalize(rd));
         break;
       }
       const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
@@ -1183,7 +1275,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
 }
 
 // --------------------------------------------------------------------------------- k_accum / resolve
-// Per-pixel sample sums in sample order.  Pixel-major bounce 0 (f.pixel_major) began them:
+// Per-pixel sample sums in sample order.  A folding bounce 0 (f.pixel_major: thread or lane group
+// per pixel) began them:
 // accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
 // batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
 // slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
@@ -1423,12 +1516,31 @@ static unsigned trace_lds(const SceneView& sv, bool lds, bool primary, uint32_t 
 // on C2 (profiles/r01h_pixel_major.txt): 1 GPU, 4.5 pixels/thread: 4.17 -> 3.74 ms; 2-way shard,
 // 2.3: 2.26 -> 2.24-2.28; 4-way, 1.1: 1.20 -> 1.28-1.29; 8-way: 0.72 -> 0.99.
 constexpr uint32_t kPixelMajorItems = 4;
+// Lane-group bounce 0 (k_trace_wp) from this many samples per batch: 8 lanes take 8 samples of one
+// pixel per round, so smaller batches would leave lanes idle.
+constexpr uint32_t kWaveFoldMinK = 16;
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
-  if (sv.lds_bytes == 0) return 0u;
-  const unsigned lb = trace_lds(sv, true, true, 0);
-  const unsigned g = sv.width == 4u ? resident_grid((const void*)&k_trace<true, false, true, true>, lb)
-                                    : resident_grid((const void*)&k_trace<true, false, true, false>, lb);
-  return (uint64_t)f.P >= (uint64_t)g * kBlock * kPixelMajorItems ? 1u : 0u;
+  if (sv.lds_bytes != 0) {
+    const unsigned lb = trace_lds(sv, true, true, 0);
+    const unsigned g = sv.width == 4u ? resident_grid((const void*)&k_trace_pm<false, true, false>, lb)
+                                      : resident_grid((const void*)&k_trace_pm<false, false, false>, lb);
+    if ((uint64_t)f.P >= (uint64_t)g * kBlock * kPixelMajorItems) return kFoldThread;
+  }
+  return f.k >= kWaveFoldMinK ? kFoldWave : kFoldNone;
+}
+
+// Template dispatch over runtime flags: dispatch(fn, Flags<>{}, b0, b1, ...) calls
+// fn(Flags<b0, b1, ...>{}) with the flags as compile-time values (one instantiation per combination).
+template <bool... B>
+struct Flags {};
+
+template <class Fn, bool... B>
+static unsigned dispatch(Fn&& fn, Flags<B...>) {
+  return fn(Flags<B...>{});
+}
+template <class Fn, bool... B, class... Rest>
+static unsigned dispatch(Fn&& fn, Flags<B...>, bool first, Rest... rest) {
+  return first ? dispatch(fn, Flags<B..., true>{}, rest...) : dispatch(fn, Flags<B..., false>{}, rest...);
 }
 
 unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
@@ -1437,28 +1549,40 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   const bool L = sv.lds_bytes != 0;
   const bool P = depth == 0;
   const bool W = sv.width == 4u;
+  const bool cube = sh.env.env != nullptr;
   const unsigned lb = trace_lds(sv, L, P, nseg);
   const EnvView ev = sh.env;
-  unsigned g = 0;
-#define SPTR_TRACE(Lc, C, Pc, Wc)                                                                   \
-  do {                                                                                              \
-    g = resident_grid((const void*)&k_trace<Lc, C, Pc, Wc>, lb);                                    \
-    hipLaunchKernelGGL((k_trace<Lc, C, Pc, Wc>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);     \
-  } while (0)
-#define SPTR_TRACE_W(Lc, C, Pc) \
-  do {                          \
-    if (W) SPTR_TRACE(Lc, C, Pc, true); else SPTR_TRACE(Lc, C, Pc, false); \
-  } while (0)
-  if (P) {
-    if (L) { if (count) SPTR_TRACE_W(true, true, true); else SPTR_TRACE_W(true, false, true); }
-    else   { if (count) SPTR_TRACE_W(false, true, true); else SPTR_TRACE_W(false, false, true); }
-  } else {
-    if (L) { if (count) SPTR_TRACE_W(true, true, false); else SPTR_TRACE_W(true, false, false); }
-    else   { if (count) SPTR_TRACE_W(false, true, false); else SPTR_TRACE_W(false, false, false); }
+  if (P && f.pixel_major == kFoldWave) {
+    return dispatch(
+        [&](auto fl) -> unsigned {
+          return [&]<bool Lc, bool C, bool Wc, bool Cube>(Flags<Lc, C, Wc, Cube>) {
+            const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube>, lb);
+            hipLaunchKernelGGL((k_trace_wp<Lc, C, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w);
+            return g;
+          }(fl);
+        },
+        Flags<>{}, L, count, W, cube);
   }
-#undef SPTR_TRACE_W
-#undef SPTR_TRACE
-  return g;
+  if (P && L && f.pixel_major == kFoldThread) {
+    return dispatch(
+        [&](auto fl) -> unsigned {
+          return [&]<bool C, bool Wc, bool Cube>(Flags<C, Wc, Cube>) {
+            const unsigned g = resident_grid((const void*)&k_trace_pm<C, Wc, Cube>, lb);
+            hipLaunchKernelGGL((k_trace_pm<C, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w);
+            return g;
+          }(fl);
+        },
+        Flags<>{}, count, W, cube);
+  }
+  return dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube>(Flags<Lc, C, Pc, Wc, Cube>) {
+          const unsigned g = resident_grid((const void*)&k_trace<Lc, C, Pc, Wc, Cube>, lb);
+          hipLaunchKernelGGL((k_trace<Lc, C, Pc, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, L, count, P, W, cube);
 }
 
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
@@ -1502,16 +1626,15 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
                      uint32_t nseg, hipStream_t s) {
   const bool L = sv.lds_bytes != 0;
   const unsigned lb = trace_lds(sv, L, false, nseg);
-  unsigned g = 0;
-#define SPTR_TAIL(Lc, Wc)                                                                            \
-  do {                                                                                               \
-    g = resident_grid((const void*)&k_tail<Lc, Wc>, lb);                                             \
-    hipLaunchKernelGGL((k_tail<Lc, Wc>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth0, nseg);  \
-  } while (0)
-  if (L) { if (sv.width == 4u) SPTR_TAIL(true, true); else SPTR_TAIL(true, false); }
-  else   { if (sv.width == 4u) SPTR_TAIL(false, true); else SPTR_TAIL(false, false); }
-#undef SPTR_TAIL
-  return g;
+  return dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
+          const unsigned g = resident_grid((const void*)&k_tail<Lc, Wc, Cube>, lb);
+          hipLaunchKernelGGL((k_tail<Lc, Wc, Cube>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth0, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
 }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s) {

@@ -127,8 +127,13 @@ struct FrameView {
   uint32_t ablate;  // SPTR_ABLATE environment variable: timing experiments only (0 in normal use)
   float4* accum;    // per local pixel: running sample sum (xyz) + resume slot (w bits), see k_accum
   uint32_t reset;   // this batch starts the accumulation (frame_begin == 1, first batch)
-  uint32_t pixel_major;  // bounce 0 runs pixel-major and folds leading misses into accum (bounce0_pixel_major)
+  uint32_t pixel_major;  // kFold*: bounce 0 folds each pixel's leading misses into accum (bounce0_pixel_major)
 };
+
+// Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
+// rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each
+// pixel's leading misses into accum and record the resume slot for k_accum.
+enum : uint32_t { kFoldNone = 0, kFoldThread = 1, kFoldWave = 2 };
 
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 

@@ -66,6 +66,12 @@ SPTR_HD vec3 safe_normalize(vec3 v) {
   return v * inv_length(l2);
 }
 
+// normalize(vec3(0.3, 0.6, -0.8)), the sun direction of EnvironmentManager::getSkyColor
+// (src/EnvironmentManager.cpp:48), evaluated once in glm's order; tests/cpp/test_index_math.cpp checks
+// the literal against normalize() on the host.  (The device's correctly rounded normalize sequence
+// is not constant-folded by the compiler.)
+constexpr float kSunDirX = 0x1.263e86p-2f, kSunDirY = 0x1.263e86p-1f, kSunDirZ = -0x1.88535ep-1f;
+
 SPTR_HD uint32_t wang_hash(uint32_t a) {
   a = (a ^ 61u) ^ (a >> 16u);
   a *= 9u;

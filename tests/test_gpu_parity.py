@@ -362,3 +362,39 @@ def test_pixel_major_bounce0_accumulation(renderer):
         rgb[m] = c_r[m]
     assert np.array_equal(one_acc.view(np.uint32), acc.view(np.uint32))
     assert np.array_equal(one_rgb, rgb)
+
+
+@pytest.mark.parametrize("scene,p0,p1,spp", [("default_emitter", 0, 0, 64), ("sphere_mesh", 60, 120, 40),
+                                             ("default", 0, 0, 100)])
+def test_wave_fold_bounce0_invariance(renderer, scene, p0, p1, spp):
+    """Batches of >= 32 samples on small (or sharded, or L2/HBM-scene) frames run bounce 0 wave per
+    pixel, folding each pixel's leading misses into the accumulator with a lane loop
+    (k_trace_wp).  The sums must be bit-identical to path-major batches (8 samples per batch, every
+    miss through rad[] and k_accum), including a partial last round of lanes (spp 40, 100)."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, scene, p0, p1)
+    st = renderer.render(cam, W, H, spp=spp)
+    assert st.waves == 1
+    acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
+    P = 3 * 2 * 1024  # local pixels: 3 x 2 tiles
+    renderer.set_wave_paths(P * 8)
+    try:
+        st8 = renderer.render(cam, W, H, spp=spp)
+    finally:
+        renderer.set_wave_paths(0)
+    assert st8.waves == (spp + 7) // 8
+    assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
+    assert np.array_equal(rgb, renderer.read_rgb8())
+    assert (st.rays_closest, st.rays_shadow) == (st8.rays_closest, st8.rays_shadow)
+    # progressive continuation from a folded batch
+    renderer.render(cam, W, H, spp=spp, frame_begin=spp + 1)
+    two = renderer.read_accum().copy()
+    renderer.render(cam, W, H, spp=2 * spp)
+    assert np.array_equal(two.view(np.uint32), renderer.read_accum().view(np.uint32))
+
+
+def test_wave_fold_vs_oracle(renderer):
+    st, rgb, acc, orgb, oacc, ocnt = _render_pair(renderer, "default_emitter", 64, 48, 48)
+    _image_close(rgb, orgb, acc, oacc)
+    assert st.samples == ocnt["samples"]
