@@ -645,14 +645,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 }
 
 // --------------------------------------------------------------------------------- k_trace
-template <bool kLds, bool kCount, bool kPrimary, bool kW4>
-__global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
-    k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
-  __shared__ LdsStack s_stack;
-  extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt;
-  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
-  if (threadIdx.x == 0) s_cn// Bounce 0, pixel-major (f.pixel_major == kFoldThread: LDS-staged scenes, where every primary ray
+// Bounce 0, pixel-major (f.pixel_major == kFoldThread: LDS-staged scenes, where every primary ray
 // costs about the same, in batches with >= kPixelMajorItems pixels per resident thread): thread <-
 // local pixel l, looping over the batch's k sample slots in sample order (path p = s*P + l, as
 // everywhere else).  Misses before the pixel's first hit are summed straight into the accumulator
@@ -817,7 +810,12 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
-reads();
+  // Bounce 0 path-major (thread <- path slot): batches of fewer than kWaveFoldMinK samples (e.g.
+  // the interactive 1 spp per call).  Later bounces: thread <- queued ray.
+  uint32_t n, per_in = 0u;
+  if (kPrimary) {
+    n = f.P * f.k;
+    __syncthreads();
   } else {
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
