@@ -50,10 +50,21 @@ __device__ __forceinline__ float div_nrm(float a, const DivBy& d) {
   return __builtin_fmaf(__builtin_fmaf(-d.b, q1, a), d.r, q1);
 }
 
-// 1 / sqrt(l2) as glm's normalize evaluates it (two correctly rounded operations)
+// 1 / sqrt(l2) as glm's normalize evaluates it (two correctly rounded operations), for l2 in
+// [2^-96, 2^100]: the squared length of a direction-like vector (callers: normalize_dir).
+__device__ __forceinline__ float inv_len_nrm(float l2) { return rcp_nrm(sqrt_nrm(l2)); }
+
+// 1 / sqrt(l2) for every float l2 (bit-identical to 1.0f / sqrtf(l2), checked over all 2^32 inputs by
+// tests/hip/crmath_check.hip).  Out-of-domain inputs are scaled by an even power of two, which
+// commutes exactly with the correctly rounded sqrt (the scaled root stays normal), so there is no
+// separate IEEE slow path for the compiler to if-convert into every normalize.
 __device__ __forceinline__ float inv_len(float l2) {
-  if (l2 >= kCrLo && l2 <= kCrHi) return rcp_nrm(sqrt_nrm(l2));
-  return 1.0f / sqrtf(l2);
+  const bool lo = l2 < kCrLo, hi = l2 > kCrHi;
+  const float sc = lo ? 0x1p100f : (hi ? 0x1p-100f : 1.0f);
+  const float un = lo ? 0x1p-50f : (hi ? 0x1p50f : 1.0f);  // 1 / sqrt(sc)
+  const float s = sqrt_nrm(l2 * sc) * un;
+  const float r = rcp_nrm(s);
+  return s == 0.0f ? __builtin_copysignf(__builtin_huge_valf(), s) : (s == __builtin_huge_valf() ? 0.0f : r);
 }
 
 }  // namespace sptr

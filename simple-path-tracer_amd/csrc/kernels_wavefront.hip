@@ -169,7 +169,7 @@ __device__ __forceinline__ vec3 camera_dir(const FrameView& f, float u, float v)
   const float nx = (u - 0.5f) * 2.0f;
   const float ny = -(v - 0.5f) * 2.0f;
   const vec3 d = f.cam_f + nx * f.half_w * f.cam_r + ny * f.half_h * f.cam_u;
-  return normalize(d);
+  return normalize_dir(d);
 }
 
 // --------------------------------------------------------------------------------- intersection
@@ -524,7 +524,7 @@ __device__ __forceinline__ void primary_at(const FrameView& f, const ImageDiv& d
   const float jx = rand01(r);
   const float jy = rand01(r);
   const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, dv.w), div_nrm(float(y) + jy, dv.h));
-  out.d = safe_normalize(dir);
+  out.d = safe_normalize_dir(dir);
   out.rng = wang_hash((ps ^ acc) ^ 1u);
 }
 __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
@@ -578,7 +578,7 @@ __device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, i
 template <bool kCube>
 __device__ __forceinline__ vec3 env_color(const EnvView& sh, vec3 dir) {
   if (!kCube) return sky_color(dir);
-  const vec3 d = normalize(dir);
+  const vec3 d = normalize_dir(dir);
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
   float ma, uc, vc;
   int face;
@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
           if (sh.debug_mode != 1) {
-            const vec3 e = (f.ablate & 1u) ? pr.d : env_color<kCube>(sh, safe_normalize(pr.d));
+            const vec3 e = (f.ablate & 1u) ? pr.d : env_color<kCube>(sh, safe_normalize_dir(pr.d));
             rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           }
           if (!fold) w.rad[p] = f4(rv, 0.0f);
@@ -768,7 +768,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         const Ray r = make_ray(f.cam_pos, pr.d);
         hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_normalize(pr.d));
+        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_normalize_dir(pr.d));
       }
       // this pixel group's hits of the round -> number of leading misses still to fold
       const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
@@ -855,7 +855,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = (f.ablate & 1u) ? d : env_color<kCube>(sh, safe_normalize(d));
+          const vec3 e = (f.ablate & 1u) ? d : env_color<kCube>(sh, safe_normalize_dir(d));
           vec3 rv;
           if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -954,7 +954,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
   if (m.metallic > 0.5f) {
     no = P + nrm * 1e-4f;
-    nd = safe_normalize(reflect(rd, nrm));
+    nd = safe_normalize_dir(reflect(rd, nrm));
     thr = thr * (albedo * m.metallic);
     return true;
   }
@@ -970,7 +970,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
     const float xi = rand01(rng);
     if (xi < F) {
       no = P + nrm * 1e-4f;
-      nd = safe_normalize(reflect(rd, nrm));
+      nd = safe_normalize_dir(reflect(rd, nrm));
       thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
     } else {
       const float ci = -dot(nrm, rd);
@@ -979,11 +979,11 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
       if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
       if (dot(refr, refr) > 0.0f) {
         no = P - nrm * 1e-4f;
-        nd = safe_normalize(refr);
+        nd = safe_normalize_dir(refr);
         thr = thr * v3(tr, tr, tr);
       } else {
         no = P + nrm * 1e-4f;
-        nd = safe_normalize(reflect(rd, nrm));
+        nd = safe_normalize_dir(reflect(rd, nrm));
       }
     }
     return true;
@@ -994,11 +994,11 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   const float rr = sqrtf(r2);
   const float lx = rr * cosf(phi), ly = rr * sinf(phi);
   const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
-  const vec3 nn = safe_normalize(nrm);
-  const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize(cross(nn, v3(0.0f, 0.0f, 1.0f)))
-                                         : normalize(cross(nn, v3(0.0f, 1.0f, 0.0f)));
+  const vec3 nn = safe_normalize_dir(nrm);
+  const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize_dir(cross(nn, v3(0.0f, 0.0f, 1.0f)))
+                                         : normalize_dir(cross(nn, v3(0.0f, 1.0f, 0.0f)));
   const vec3 bt = cross(tg, nn);
-  const vec3 sdir = safe_normalize(tg * lx + bt * ly + nn * lz);
+  const vec3 sdir = safe_normalize_dir(tg * lx + bt * ly + nn * lz);
   no = P + nrm * 1e-4f;
   const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
   const float xi = rand01(rng);
@@ -1009,7 +1009,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   } else {
     thr = thr * albedo;
   }
-  nd = safe_normalize(sdir);
+  nd = safe_normalize_dir(sdir);
   return cont;
 }
 
@@ -1233,7 +1233,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
         loaded = true;
       }
       if (!hit) {
-        radv = radv + thr * env_color<kCube>(sh.env, safe_normalize(rd));
+        radv = radv + thr * env_color<kCube>(sh.env, safe_normalize_dir(rd));
         break;
       }
       const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
@@ -1421,7 +1421,7 @@ __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, ui
     const float jx = rand01(r);
     const float jy = rand01(r);
     const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, idiv.w), div_nrm(float(y) + jy, idiv.h));  // as primary_path
-    const vec3 d = safe_normalize(dir);
+    const vec3 d = safe_normalize_dir(dir);
     dirs[(size_t)i * 3 + 0] = d.x;
     dirs[(size_t)i * 3 + 1] = d.y;
     dirs[(size_t)i * 3 + 2] = d.z;

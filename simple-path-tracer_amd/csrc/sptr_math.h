@@ -56,14 +56,25 @@ inline float sq_root(float x) { return std::sqrt(x); }
 // sequences of cr_math.h (bit-identical in range, verified exhaustively on gfx950).
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ float inv_length(float l2) { return inv_len(l2); }
+__device__ __forceinline__ float inv_length_dir(float l2) { return inv_len_nrm(l2); }
 #else
 SPTR_HD float inv_length(float l2) { return 1.0f / sq_root(l2); }
+SPTR_HD float inv_length_dir(float l2) { return 1.0f / sq_root(l2); }
 #endif
 SPTR_HD vec3 normalize(vec3 v) { return v * inv_length(dot(v, v)); }
 SPTR_HD vec3 safe_normalize(vec3 v) {
   const float l2 = dot(v, v);
   if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
   return v * inv_length(l2);
+}
+// The same operations for direction-like vectors whose squared length is known to lie in
+// [2^-96, 2^100] (camera and ray directions, reflections, refractions, cosine samples, tangents:
+// lengths between ~0.04 and ~2), where the device skips the range handling of inv_len.
+SPTR_HD vec3 normalize_dir(vec3 v) { return v * inv_length_dir(dot(v, v)); }
+SPTR_HD vec3 safe_normalize_dir(vec3 v) {
+  const float l2 = dot(v, v);
+  if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
+  return v * inv_length_dir(l2);
 }
 
 // normalize(vec3(0.3, 0.6, -0.8)), the sun direction of EnvironmentManager::getSkyColor

@@ -3,6 +3,7 @@
 // gfx950 over their stated domains.  Built and run by tests/test_gpu_crmath.py.
 //   sqrt_nrm : every float in [2^-96, 2^100]
 //   rcp_nrm  : every float in [2^-100, 2^100]
+//   inv_len  : every one of the 2^32 float bit patterns (NaN == NaN), against 1.0f / sqrtf(x)
 //   div_nrm  : divisors 1..8192 and the bench/test image sizes, 2^22 dividends each of the form
 //              float(x) + j (x integer pixel coordinate < b, j a 24-bit jitter), plus random floats
 #include <hip/hip_runtime.h>
@@ -15,8 +16,8 @@
 
 using namespace sptr;
 
-__device__ unsigned long long g_bad[3];
-__device__ unsigned int g_first[3];
+__device__ unsigned long long g_bad[4];
+__device__ unsigned int g_first[4];
 
 __global__ void k_sqrt(uint32_t lo, uint32_t hi) {
   for (uint64_t u = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= hi; u += (uint64_t)gridDim.x * blockDim.x) {
@@ -32,9 +33,21 @@ __global__ void k_rcp(uint32_t lo, uint32_t hi) {
   for (uint64_t u = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= hi; u += (uint64_t)gridDim.x * blockDim.x) {
     const float y = __uint_as_float((uint32_t)u);
     const float ref = 1.0f / y;
-    if (__float_as_uint(rcp_nrm(y)) != __float_as_uint(ref) || __float_as_uint(inv_len(y)) != __float_as_uint(1.0f / sqrtf(y))) {
+    if (__float_as_uint(rcp_nrm(y)) != __float_as_uint(ref) || __float_as_uint(inv_len_nrm(y)) != __float_as_uint(1.0f / sqrtf(y))) {
       atomicAdd(&g_bad[1], 1ull);
       atomicMin(&g_first[1], (uint32_t)u);
+    }
+  }
+}
+
+__global__ void k_invlen_all() {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= 0xFFFFFFFFull; u += (uint64_t)gridDim.x * blockDim.x) {
+    const float x = __uint_as_float((uint32_t)u);
+    const float got = inv_len(x), ref = 1.0f / sqrtf(x);
+    const bool same = __float_as_uint(got) == __float_as_uint(ref) || (got != got && ref != ref);
+    if (!same) {
+      atomicAdd(&g_bad[3], 1ull);
+      atomicMin(&g_first[3], (uint32_t)u);
     }
   }
 }
@@ -68,14 +81,15 @@ __global__ void k_div(const float* divisors, int nd, uint32_t samples) {
 }
 
 int main() {
-  const unsigned long long zero[3] = {0, 0, 0};
-  const unsigned int big[3] = {~0u, ~0u, ~0u};
+  const unsigned long long zero[4] = {0, 0, 0, 0};
+  const unsigned int big[4] = {~0u, ~0u, ~0u, ~0u};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_first), big, sizeof(big));
   const uint32_t s_lo = 0x0F800000u, s_hi = 0x71800000u;  // 2^-96 .. 2^100
   const uint32_t r_lo = 0x0D800000u, r_hi = 0x71800000u;  // 2^-100 .. 2^100
   hipLaunchKernelGGL(k_sqrt, dim3(8192), dim3(256), 0, 0, s_lo, s_hi);
   hipLaunchKernelGGL(k_rcp, dim3(8192), dim3(256), 0, 0, r_lo, r_hi);
+  hipLaunchKernelGGL(k_invlen_all, dim3(16384), dim3(256), 0, 0);
   std::vector<float> dv;
   for (int b = 1; b <= 8192; ++b) dv.push_back((float)b);
   for (float b : {3840.0f, 2160.0f, 7680.0f, 4320.0f, 15360.0f}) dv.push_back(b);
@@ -87,13 +101,13 @@ int main() {
     std::printf("hip error\n");
     return 2;
   }
-  unsigned long long bad[3];
-  unsigned int first[3];
+  unsigned long long bad[4];
+  unsigned int first[4];
   (void)hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad));
   (void)hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first));
-  const char* names[3] = {"sqrt_nrm", "rcp_nrm/inv_len", "div_nrm"};
+  const char* names[4] = {"sqrt_nrm", "rcp_nrm/inv_len_nrm", "div_nrm", "inv_len (all 2^32)"};
   int rc = 0;
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
     std::printf("%s: %llu mismatches%s", names[i], bad[i], bad[i] ? "" : "\n");
     if (bad[i]) {
       std::printf(" (first input bits 0x%08x)\n", first[i]);
