@@ -715,9 +715,9 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
-// Bounce 0, lane groups per pixel (f.pixel_major == kFoldWave: batches of >= kWaveFoldMinK samples
-// where the thread-per-pixel loop above would leave resident threads idle (sharded frames) or be
-// unbalanced (scenes traversed from L2/HBM, where per-pixel cost varies by orders of magnitude)).
+// Bounce 0, lane groups per pixel (f.pixel_major == kFoldWave: LDS-staged scenes in batches of >=
+// kWaveFoldMinK samples where the thread-per-pixel loop above would leave resident threads idle,
+// i.e. the per-rank share of a sharded frame).
 // A wave owns 8 local pixels; the 8 lanes of pixel g trace its samples 8 at a time (lane q takes
 // sample r*8 + q of round r), so a wave's rays come from 8 neighbouring pixels.  A pixel's leading
 // misses (the samples before its first hit) are summed into the accumulator in sample order — an
@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
 // 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 template <bool kLds, bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
     k_trace_wp(SceneView sv, EnvView sh, FrameView f, WaveView w) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
@@ -1524,7 +1524,10 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
                                       : resident_grid((const void*)&k_trace_pm<false, false, false>, lb);
     if ((uint64_t)f.P >= (uint64_t)g * kBlock * kPixelMajorItems) return kFoldThread;
   }
-  return f.k >= kWaveFoldMinK ? kFoldWave : kFoldNone;
+  // L2/HBM scenes stay path-major: measured on MI355X (r02l), the lane-group kernel's fold state
+  // costs the BVH4 traversal its registers (33 VGPR spills at 7 waves) and more than the saved
+  // radiance round trip (C3 trace0 + k_accum 10.0 -> 10.9 ms, C5 7.3 -> 10.6 ms)
+  return (sv.lds_bytes != 0 && f.k >= kWaveFoldMinK) ? kFoldWave : kFoldNone;
 }
 
 // Template dispatch over runtime flags: dispatch(fn, Flags<>{}, b0, b1, ...) calls
