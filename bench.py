@@ -262,6 +262,9 @@ def main():
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="timing experiment on one GPU: render only shard 0 of G (the per-rank work of a G-GPU run); "
                          "the line is marked emulated and is not a G-GPU measurement")
+    ap.add_argument("--integrator", default="wavefront", choices=["wavefront", "pathtracer"],
+                    help="pathtracer: the reference's default CPU integrator semantics (PathTracer.cpp), "
+                         "4 samples per frame; the headline metric is the wavefront integrator's")
     ap.add_argument("--stage-timing", action="store_true",
                     help="HIP events around every stage (default: around the k_trace launches only, which the "
                          "roofline needs; events between the other stages would add dispatch gaps)")
@@ -324,11 +327,15 @@ def main():
     torch.cuda.set_stream(torch_stream)
     stream = torch_stream.cuda_stream
 
+    integ = sptr.SPTR_INTEGRATOR_PATHTRACER if args.integrator == "pathtracer" else sptr.SPTR_INTEGRATOR_WAVEFRONT
+    # PathTracer mode: a frame is 4 samples (setupPathTracer), so spp/4 frames give the same samples
+    frames = max(1, wl.spp // 4) if args.integrator == "pathtracer" else wl.spp
+
     def step(flags=0):
         # every stage of a step is enqueued on torch's current stream, with no host synchronisation:
         # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL all-gather -> rank-0 unpack
-        r.render(cam, W, H, spp=wl.spp, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
-                 flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream)
+        r.render(cam, W, H, spp=frames, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
+                 flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream, integrator=integ, samples_per_frame=4)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
         send[: local_tiles.numel()].copy_(local_tiles)
@@ -369,7 +376,8 @@ def main():
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, rays, samples = float(tmax[0]), float(tsum[1]), float(tsum[2])
         # the gathered frame is the same bytes a 1-GPU render gives (tests/test_gpu_parity.py shard union)
-        assert int(tsum[2]) == W * H * wl.spp * args.steps, (int(tsum[2]), W * H * wl.spp * args.steps)
+        want = W * H * (frames * 4 if args.integrator == "pathtracer" else wl.spp) * args.steps
+        assert int(tsum[2]) == want, (int(tsum[2]), want)
 
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
@@ -393,6 +401,7 @@ def main():
             "config": {"workload": wl.description, "scene": os.path.basename(wl.scene), "width": W, "height": H,
                        "spp": wl.spp, "max_depth": wl.max_depth,
                        "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL all-gather"},
+            "integrator": args.integrator,
             "world_size": world,
             "collective": ("RCCL all_gather_into_tensor of the RGBA8 tiles, once per step" if distributed
                            else "none (1 rank)"),
@@ -409,9 +418,12 @@ def main():
             line["experiment_knobs"] = knobs
         if args.emulate_shards:
             line["emulated"] = f"shard 0 of {shards} on one GPU: per-rank work of a {shards}-GPU run (not a multi-GPU value)"
-        if world == 1 and not args.no_interactive and not args.emulate_shards:
+        if args.integrator == "pathtracer":
+            line["note"] = ("PathTracer-mode throughput (the reference's default CPU integrator semantics, path per "
+                            "thread); not the headline wavefront metric; roofline fields describe no k_trace launch")
+        if world == 1 and not args.no_interactive and not args.emulate_shards and args.integrator == "wavefront":
             line["interactive"] = interactive(200)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.integrator == "wavefront":
             line["cpu_baseline"] = cpu_baseline(wl, flat, cam)
         print(json.dumps(line), flush=True)
     r.close()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 2
+#define SPTR_ABI_VERSION 3
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -112,10 +112,27 @@ enum sptr_frame_flags {
                                    trace_launches): the other stages run back to back */
 };
 
-/* One render call = `spp` progressive frames (samples per pixel) starting at accumulation index
- * frame_begin (1-based, as GLRenderer::m_accumulated_samples; frame_begin == 1 clears the
- * accumulation).  Pixels are rendered in 32x32 tiles (GLRenderer.h:36); with shard_count > 1 only
- * tiles t with t % shard_count == shard_rank are rendered (interleaved multi-GPU sharding). */
+/* Integrators (sptr_frame.integrator).  The reference selects between them per frame in
+ * GLRenderer::renderLoop (src/GLRenderer.cpp:163-176):
+ *   SPTR_INTEGRATOR_WAVEFRONT : WavefrontPathTracerCPU semantics (src/wavefront/wf_pt_cpu.cpp:61-255,
+ *                               seeded and resolved by GLRenderer::renderWavefrontTileTask, :353-435):
+ *                               one jittered sample per frame, deterministic wang-hash RNG, ACES +
+ *                               gamma at resolve.  The default, and the parity / benchmark path.
+ *   SPTR_INTEGRATOR_PATHTRACER: PathTracer semantics, the reference's default CPU integrator
+ *                               (src/PathTracer.cpp:113-391): pixel-corner rays without jitter,
+ *                               samples_per_frame recursive samples per frame averaged, ACES + gamma
+ *                               per frame, tonemapped frames accumulated.  The reference draws from a
+ *                               non-reproducible mt19937(random_device); this mode uses a
+ *                               deterministic per-(pixel, frame, sample) wang-hash stream instead
+ *                               (DESIGN.md), so it matches the reference in distribution only. */
+enum sptr_integrator { SPTR_INTEGRATOR_WAVEFRONT = 0, SPTR_INTEGRATOR_PATHTRACER = 1 };
+
+/* One render call = `spp` progressive frames starting at accumulation index frame_begin (1-based,
+ * as GLRenderer::m_accumulated_samples; frame_begin == 1 clears the accumulation).  A wavefront
+ * frame is one sample per pixel; a PathTracer frame is samples_per_frame samples (0 = 4, the
+ * reference's setupPathTracer, src/main.cpp:105-113).  Pixels are rendered in 32x32 tiles
+ * (GLRenderer.h:36); with shard_count > 1 only tiles t with t % shard_count == shard_rank are
+ * rendered (interleaved multi-GPU sharding). */
 typedef struct sptr_frame {
   int32_t width, height;
   sptr_camera camera;
@@ -124,6 +141,8 @@ typedef struct sptr_frame {
   uint32_t max_depth;
   int32_t shard_rank, shard_count;
   uint32_t flags;
+  uint32_t integrator;        /* sptr_integrator */
+  uint32_t samples_per_frame; /* PathTracer mode only */
 } sptr_frame;
 
 typedef struct sptr_stats {
@@ -188,8 +207,9 @@ int sptr_scene_layout_info(const sptr_ctx* ctx, sptr_scene_layout* out);
 int sptr_render(sptr_ctx* ctx, const sptr_frame* frame, void* stream, sptr_stats* stats);
 /* Wait for the uncollected render calls and return their summed stats (zero when there are none). */
 int sptr_collect_stats(sptr_ctx* ctx, sptr_stats* stats);
-/* Full image RGB8 (width*height*3; only this shard's tiles are written) and the linear accumulation
- * sums (width*height*3 floats: sum of samples, divide by the sample count for the mean). */
+/* Full image RGB8 (width*height*3; only this shard's tiles are written) and the accumulation sums
+ * (width*height*3 floats; divide by the frame count for the mean): linear radiance in wavefront
+ * mode, tonemapped per-frame colours in PathTracer mode (what GLRenderer accumulates). */
 int sptr_read_rgb8(sptr_ctx* ctx, uint8_t* rgb);
 int sptr_read_accum(sptr_ctx* ctx, float* accum);
 /* Device view of this shard's resolved tiles: RGBA8, [local tile][32][32] uint32, for the

@@ -72,6 +72,7 @@ def lib():
             "oracle_env": (None, [fp, C.c_int, C.c_float, C.c_float, fp, C.c_uint32, fp]),
             "oracle_equirect_to_faces": (None, [fp, C.c_int, C.c_int, C.c_int, fp]),
             "oracle_render": (C.c_int, [vp, C.POINTER(Job)]),
+            "oracle_render_pt": (C.c_int, [vp, C.POINTER(Job), C.c_uint32]),
             "oracle_resolve": (None, [fp, C.c_uint32, C.c_uint32, bp]),
         }
         for n, (r, a) in sig.items():
@@ -175,8 +176,10 @@ class Prepared:
     def render(self, cam: np.ndarray, width: int, height: int, materials: np.ndarray, lights: np.ndarray,
                frames: int = 1, frame_begin: int = 1, max_depth: int = 6, shard_rank: int = 0,
                shard_count: int = 1, threads: int = 0, env_faces: np.ndarray | None = None,
-               env_intensity: float = 0.8, env_clamp: float = 5.0, accum: np.ndarray | None = None):
-        """Returns (accum (H,W,3) float32 sums, rgb8 (H,W,3), counters dict)."""
+               env_intensity: float = 0.8, env_clamp: float = 5.0, accum: np.ndarray | None = None,
+               pathtracer_spf: int = 0):
+        """Returns (accum (H,W,3) float32 sums, rgb8 (H,W,3), counters dict).  pathtracer_spf > 0 selects
+        the PathTracer integrator (the reference's default CPU path) with that many samples per frame."""
         mats = np.ascontiguousarray(materials, np.float32)
         lts = np.ascontiguousarray(lights, np.float32)
         acc = np.zeros((height, width, 3), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32)
@@ -194,7 +197,8 @@ class Prepared:
         j.shard_rank, j.shard_count = shard_rank, shard_count
         j.threads, j.use_bvh = threads, 1 if self.bvh else 0
         j.accum, j.rgb = _f(acc), _b(rgb)
-        rc = lib().oracle_render(self.h, C.byref(j))
+        rc = lib().oracle_render_pt(self.h, C.byref(j), pathtracer_spf) if pathtracer_spf else \
+            lib().oracle_render(self.h, C.byref(j))
         if rc != 0:
             raise RuntimeError(f"oracle_render rc={rc}")
         c = list(j.counters)

@@ -15,6 +15,9 @@
 //    BRDF     : src/Material.cpp:32-117, include/Material.h:19-147, src/MaterialManager.cpp:21-103
 //    lights   : src/Light.cpp:16-55
 //    env      : src/EnvironmentManager.cpp:9-74, src/Cubemap.cpp:82-180, 252-345
+//    PathTracer mode: src/PathTracer.cpp:59-75, 82-111, 113-224, 280-303, 331-406 (the reference's
+//               default CPU integrator; its mt19937(random_device) is replaced by the same
+//               deterministic per-(pixel, frame, sample) wang-hash stream as the product's pt_seed)
 //
 //  PARITY UNPINNED: the reference ships no tests, golden images or known-answer vectors for this
 //  path and cannot be compiled here (Embree, glm, TBB, OptiX absent), so this
@@ -919,6 +922,93 @@ static inline void resolve_pixel(V3 acc, uint32_t n, uint8_t* out) {
   out[2] = static_cast<unsigned char>(c.z * 255.0f);
 }
 
+// ----------------------------------------------------------------------------- PathTracer mode
+// PathTracer::tracePathMonteCarlo (PathTracer.cpp:113-224) evaluated forward with a throughput (as
+// the product does; the estimator is the recursion's), with the deterministic RNG stream below.
+static inline uint32_t pt_seed(uint32_t ps, uint32_t acc, uint32_t s) {
+  return wang_hash(wang_hash(ps ^ (acc * 9781u)) ^ (s * 0x9E3779B9u + 0x68E31DA4u));
+}
+static V3 pt_path(const Ctx& x, V3 o, V3 d, uint32_t& rng, Counters& cnt) {
+  const float inf = std::numeric_limits<float>::infinity();
+  V3 rad = mk(0, 0, 0), thr = mk(1, 1, 1);
+  for (uint32_t lvl = 0; lvl < x.max_depth; ++lvl) {
+    HitRec h;
+    ++cnt.closest;
+    if (!closest_hit(*x.P, o, d, 1e-4f, inf, h, x.bvh)) {  // intersectRay: tnear 1e-4 (:82-100)
+      rad = rad + thr * env_color(x.env, normalize(d));
+      break;
+    }
+    const V3 P = o + h.t * d;
+    V3 n = normalize(h.Ng);
+    if (dot(n, d) > 0.0f) n = -n;
+    const Material& m = material_of(x, h.geom);
+    V3 color = m.emission;
+    const V3 view = -d;
+    for (const Light& L : *x.lights) {
+      V3 ldir;
+      float ldist = 0.0f;
+      const V3 Li = light_radiance(L, P, ldir, ldist);
+      const float cs = std::max(dot(n, ldir), 0.0f);
+      if (!(cs > 0.0f)) continue;
+      const float eps = 1e-4f * gmax(1.0f, gmax(gmax(std::fabs(P.x), std::fabs(P.y)), std::fabs(P.z)));
+      ++cnt.shadow;
+      if (!occluded(*x.P, P + n * eps, ldir, 1e-4f, ldist - 1e-4f, x.bvh)) color = color + eval_brdf(m, n, view, ldir) * Li * cs;
+    }
+    rad = rad + thr * color;
+    // calculateSafeRayOrigin (:103-111)
+    const float eps = 1e-4f * gmax(1.0f, gmax(gmax(std::fabs(P.x), std::fabs(P.y)), std::fabs(P.z)));
+    if (m.metallic > 0.5f) {
+      d = reflect(d, n);
+      o = P + n * eps;
+      thr = (thr * m.albedo) * m.metallic;
+      continue;
+    }
+    if (is_transparent(m)) {
+      const float ior = m.ior;
+      const float cosine = -dot(d, n);
+      const float eta = cosine > 0.0f ? (1.0f / ior) : ior;
+      const float tr = transparency(m);
+      float r0 = (1.0f - ior) / (1.0f + ior);  // schlickFresnel (:391-395)
+      r0 = r0 * r0;
+      const float fres = r0 + (1.0f - r0) * std::pow(1.0f - std::fabs(cosine), 5.0f);
+      if (rand01(rng) < fres) {
+        d = reflect(d, n);
+        o = P + n * eps;
+        thr = thr * (1.0f - tr);
+        continue;
+      }
+      const float cos_i = -dot(d, n);  // PathTracer::refract (:396-406)
+      const float sin_t2 = eta * eta * (1.0f - cos_i * cos_i);
+      V3 refr = mk(0, 0, 0);
+      if (!(sin_t2 >= 1.0f)) refr = eta * d + (eta * cos_i - std::sqrt(1.0f - sin_t2)) * n;
+      if (dot(refr, refr) > 0.0f) {
+        o = P - n * eps;
+        d = refr;
+        thr = thr * tr;
+      } else {
+        d = reflect(d, n);
+        o = P + n * eps;
+      }
+      continue;
+    }
+    const float r1 = rand01(rng);  // cosineHemisphereSample (:59-75)
+    const float r2 = rand01(rng);
+    const float cos_t = std::sqrt(r1), sin_t = std::sqrt(1.0f - r1);
+    const float phi = float(2.0 * 3.14159265358979323846 * double(r2));
+    const V3 sd = mk(sin_t * std::cos(phi), cos_t, sin_t * std::sin(phi));
+    const V3 up = (std::fabs(n.x) < 0.9f) ? mk(1, 0, 0) : mk(0, 1, 0);
+    const V3 tg = normalize(cross(up, n));
+    const V3 bt = cross(n, tg);
+    const V3 scatter = tg * sd.x + n * sd.y + bt * sd.z;
+    o = P + n * eps;
+    const float surv = gmax(gmax(m.albedo.x, m.albedo.y), m.albedo.z);
+    if (!(rand01(rng) < surv)) break;
+    thr = (thr * m.albedo) / surv;
+    d = scatter;
+  }
+  return rad;
+}
+
 }  // namespace orc
 
 // ===================================================================================== C ABI
@@ -956,7 +1046,7 @@ struct oracle_job {
   uint64_t counters[4];  // closest-hit queries, shadow queries, samples, bounces
 };
 
-int oracle_version(void) { return 3; }
+int oracle_version(void) { return 4; }
 
 uint32_t oracle_wang_hash(uint32_t a) { return wang_hash(a); }
 
@@ -1195,6 +1285,96 @@ int oracle_render(void* h, oracle_job* job) {
   job->counters[1] = c_shadow;
   job->counters[2] = c_samples;
   job->counters[3] = c_bounces;
+  return 0;
+}
+
+// PathTracer-mode render (PathTracer::renderImage / renderTileTask / traceRay, PathTracer.cpp:280-389):
+// per pixel the corner ray u = x/W, v = y/H; per frame `samples_per_frame` paths averaged, ACES, gamma;
+// accum += frame colour; rgb = clamp(accum / frames) * 255.  Same tiles / shards / threads as
+// oracle_render.
+int oracle_render_pt(void* h, oracle_job* job, uint32_t samples_per_frame) {
+  const Prepared& P = *static_cast<Prepared*>(h);
+  std::vector<Material> mats(job->num_materials);
+  for (uint32_t i = 0; i < job->num_materials; ++i) {
+    const float* m = job->materials + i * 12;
+    mats[i] = Material{mk(m[0], m[1], m[2]), m[3], m[4], mk(m[5], m[6], m[7]), m[8], int(m[9])};
+  }
+  std::vector<Light> lights(job->num_lights);
+  for (uint32_t i = 0; i < job->num_lights; ++i) {
+    const float* l = job->lights + i * 8;
+    lights[i] = Light{int(l[0]), mk(l[1], l[2], l[3]), mk(l[4], l[5], l[6]), l[7]};
+  }
+  if (mats.empty() || samples_per_frame == 0) return -1;
+  Ctx x;
+  x.P = &P;
+  x.mats = &mats;
+  x.lights = &lights;
+  x.env.faces = job->env_faces;
+  x.env.size = job->env_size;
+  x.env.intensity = job->env_intensity;
+  x.env.max_clamp = job->env_clamp;
+  x.max_depth = job->max_depth;
+  x.bvh = job->use_bvh != 0;
+  const Camera cam = cam_from(job->cam);
+  const int W = job->width, H = job->height, TS = 32;
+  const int ntx = (W + TS - 1) / TS, nty = (H + TS - 1) / TS, ntiles = ntx * nty;
+  const int G = job->shard_count > 0 ? job->shard_count : 1, R = job->shard_rank;
+  std::atomic<int> next{0};
+  std::atomic<uint64_t> c_closest{0}, c_shadow{0}, c_samples{0};
+  auto worker = [&]() {
+    Counters cnt;
+    for (;;) {
+      const int t = next.fetch_add(1);
+      if (t >= ntiles) break;
+      if (t % G != R) continue;
+      const int tx = t % ntx, ty = t / ntx;
+      const int x0 = tx * TS, y0 = ty * TS, x1 = std::min(x0 + TS, W), y1 = std::min(y0 + TS, H);
+      for (int y = y0; y < y1; ++y)
+        for (int xx = x0; xx < x1; ++xx) {
+          const uint32_t ps = uint32_t(y * W + xx);
+          float* acc = job->accum + size_t(ps) * 3;
+          V3 a = mk(acc[0], acc[1], acc[2]);
+          const V3 dir = ray_dir(cam, float(xx) / float(W), float(y) / float(H));
+          for (uint32_t f = 0; f < job->num_frames; ++f) {
+            const uint32_t n = job->frame_begin + f;
+            V3 c = mk(0, 0, 0);
+            for (uint32_t s = 0; s < samples_per_frame; ++s) {
+              uint32_t rng = pt_seed(ps, n, s);
+              c = c + pt_path(x, cam.pos, dir, rng, cnt);
+              ++cnt.samples;
+            }
+            c = c / float(samples_per_frame);
+            const float ka = 2.51f, kb = 0.03f, kc = 2.43f, kd = 0.59f, ke = 0.14f;  // acesToneMapping
+            c = gclamp((c * (ka * c + kb)) / (c * (kc * c + kd) + ke), 0.0f, 1.0f);
+            const float g = 1.0f / 2.2f;
+            c = mk(std::pow(c.x, g), std::pow(c.y, g), std::pow(c.z, g));
+            a = a + c;
+          }
+          acc[0] = a.x; acc[1] = a.y; acc[2] = a.z;
+          if (job->rgb) {
+            const uint32_t frames = job->frame_begin + job->num_frames - 1;
+            const V3 avg = gclamp(a / float(frames), 0.0f, 1.0f);
+            uint8_t* o = job->rgb + size_t(ps) * 3;
+            o[0] = static_cast<unsigned char>(avg.x * 255.0f);
+            o[1] = static_cast<unsigned char>(avg.y * 255.0f);
+            o[2] = static_cast<unsigned char>(avg.z * 255.0f);
+          }
+        }
+    }
+    c_closest += cnt.closest;
+    c_shadow += cnt.shadow;
+    c_samples += cnt.samples;
+  };
+  int nt = job->threads > 0 ? job->threads : int(std::thread::hardware_concurrency());
+  if (nt < 1) nt = 1;
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  job->counters[0] = c_closest;
+  job->counters[1] = c_shadow;
+  job->counters[2] = c_samples;
+  job->counters[3] = 0;
   return 0;
 }
 

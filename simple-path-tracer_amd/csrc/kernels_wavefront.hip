@@ -18,6 +18,7 @@
 // place that uses fma: they only prune traversal and are padded to stay conservative.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "sptr_internal.h"
@@ -1324,16 +1325,27 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float
   }
 }
 
-__device__ __forceinline__ uint32_t resolve_rgba(vec3 acc, uint32_t n) {
-  vec3 c = acc / float(n);
-  c = clamp_g((c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f), 0.0f, 1.0f);
-  const float g = 1.0f / 2.2f;
-  c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
-  c = clamp_g(c, 0.0f, 1.0f);
+// EnvironmentManager::acesToneMapping (src/EnvironmentManager.cpp:63-74)
+__device__ __forceinline__ vec3 aces(vec3 c) {
+  return clamp_g((c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f), 0.0f, 1.0f);
+}
+__device__ __forceinline__ uint32_t pack_rgba(vec3 c) {
   const uint32_t r = (uint32_t)(unsigned char)(c.x * 255.0f);
   const uint32_t gg = (uint32_t)(unsigned char)(c.y * 255.0f);
   const uint32_t b = (uint32_t)(unsigned char)(c.z * 255.0f);
   return r | (gg << 8) | (b << 16) | 0xFF000000u;
+}
+// Wavefront tile task resolve (GLRenderer.cpp:411-431): mean -> ACES -> gamma -> clamp -> 8 bit
+__device__ __forceinline__ uint32_t resolve_rgba(vec3 acc, uint32_t n) {
+  vec3 c = aces(acc / float(n));
+  const float g = 1.0f / 2.2f;
+  c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
+  return pack_rgba(clamp_g(c, 0.0f, 1.0f));
+}
+// PathTracer::renderTileTask resolve (PathTracer.cpp:364-384): the frames were tonemapped as they
+// were traced, so the display value is the clamped mean
+__device__ __forceinline__ uint32_t resolve_rgba_pt(vec3 acc, uint32_t n) {
+  return pack_rgba(clamp_g(acc / float(n), 0.0f, 1.0f));
 }
 
 __global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n, uint32_t* tiles,
@@ -1341,7 +1353,8 @@ __global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* a
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     int x, y;
     const bool valid = local_pixel(f, l, x, y);
-    const uint32_t px = valid ? resolve_rgba(xyz(accum[l]), n) : 0u;
+    uint32_t px = 0u;
+    if (valid) px = f.integrator == SPTR_INTEGRATOR_PATHTRACER ? resolve_rgba_pt(xyz(accum[l]), n) : resolve_rgba(xyz(accum[l]), n);
     tiles[l] = px;
     if (valid && image) {
       uint8_t* o = image + ((size_t)y * f.W + x) * 3;
@@ -1364,6 +1377,179 @@ __global__ void __launch_bounds__(kBlock) k_unpack(const uint32_t* g, int G, uin
     rgb[(size_t)i * 3 + 1] = (uint8_t)((px >> 8) & 0xFF);
     rgb[(size_t)i * 3 + 2] = (uint8_t)((px >> 16) & 0xFF);
   }
+}
+
+// --------------------------------------------------------------------------------- k_pathtracer
+// The reference's default CPU integrator, PathTracer (src/PathTracer.cpp:113-391), for
+// SPTR_INTEGRATOR_PATHTRACER.  Differences from the wavefront integrator, all reproduced:
+//   * camera ray through the pixel corner, u = x/W, v = y/H, no jitter (renderTileTask :351-355);
+//   * intersection tnear 1e-4 (intersectRay :82-100) and normal = normalize(Ng) (:131-137);
+//   * continuation origins offset by 1e-4 * max(1, |P|inf) (calculateSafeRayOrigin :103-111);
+//     reflection, refraction and scatter directions are not renormalised;
+//   * glass: eta from cosine > 0, refract() with sin_t2 >= 1 as total internal reflection
+//     (:176-206, :396-406); Fresnel pow((1 - c), 5.0f) (:391-395);
+//   * diffuse: cosineHemisphereSample (:59-75, y-up local frame, phi in double), Russian roulette
+//     at every bounce (:208-219);
+//   * samples_per_frame samples per frame averaged, then ACES and gamma (traceRay :280-303); the
+//     tonemapped frames are what accumulates.
+// The recursion color = emission + direct + weight * trace(depth - 1) is evaluated forward with a
+// path throughput (same terms and estimator; the rounding of the outer sums differs).  RNG: the
+// reference's thread-local mt19937(random_device) is not reproducible; each (pixel, frame, sample)
+// here draws from its own wang-hash stream (pt_seed), which the oracle restates.
+__device__ __forceinline__ uint32_t pt_seed(uint32_t ps, uint32_t acc, uint32_t s) {
+  return wang_hash(wang_hash(ps ^ (acc * 9781u)) ^ (s * 0x9E3779B9u + 0x68E31DA4u));
+}
+
+template <bool kW4, bool kCube>
+__device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& sh, const DevMaterial* smat, uint32_t nm,
+                        vec3 o, vec3 d, uint32_t depth, uint32_t& rng, Visits& vc, LdsStack& ls, uint32_t& n_closest,
+                        uint32_t& n_shadow) {
+  vec3 rad = v3(0.0f, 0.0f, 0.0f), thr = v3(1.0f, 1.0f, 1.0f);
+  for (uint32_t lvl = 0; lvl < depth; ++lvl) {
+    ++n_closest;
+    float t = __builtin_huge_valf();
+    uint32_t ref = kNoHit;
+    if (!traverse_w<kW4, false, false>(sc, sv, make_ray(o, d), 1e-4f, t, ref, vc, ls)) {
+      rad = rad + thr * env_color<kCube>(sh.env, normalize_dir(d));
+      break;
+    }
+    const vec3 P = o + t * d;
+    const uint32_t idx = ref & kIndexMask;
+    vec3 ng;
+    uint32_t mid;
+    if (ref & kSphereBit) {
+      const float4 c = sc.sph[idx];
+      ng = v3((P.x - c.x) / c.w, (P.y - c.y) / c.w, (P.z - c.z) / c.w);
+      mid = sh.geom_mat[sv.sph_geom[idx]];
+    } else {
+      const float4 c = sc.tris[3 * idx + 2];
+      ng = v3(c.y, c.z, c.w);
+      mid = sh.geom_mat[sv.tri_geom[idx]];
+    }
+    vec3 n = normalize(ng);
+    if (dot(n, d) > 0.0f) n = -n;
+    const DevMaterial& m = (mid < nm) ? smat[mid] : sh.mats[mid];
+    const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    vec3 color = v3(m.emission[0], m.emission[1], m.emission[2]);
+    const vec3 view = -d;
+    for (uint32_t li = 0; li < sh.num_lights; ++li) {
+      vec3 ldir, Li;
+      float ldist;
+      light_at(sh.lights[li], P, ldir, ldist, Li);
+      const float cs = fmax_g(dot(n, ldir), 0.0f);
+      if (!(cs > 0.0f)) continue;
+      // Light::isOccluded (Light.cpp:16-40)
+      const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
+      float st = ldist - 1e-4f;
+      uint32_t sref = kNoHit;
+      ++n_shadow;
+      if (!traverse_w<kW4, true, false>(sc, sv, make_ray(P + n * eps, ldir), 1e-4f, st, sref, vc, ls))
+        color = color + eval_brdf(m, n, view, ldir) * Li * cs;
+    }
+    rad = rad + thr * color;
+    const float eps = 1e-4f * fmax_g(1.0f, fmax_g(fmax_g(fabsf(P.x), fabsf(P.y)), fabsf(P.z)));
+    if (m.metallic > 0.5f) {
+      d = reflect(d, n);
+      o = P + n * eps;
+      thr = (thr * albedo) * m.metallic;
+      continue;
+    }
+    if (m.metallic < 0.1f && m.ior > 1.3f) {
+      const float ior = m.ior;
+      const float cosine = -dot(d, n);
+      const float eta = cosine > 0.0f ? (1.0f / ior) : ior;
+      const float tr = clamp_g((ior - 1.0f) / 0.7f, 0.0f, 0.95f);
+      float r0 = (1.0f - ior) / (1.0f + ior);
+      r0 = r0 * r0;
+      const float fres = r0 + (1.0f - r0) * pow5(1.0f - fabsf(cosine));
+      if (rand01(rng) < fres) {
+        d = reflect(d, n);
+        o = P + n * eps;
+        thr = thr * (1.0f - tr);
+        continue;
+      }
+      // PathTracer::refract (PathTracer.cpp:396-406)
+      const float cos_i = -dot(d, n);
+      const float sin_t2 = eta * eta * (1.0f - cos_i * cos_i);
+      vec3 refr = v3(0.0f, 0.0f, 0.0f);
+      if (!(sin_t2 >= 1.0f)) refr = eta * d + (eta * cos_i - sqrtf(1.0f - sin_t2)) * n;
+      if (dot(refr, refr) > 0.0f) {
+        o = P - n * eps;
+        d = refr;
+        thr = thr * tr;
+      } else {
+        d = reflect(d, n);
+        o = P + n * eps;
+      }
+      continue;
+    }
+    // cosineHemisphereSample (PathTracer.cpp:59-75)
+    const float r1 = rand01(rng);
+    const float r2 = rand01(rng);
+    const float cos_t = sqrtf(r1), sin_t = sqrtf(1.0f - r1);
+    const float phi = (float)(2.0 * 3.14159265358979323846 * (double)r2);
+    const vec3 sd = v3(sin_t * cosf(phi), cos_t, sin_t * sinf(phi));
+    const vec3 up = (fabsf(n.x) < 0.9f) ? v3(1.0f, 0.0f, 0.0f) : v3(0.0f, 1.0f, 0.0f);
+    const vec3 tg = normalize_dir(cross(up, n));
+    const vec3 bt = cross(n, tg);
+    const vec3 scatter = tg * sd.x + n * sd.y + bt * sd.z;
+    o = P + n * eps;
+    const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
+    if (!(rand01(rng) < surv)) break;
+    thr = (thr * albedo) / surv;
+    d = scatter;
+  }
+  return rad;
+}
+
+// Thread per local pixel: the batch's k frames in order, samples_per_frame paths each; accum.xyz
+// += the frame's tonemapped colour (the reference's accumulation_buffer, GLRenderer's
+// m_accumulated_samples frames).
+template <bool kLds, bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView f, WaveView w) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ DevMaterial smat[32];
+  const uint32_t nm = stage_materials(sh, smat);
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  __syncthreads();
+  const ImageDiv idiv = image_div(f);
+  Visits vc;
+  uint32_t n_closest = 0u, n_shadow = 0u;
+  const Sched sd = block_sched(f.P);
+  for (uint32_t l = sd.first + threadIdx.x; l < f.P; l += sd.step) {
+    int x = 0, y = 0;
+    if (!local_pixel(f, l, x, y)) continue;
+    const uint32_t ps = (uint32_t)(y * f.W + x);
+    // renderTileTask: u = x / W, v = y / H (no +0.5, no jitter); Camera::getRayDirection
+    const vec3 dir = camera_dir(f, div_nrm(float(x), idiv.w), div_nrm(float(y), idiv.h));
+    vec3 acc = f.reset ? v3(0.0f, 0.0f, 0.0f) : xyz(f.accum[l]);
+    for (uint32_t fr = 0; fr < f.k; ++fr) {
+      const uint32_t accn = f.acc0 + fr;
+      vec3 c = v3(0.0f, 0.0f, 0.0f);
+      for (uint32_t s = 0; s < f.spf; ++s) {
+        uint32_t rng = pt_seed(ps, accn, s);
+        c = c + pt_path<kW4, kCube>(sc, sv, sh, smat, nm, f.cam_pos, dir, f.max_depth, rng, vc, s_stack, n_closest,
+                                    n_shadow);
+      }
+      c = c / float(f.spf);
+      c = aces(c);
+      const float g = 1.0f / 2.2f;
+      c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
+      acc = acc + c;
+    }
+    f.accum[l] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+  }
+  unsigned long long a = n_closest, b = n_shadow;
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  if (lane_id() == 0u) {
+    atomicAdd(&w.tot[kTotClosest], a);
+    atomicAdd(&w.tot[kTotShadow], b);
+  }
+  report_stack(vc, w.tot);
 }
 
 // --------------------------------------------------------------------------------- query kernels
@@ -1632,6 +1818,21 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
         return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
           const unsigned g = resident_grid((const void*)&k_tail<Lc, Wc, Cube>, lb);
           hipLaunchKernelGGL((k_tail<Lc, Wc, Cube>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth0, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
+}
+
+void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {
+  const bool L = sv.lds_bytes != 0;
+  const unsigned lb = L ? sv.lds_bytes : 16u;
+  dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
+          const unsigned g = std::min<unsigned>(resident_grid((const void*)&k_pathtracer<Lc, Wc, Cube>, lb),
+                                                (unsigned)((f.P + kBlock - 1) / kBlock));
+          hipLaunchKernelGGL((k_pathtracer<Lc, Wc, Cube>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w);
           return g;
         }(fl);
       },

@@ -195,6 +195,8 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.accum = static_cast<float4*>(c.accum.p);
   v.reset = 0;
   v.pixel_major = 0;
+  v.integrator = f.integrator;
+  v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
 }
 
@@ -336,6 +338,52 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   c.last_samples = 0;
   resized = true;
   return SPTR_OK;
+}
+
+// PathTracer-mode render call (SPTR_INTEGRATOR_PATHTRACER): path-per-thread frames, no wavefront
+// streams.  Frames are launched kPtFramesPerLaunch at a time (bounded launch length); the
+// accumulation order is the frame order either way.
+constexpr uint32_t kPtFramesPerLaunch = 4;
+int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s, sptr_stats* stats) {
+  const SceneView sv = scene_view(c);
+  const ShadeView sh = shade_view(c);
+  WaveView w = wave_view(c);
+  FrameView fv = frame_view(c, f);
+  const bool timing = (f.flags & (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE)) != 0;
+  StageTimer tm{c, timing, false, s};
+  if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+  tm.begin_call();
+  uint32_t done = 0, launches = 0;
+  while (done < f.spp) {
+    fv.k = std::min<uint32_t>(kPtFramesPerLaunch, f.spp - done);
+    fv.acc0 = f.frame_begin + done;
+    fv.reset = (reset && done == 0) ? 1u : 0u;
+    tm.begin(7);
+    launch_pathtracer(sv, sh, fv, w, s);
+    tm.end();
+    done += fv.k;
+    ++launches;
+  }
+  const uint32_t total = f.frame_begin + f.spp - 1;
+  if (!(f.flags & SPTR_FRAME_NO_RESOLVE)) {
+    tm.begin(4);
+    launch_resolve(fv, static_cast<const float4*>(c.accum.p), total, static_cast<uint32_t*>(c.tiles.p),
+                   static_cast<uint8_t*>(c.image.p), s);
+    tm.end();
+  }
+  tm.end_call();
+  API_HIP(hipGetLastError());
+  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
+  c.last_samples = total;
+  ++c.pending;
+  c.pending_stream = s;
+  c.pending_samples += (uint64_t)fv.valid * f.spp * fv.spf;
+  c.pending_waves += launches;
+  if (f.flags & SPTR_FRAME_ASYNC) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    return SPTR_OK;
+  }
+  return collect_pending(c, stats);
 }
 
 }  // namespace
@@ -560,6 +608,9 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   if (f->width <= 0 || f->height <= 0 || f->spp == 0 || f->max_depth == 0 || f->max_depth > (uint32_t)kMaxDepth ||
       f->frame_begin == 0)
     return fail(c, SPTR_ERR_INVALID, "render: bad frame parameters");
+  if (f->integrator > SPTR_INTEGRATOR_PATHTRACER) return fail(c, SPTR_ERR_INVALID, "render: unknown integrator");
+  if (f->integrator == SPTR_INTEGRATOR_PATHTRACER && f->samples_per_frame > 4096)
+    return fail(c, SPTR_ERR_INVALID, "render: samples_per_frame above 4096");
   const int G = f->shard_count > 0 ? f->shard_count : 1, R = f->shard_count > 0 ? f->shard_rank : 0;
   if (R < 0 || R >= G) return fail(c, SPTR_ERR_INVALID, "render: shard_rank out of range");
   const int ntiles = ((f->width + kTile - 1) / kTile) * ((f->height + kTile - 1) / kTile);
@@ -574,6 +625,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const bool reset = f->frame_begin == 1;
   if (!reset && f->frame_begin != c.last_samples + 1)
     return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
+  if (f->integrator == SPTR_INTEGRATOR_PATHTRACER) return render_pathtracer(c, *f, reset, s, stats);
   uint64_t wave_paths = c.wave_paths;
   if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
     wave_paths = kDefaultWavePaths;

@@ -128,6 +128,8 @@ struct FrameView {
   float4* accum;    // per local pixel: running sample sum (xyz) + resume slot (w bits), see k_accum
   uint32_t reset;   // this batch starts the accumulation (frame_begin == 1, first batch)
   uint32_t pixel_major;  // kFold*: bounce 0 folds each pixel's leading misses into accum (bounce0_pixel_major)
+  uint32_t integrator;   // sptr_integrator
+  uint32_t spf;          // PathTracer mode: samples per frame
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -255,6 +257,8 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
+// PathTracer-mode frames (the k frames of f from f.acc0), one launch: accum += tonemapped frames.
+void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
                    hipStream_t s);
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,

@@ -107,6 +107,8 @@ bool HipBackend::renderInternal(int w, int h, const Camera& camera) {
   fr.max_depth = settings_.max_depth;
   fr.shard_rank = 0;
   fr.shard_count = 1;
+  fr.integrator = settings_.integrator;
+  fr.samples_per_frame = settings_.samples_per_frame;
   const int rc = sptr_render(ctx_, &fr, nullptr, &stats_);
   if (rc != SPTR_OK) {
     err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);
@@ -126,7 +128,7 @@ void HipBackend::render(unsigned char* pixels, int width, int height, const Came
 
 bool HipBackend::renderLinear(float* rgb32, int width, int height, const Camera& camera) {
   if (!renderInternal(width, height, camera)) return false;
-  if (sptr_read_accum(ctx_, rgb32) != SPTR_OK) return false;
+  if (sptr_read_accum(ctx_, rgb32) != SPTR_OK) return false;  // PathTracer mode: mean tonemapped colour
   const float n = float(frame_index_);
   for (size_t i = 0; i < size_t(width) * height * 3; ++i) rgb32[i] /= n;
   return true;

@@ -21,6 +21,10 @@ class HipBackend {
   struct Settings {
     uint32_t spp_per_call = 1;  // progressive frames per render() call (GLRenderer renders 1)
     uint32_t max_depth = 6;     // PathTracer::Settings::max_depth used by the wavefront tile task
+    // SPTR_INTEGRATOR_WAVEFRONT (the 'T' key's wavefront CPU semantics, default) or
+    // SPTR_INTEGRATOR_PATHTRACER (the default key's PathTracer semantics, src/GLRenderer.cpp:172-176)
+    uint32_t integrator = SPTR_INTEGRATOR_WAVEFRONT;
+    uint32_t samples_per_frame = 4;  // PathTracer::Settings::samples_per_pixel (src/main.cpp:107)
   };
 
   explicit HipBackend(int device = 0);

@@ -24,6 +24,9 @@ SPTR_FRAME_COUNT_VISITS = 4
 SPTR_FRAME_ASYNC = 8
 SPTR_FRAME_TIMING_TRACE = 16
 
+SPTR_INTEGRATOR_WAVEFRONT = 0   # WavefrontPathTracerCPU semantics (default)
+SPTR_INTEGRATOR_PATHTRACER = 1  # PathTracer (the reference's default CPU integrator) semantics
+
 
 class SptrError(RuntimeError):
     pass
@@ -65,7 +68,8 @@ class Camera(C.Structure):
 class Frame(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("camera", Camera), ("frame_begin", C.c_uint32),
                 ("spp", C.c_uint32), ("max_depth", C.c_uint32), ("shard_rank", C.c_int32),
-                ("shard_count", C.c_int32), ("flags", C.c_uint32)]
+                ("shard_count", C.c_int32), ("flags", C.c_uint32), ("integrator", C.c_uint32),
+                ("samples_per_frame", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -398,8 +402,11 @@ class Renderer:
 
     def render(self, cam: Camera, width: int, height: int, spp: int = 1, frame_begin: int = 1,
                max_depth: int = 6, shard_rank: int = 0, shard_count: int = 1, flags: int = 0,
-               stream: int | None = None) -> Stats:
-        f = Frame(width, height, cam, frame_begin, spp, max_depth, shard_rank, shard_count, flags)
+               stream: int | None = None, integrator: int = SPTR_INTEGRATOR_WAVEFRONT,
+               samples_per_frame: int = 0) -> Stats:
+        """spp = progressive frames; integrator / samples_per_frame as in include/sptr_hip.h."""
+        f = Frame(width, height, cam, frame_begin, spp, max_depth, shard_rank, shard_count, flags, integrator,
+                  samples_per_frame)
         st = Stats()
         self._check(self._L.sptr_render(self._h, C.byref(f), C.c_void_p(stream) if stream else None, C.byref(st)),
                     "render")

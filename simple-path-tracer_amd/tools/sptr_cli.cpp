@@ -4,7 +4,7 @@
 // one render() per frame, progressive accumulation.
 //   sptr_cli [--scene default|default_emitter|test_triangle|sphere_mesh:STACKS:SLICES|gltf:PATH]
 //            [--w 800] [--h 600] [--spp 4] [--depth 6] [--env sky|FILE.hdr] [--out image.ppm]
-//            [--warmup N] [--json]
+//            [--warmup N] [--json] [--integrator wavefront|pathtracer] [--spf 4]
 // --spp N renders N progressive frames of 1 spp each (GLRenderer's m_accumulated_samples loop);
 // --warmup N renders N untimed frames first (then restarts the accumulation by a camera change);
 // --json prints one line with per-frame wall-clock statistics (render + RGB8 read back, as the
@@ -42,6 +42,8 @@ int main(int argc, char** argv) {
   std::string scene_name = "default", env = "sky", out = "image.ppm";
   int w = 800, h = 600, spp = 4, depth = 6, warmup = 0;
   bool json = false;
+  std::string integrator = "wavefront";
+  int spf = 4;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -54,6 +56,8 @@ int main(int argc, char** argv) {
     else if (a == "--out") out = next();
     else if (a == "--warmup") warmup = std::atoi(next());
     else if (a == "--json") json = true;
+    else if (a == "--integrator") integrator = next();
+    else if (a == "--spf") spf = std::atoi(next());
     else {
       std::fprintf(stderr, "usage: %s [--scene S] [--w W] [--h H] [--spp N] [--depth D] [--env sky|F.hdr] [--out F] [--warmup N] [--json]\n",
                    argv[0]);
@@ -80,6 +84,12 @@ int main(int argc, char** argv) {
   be.setEnvironment(&em);
   backends::HipBackend::Settings st;
   st.max_depth = uint32_t(depth);
+  if (integrator == "pathtracer") st.integrator = SPTR_INTEGRATOR_PATHTRACER;
+  else if (integrator != "wavefront") {
+    std::fprintf(stderr, "unknown integrator %s\n", integrator.c_str());
+    return 2;
+  }
+  st.samples_per_frame = uint32_t(spf);
   be.setSettings(st);
   if (!be.build(sd)) {
     std::fprintf(stderr, "%s\n", be.lastError().c_str());
