@@ -124,8 +124,15 @@ enum sptr_frame_flags {
  *                               per frame, tonemapped frames accumulated.  The reference draws from a
  *                               non-reproducible mt19937(random_device); this mode uses a
  *                               deterministic per-(pixel, frame, sample) wang-hash stream instead
- *                               (DESIGN.md), so it matches the reference in distribution only. */
-enum sptr_integrator { SPTR_INTEGRATOR_WAVEFRONT = 0, SPTR_INTEGRATOR_PATHTRACER = 1 };
+ *                               (DESIGN.md), so it matches the reference in distribution only.
+ *   SPTR_INTEGRATOR_OPTIX     : the shading of the reference's OptiX device programs
+ *                               (src/optix/device_programs.cu:220-690, 854-899; the 'G' key's GPU
+ *                               path): pixel-centre rays, wang_hash((pixel+1) ^ (frame*9781+1)) seeds,
+ *                               tmin 1e-3, direct sun light without shadow rays, GGX-sampled metals,
+ *                               delta dielectrics, depth-cap normal visualisation, exposure 2.2 +
+ *                               Reinhard + gamma at resolve.  Exact functions replace CUDA's
+ *                               approximate rsqrtf/sincosf. */
+enum sptr_integrator { SPTR_INTEGRATOR_WAVEFRONT = 0, SPTR_INTEGRATOR_PATHTRACER = 1, SPTR_INTEGRATOR_OPTIX = 2 };
 
 /* One render call = `spp` progressive frames starting at accumulation index frame_begin (1-based,
  * as GLRenderer::m_accumulated_samples; frame_begin == 1 clears the accumulation).  A wavefront

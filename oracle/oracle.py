@@ -73,6 +73,7 @@ def lib():
             "oracle_equirect_to_faces": (None, [fp, C.c_int, C.c_int, C.c_int, fp]),
             "oracle_render": (C.c_int, [vp, C.POINTER(Job)]),
             "oracle_render_pt": (C.c_int, [vp, C.POINTER(Job), C.c_uint32]),
+            "oracle_render_optix": (C.c_int, [vp, C.POINTER(Job), fp]),
             "oracle_resolve": (None, [fp, C.c_uint32, C.c_uint32, bp]),
         }
         for n, (r, a) in sig.items():
@@ -177,9 +178,11 @@ class Prepared:
                frames: int = 1, frame_begin: int = 1, max_depth: int = 6, shard_rank: int = 0,
                shard_count: int = 1, threads: int = 0, env_faces: np.ndarray | None = None,
                env_intensity: float = 0.8, env_clamp: float = 5.0, accum: np.ndarray | None = None,
-               pathtracer_spf: int = 0):
+               pathtracer_spf: int = 0, optix: bool = False, accum_w: np.ndarray | None = None):
         """Returns (accum (H,W,3) float32 sums, rgb8 (H,W,3), counters dict).  pathtracer_spf > 0 selects
-        the PathTracer integrator (the reference's default CPU path) with that many samples per frame."""
+        the PathTracer integrator (the reference's default CPU path) with that many samples per frame;
+        optix=True the OptiX device-program shading (accum_w: the per-pixel sample counts, (H,W) float32,
+        returned as the 4th counters key "accum_w")."""
         mats = np.ascontiguousarray(materials, np.float32)
         lts = np.ascontiguousarray(lights, np.float32)
         acc = np.zeros((height, width, 3), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32)
@@ -197,12 +200,21 @@ class Prepared:
         j.shard_rank, j.shard_count = shard_rank, shard_count
         j.threads, j.use_bvh = threads, 1 if self.bvh else 0
         j.accum, j.rgb = _f(acc), _b(rgb)
-        rc = lib().oracle_render_pt(self.h, C.byref(j), pathtracer_spf) if pathtracer_spf else \
-            lib().oracle_render(self.h, C.byref(j))
+        aw = None
+        if optix:
+            aw = np.zeros((height, width), np.float32) if accum_w is None else np.ascontiguousarray(accum_w, np.float32)
+            rc = lib().oracle_render_optix(self.h, C.byref(j), _f(aw))
+        elif pathtracer_spf:
+            rc = lib().oracle_render_pt(self.h, C.byref(j), pathtracer_spf)
+        else:
+            rc = lib().oracle_render(self.h, C.byref(j))
         if rc != 0:
             raise RuntimeError(f"oracle_render rc={rc}")
         c = list(j.counters)
-        return acc, rgb, {"rays_closest": c[0], "rays_shadow": c[1], "samples": c[2]}
+        out = {"rays_closest": c[0], "rays_shadow": c[1], "samples": c[2]}
+        if aw is not None:
+            out["accum_w"] = aw
+        return acc, rgb, out
 
 
 def primary(cam: np.ndarray, width: int, height: int, acc: int):

@@ -18,6 +18,9 @@
 //    PathTracer mode: src/PathTracer.cpp:59-75, 82-111, 113-224, 280-303, 331-406 (the reference's
 //               default CPU integrator; its mt19937(random_device) is replaced by the same
 //               deterministic per-(pixel, frame, sample) wang-hash stream as the product's pt_seed)
+//    OptiX mode: src/optix/device_programs.cu:78-218 (helpers), 220-274 (raygen), 297-309 (trace),
+//               315-690 (shade), 761-820 (closest hit), 854-899 (resolve); camera basis and light from
+//               src/backends/OptixBackend.cpp:1515-1620 (correctly rounded normalize for rsqrtf)
 //
 //  PARITY UNPINNED: the reference ships no tests, golden images or known-answer vectors for this
 //  path and cannot be compiled here (Embree, glm, TBB, OptiX absent), so this
@@ -1009,6 +1012,199 @@ static V3 pt_path(const Ctx& x, V3 o, V3 d, uint32_t& rng, Counters& cnt) {
   return rad;
 }
 
+// ----------------------------------------------------------------------------- OptiX mode
+static inline V3 ox_nrm(V3 v) { return v * (1.0f / std::sqrt(dot(v, v))); }  // f3_normalize
+static inline V3 ox_cross(V3 a, V3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static inline V3 ox_reflect(V3 v, V3 n) { return v + n * (-2.0f * dot(v, n)); }
+static inline void ox_onb(V3 n, V3& t, V3& b) {
+  const V3 up = (std::fabs(n.z) < 0.999f) ? mk(0, 0, 1) : mk(1, 0, 0);
+  t = ox_nrm(ox_cross(up, n));
+  b = ox_cross(n, t);
+}
+static inline V3 ox_fresnel(float cosVH, V3 F0) {
+  const float m = 1.0f - std::min(std::max(cosVH, 0.0f), 1.0f);
+  const float m2 = m * m;
+  const float m5 = m2 * m2 * m;
+  return F0 + mk(1.0f - F0.x, 1.0f - F0.y, 1.0f - F0.z) * m5;
+}
+static inline float ox_smith(float cosNL, float cosNV, float alpha) {
+  const float a = alpha + 1.0f;
+  const float k = (a * a) * 0.125f;
+  return (cosNL / (cosNL * (1.0f - k) + k)) * (cosNV / (cosNV * (1.0f - k) + k));
+}
+static inline V3 ox_fallback_reflect(V3 d, V3 n) {
+  const V3 R = ox_reflect(d, n);
+  const float l2 = dot(R, R);
+  return l2 > 0.0f ? R * (1.0f / std::sqrt(l2)) : n;
+}
+struct OxFrame {
+  V3 u, v, w, light_dir, light_rad;
+  bool has_light;
+};
+static void ox_path(const Ctx& x, const OxFrame& F, V3 o, V3 d, uint32_t rng, V3& acc, Counters& cnt) {
+  const float kPi = 3.14159265358979323846f;
+  V3 thr = mk(1, 1, 1);
+  for (uint32_t depth = 0; depth < x.max_depth; ++depth) {
+    HitRec h;
+    ++cnt.closest;
+    if (!closest_hit(*x.P, o, d, 1e-3f, 1e16f, h, x.bvh)) {
+      const V3 c = env_color(x.env, ox_nrm(d));
+      acc = acc + mk(c.x * thr.x, c.y * thr.y, c.z * thr.z);
+      return;
+    }
+    const V3 P = o + d * h.t;
+    V3 ng;
+    const bool sphere = h.geom >= x.P->ngeom_tri;
+    if (sphere) {
+      const float* s = &x.P->sph[size_t(h.geom - x.P->ngeom_tri) * 4];
+      ng = ox_nrm(ox_nrm(mk(P.x - s[0], P.y - s[1], P.z - s[2])));
+    } else {
+      const uint32_t tri = x.P->geom_first[h.geom] + h.prim;
+      const uint32_t* ix = &x.P->idx[size_t(tri) * 3];
+      const float* a = &x.P->pos[size_t(ix[0]) * 3];
+      const float* b = &x.P->pos[size_t(ix[1]) * 3];
+      const float* c = &x.P->pos[size_t(ix[2]) * 3];
+      const V3 v0 = mk(a[0], a[1], a[2]), v1 = mk(b[0], b[1], b[2]), v2 = mk(c[0], c[1], c[2]);
+      ng = ox_nrm(ox_nrm(ox_cross(v1 - v0, v2 - v0)));
+    }
+    {
+      const float l2 = dot(ng, ng);
+      ng = l2 > 0.0f ? ng * (1.0f / std::sqrt(l2)) : mk(0, 1, 0);
+    }
+    const std::vector<Material>& M = *x.mats;
+    uint32_t mid = x.P->geom_material[h.geom];
+    if (mid >= M.size()) mid = uint32_t(M.size() - 1);
+    const Material& m = M[mid];
+    const V3 base = mk(std::min(std::max(m.albedo.x, 0.0f), 1.0f), std::min(std::max(m.albedo.y, 0.0f), 1.0f),
+                       std::min(std::max(m.albedo.z, 0.0f), 1.0f));
+    const bool dielectric = m.type == 1;
+    const float omm = std::min(std::max(1.0f - m.metallic, 0.0f), 1.0f);
+    const V3 diffuse = base * omm;
+    if (depth + 1u >= x.max_depth) {
+      const V3 nvis = (ng + mk(1, 1, 1)) * 0.5f;
+      const V3 shd = diffuse * nvis;
+      acc = acc + mk(shd.x * thr.x, shd.y * thr.y, shd.z * thr.z);
+      return;
+    }
+    const bool entering = dot(d, ng) < 0.0f;
+    const V3 n = entering ? ng : -ng;
+    if (F.has_light) {
+      const V3 V = ox_nrm(-d);
+      const V3 L = ox_nrm(-F.light_dir);
+      const float NdotL = std::max(dot(n, L), 0.0f);
+      if (NdotL > 0.0f && !dielectric) {
+        V3 fr = mk(0, 0, 0);
+        if (m.metallic > 0.5f) {
+          const float r = std::min(std::max(m.roughness, 0.02f), 1.0f);
+          const float alpha = r * r;
+          const V3 H = ox_nrm(V + L);
+          const float cosNV = std::max(dot(n, V), 0.0f), cosNL = NdotL, cosVH = std::max(dot(V, H), 0.0f);
+          if (cosNV > 0.0f && cosNL > 0.0f) {
+            const float cosNH = std::max(dot(n, H), 0.0f);
+            const float a2 = alpha * alpha;
+            const float den = cosNH * cosNH * (a2 - 1.0f) + 1.0f;
+            const float D = a2 / (kPi * den * den);
+            const float G = ox_smith(cosNL, cosNV, alpha);
+            const V3 Fr = ox_fresnel(cosVH, base);
+            const float dn = std::max(4.0f * cosNV * cosNL, 1e-6f);
+            fr = Fr * ((D * G) / dn);
+          }
+        } else {
+          fr = diffuse * (1.0f / kPi);
+        }
+        acc = acc + ((thr * fr) * F.light_rad) * NdotL;
+      }
+    }
+    if (dielectric) {
+      const float xi = rand01(rng);
+      const float etaI = entering ? 1.0f : m.ior, etaT = entering ? m.ior : 1.0f;
+      const float eta = etaI / etaT;
+      const float cosI = std::min(std::max(-dot(d, n), -1.0f), 1.0f);
+      float R0 = (etaT - etaI) / (etaT + etaI);
+      R0 = R0 * R0;
+      const float mm = 1.0f - std::min(std::max(cosI, 0.0f), 1.0f);
+      const float Fr = R0 + (1.0f - R0) * (mm * mm * mm * mm * mm);
+      const float ci = std::min(std::max(-dot(n, d), -1.0f), 1.0f);
+      const float sin2T = eta * eta * std::max(0.0f, 1.0f - ci * ci);
+      const bool can = !(sin2T > 1.0f);
+      V3 refr = mk(0, 0, 0);
+      if (can) {
+        const float cosT = std::sqrt(std::max(0.0f, 1.0f - sin2T));
+        refr = d * eta + n * (eta * ci - cosT);
+        const float l2 = dot(refr, refr);
+        if (l2 > 0.0f) refr = refr * (1.0f / std::sqrt(l2));
+      }
+      V3 nd = (!can || xi < Fr) ? ox_reflect(d, n) : refr;
+      nd = ox_nrm(nd);
+      o = P + nd * 1e-3f;
+      d = nd;
+      continue;
+    }
+    if (m.metallic > 0.5f) {
+      const float r = std::min(std::max(m.roughness, 0.02f), 1.0f);
+      const float alpha = r * r;
+      const V3 V = ox_nrm(-d);
+      const float cosNV_raw = dot(n, V);
+      if (cosNV_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      const float u1 = rand01(rng), u2 = rand01(rng);
+      const float a2 = alpha * alpha;
+      const float phi = 6.28318530717958647692f * u1;
+      const float den = 1.0f + (a2 - 1.0f) * u2;
+      const float cosT = std::sqrt(std::max(0.0f, (1.0f - u2) / den));
+      const float sinT = std::sqrt(std::max(0.0f, 1.0f - cosT * cosT));
+      const float sp = std::sin(phi), cp = std::cos(phi);
+      V3 tb, bb;
+      ox_onb(n, tb, bb);
+      V3 H = tb * (sinT * cp) + bb * (sinT * sp) + n * cosT;
+      const float hl2 = dot(H, H);
+      H = hl2 > 0.0f ? H * (1.0f / std::sqrt(hl2)) : n;
+      const float cosNH_raw = dot(n, H);
+      if (cosNH_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      V3 L = ox_reflect(-V, H);
+      const float ll2 = dot(L, L);
+      L = ll2 > 0.0f ? L * (1.0f / std::sqrt(ll2)) : n;
+      const float cosNL_raw = dot(n, L);
+      if (cosNL_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      const float cosNV = std::max(cosNV_raw, 1e-6f), cosNL = std::max(cosNL_raw, 1e-6f), cosNH = std::max(cosNH_raw, 1e-6f);
+      const float cosVH = std::max(dot(V, H), 0.0f);
+      const V3 Fr = ox_fresnel(cosVH, base);
+      const float G = ox_smith(cosNL, cosNV, alpha);
+      float scale = (G * cosVH) / (cosNV * cosNH);
+      scale = std::min(scale, 50.0f);
+      if (scale < 0.0f) scale = 0.0f;
+      o = P + n * 1e-3f;
+      d = L;
+      thr = thr * (Fr * scale);
+      continue;
+    }
+    const float u1 = rand01(rng), u2 = rand01(rng);
+    const float rr = std::sqrt(u1);
+    const float phi = 2.0f * 3.14159265358979323846f * u2;
+    const float sp = std::sin(phi), cp = std::cos(phi);
+    const V3 loc = mk(rr * cp, rr * sp, std::sqrt(std::max(0.0f, 1.0f - u1)));
+    V3 tb, bb;
+    ox_onb(n, tb, bb);
+    d = ox_nrm(tb * loc.x + bb * loc.y + n * loc.z);
+    o = P + n * 1e-3f;
+    thr = thr * diffuse;
+  }
+}
+
 }  // namespace orc
 
 // ===================================================================================== C ABI
@@ -1373,6 +1569,114 @@ int oracle_render_pt(void* h, oracle_job* job, uint32_t samples_per_frame) {
   for (auto& th : pool) th.join();
   job->counters[0] = c_closest;
   job->counters[1] = c_shadow;
+  job->counters[2] = c_samples;
+  job->counters[3] = 0;
+  return 0;
+}
+
+// OptiX-mode render (the reference's OptiX wavefront programs, restated path per thread): per pixel
+// and frame one path from the pixel centre; accum.xyz += contributions, count += 1 per frame
+// (accum_w: width*height floats, read-modify-write); rgb = __raygen__resolve of accum / count.
+int oracle_render_optix(void* h, oracle_job* job, float* accum_w) {
+  const Prepared& P = *static_cast<Prepared*>(h);
+  std::vector<Material> mats(job->num_materials);
+  for (uint32_t i = 0; i < job->num_materials; ++i) {
+    const float* m = job->materials + i * 12;
+    mats[i] = Material{mk(m[0], m[1], m[2]), m[3], m[4], mk(m[5], m[6], m[7]), m[8], int(m[9])};
+  }
+  if (mats.empty()) return -1;
+  Ctx x;
+  x.P = &P;
+  x.mats = &mats;
+  x.lights = nullptr;
+  x.env.faces = job->env_faces;
+  x.env.size = job->env_size;
+  x.env.intensity = job->env_intensity;
+  x.env.max_clamp = job->env_clamp;
+  x.max_depth = job->max_depth;
+  x.bvh = job->use_bvh != 0;
+  const Camera cam = cam_from(job->cam);
+  // OptixBackend::render camera basis (OptixBackend.cpp:1515-1620)
+  OxFrame F;
+  {
+    const V3 fwd = normalize(cam.fwd), right = normalize(cam.right), up = normalize(cam.up);
+    const V3 dx = ray_dir(cam, 1.0f, 0.5f), dy = ray_dir(cam, 0.5f, 0.0f);
+    const float den_x = dot(dx, fwd), den_y = dot(dy, fwd);
+    const float hw = den_x != 0.0f ? dot(dx, right) / den_x : 0.0f;
+    const float hh = den_y != 0.0f ? dot(dy, up) / den_y : 0.0f;
+    F.u = right * hw;
+    F.v = up * hh;
+    F.w = fwd;
+    F.has_light = false;
+    F.light_dir = mk(0, -1, 0);
+    F.light_rad = mk(0, 0, 0);
+    for (uint32_t i = 0; i < job->num_lights; ++i) {
+      const float* l = job->lights + i * 8;
+      if (int(l[0]) != 0) continue;
+      const V3 to_light = normalize(-mk(l[1], l[2], l[3]));  // DirectionalLight stores normalize(-d)
+      F.light_dir = -to_light;
+      F.light_rad = mk(l[4], l[5], l[6]) * l[7];
+      F.has_light = true;
+      break;
+    }
+  }
+  const int W = job->width, H = job->height, TS = 32;
+  const int ntx = (W + TS - 1) / TS, nty = (H + TS - 1) / TS, ntiles = ntx * nty;
+  const int G = job->shard_count > 0 ? job->shard_count : 1, R = job->shard_rank;
+  std::atomic<int> next{0};
+  std::atomic<uint64_t> c_closest{0}, c_samples{0};
+  auto worker = [&]() {
+    Counters cnt;
+    for (;;) {
+      const int t = next.fetch_add(1);
+      if (t >= ntiles) break;
+      if (t % G != R) continue;
+      const int tx = t % ntx, ty = t / ntx;
+      const int x0 = tx * TS, y0 = ty * TS, x1 = std::min(x0 + TS, W), y1 = std::min(y0 + TS, H);
+      for (int y = y0; y < y1; ++y)
+        for (int xx = x0; xx < x1; ++xx) {
+          const uint32_t pixel = uint32_t(y * W + xx);
+          float* acc = job->accum + size_t(pixel) * 3;
+          V3 a = mk(acc[0], acc[1], acc[2]);
+          float wcnt = accum_w[pixel];
+          const float ndx = ((float(xx) + 0.5f) / float(W)) * 2.0f - 1.0f;
+          const float ndy = 1.0f - ((float(y) + 0.5f) / float(H)) * 2.0f;
+          const V3 dir = ox_nrm((F.u * ndx + F.v * ndy) + F.w);
+          for (uint32_t f = 0; f < job->num_frames; ++f) {
+            const uint32_t frame = job->frame_begin + f - 1u;
+            const uint32_t rng = wang_hash((pixel + 1u) ^ (frame * 9781u + 1u));
+            ox_path(x, F, cam.pos, dir, rng, a, cnt);
+            wcnt = wcnt + 1.0f;
+            ++cnt.samples;
+          }
+          acc[0] = a.x; acc[1] = a.y; acc[2] = a.z;
+          accum_w[pixel] = wcnt;
+          if (job->rgb) {  // __raygen__resolve
+            const float inv = (wcnt > 0.0f) ? (1.0f / wcnt) : 0.0f;
+            V3 c = mk(std::max(a.x * inv, 0.0f), std::max(a.y * inv, 0.0f), std::max(a.z * inv, 0.0f));
+            c = c * 2.2f;
+            c = mk(c.x / (1.0f + c.x), c.y / (1.0f + c.y), c.z / (1.0f + c.z));
+            const float g = 1.0f / 2.2f;
+            c = mk(std::pow(c.x, g), std::pow(c.y, g), std::pow(c.z, g));
+            c = gclamp(c, 0.0f, 1.0f);
+            uint8_t* o = job->rgb + size_t(pixel) * 3;
+            o[0] = static_cast<unsigned char>(c.x * 255.0f);
+            o[1] = static_cast<unsigned char>(c.y * 255.0f);
+            o[2] = static_cast<unsigned char>(c.z * 255.0f);
+          }
+        }
+    }
+    c_closest += cnt.closest;
+    c_samples += cnt.samples;
+  };
+  int nt = job->threads > 0 ? job->threads : int(std::thread::hardware_concurrency());
+  if (nt < 1) nt = 1;
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nt; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  job->counters[0] = c_closest;
+  job->counters[1] = 0;
   job->counters[2] = c_samples;
   job->counters[3] = 0;
   return 0;

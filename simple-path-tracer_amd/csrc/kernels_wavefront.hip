@@ -1348,13 +1348,29 @@ __device__ __forceinline__ uint32_t resolve_rgba_pt(vec3 acc, uint32_t n) {
   return pack_rgba(clamp_g(acc / float(n), 0.0f, 1.0f));
 }
 
+// OptiX __raygen__resolve (device_programs.cu:854-899): accum / w (by reciprocal) -> exposure 2.2
+// -> Reinhard -> gamma 2.2 -> clamp -> 8 bit
+__device__ __forceinline__ uint32_t resolve_rgba_optix(float4 a) {
+  const float inv = (a.w > 0.0f) ? (1.0f / a.w) : 0.0f;
+  vec3 c = v3(fmaxf(a.x * inv, 0.0f), fmaxf(a.y * inv, 0.0f), fmaxf(a.z * inv, 0.0f));
+  c = c * 2.2f;
+  c = v3(c.x / (1.0f + c.x), c.y / (1.0f + c.y), c.z / (1.0f + c.z));
+  const float g = 1.0f / 2.2f;
+  c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
+  return pack_rgba(v3(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f)));
+}
+
 __global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n, uint32_t* tiles,
                                                     uint8_t* image) {
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     int x, y;
     const bool valid = local_pixel(f, l, x, y);
     uint32_t px = 0u;
-    if (valid) px = f.integrator == SPTR_INTEGRATOR_PATHTRACER ? resolve_rgba_pt(xyz(accum[l]), n) : resolve_rgba(xyz(accum[l]), n);
+    if (valid) {
+      if (f.integrator == SPTR_INTEGRATOR_PATHTRACER) px = resolve_rgba_pt(xyz(accum[l]), n);
+      else if (f.integrator == SPTR_INTEGRATOR_OPTIX) px = resolve_rgba_optix(accum[l]);
+      else px = resolve_rgba(xyz(accum[l]), n);
+    }
     tiles[l] = px;
     if (valid && image) {
       uint8_t* o = image + ((size_t)y * f.W + x) * 3;
@@ -1549,6 +1565,258 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneVie
     atomicAdd(&w.tot[kTotClosest], a);
     atomicAdd(&w.tot[kTotShadow], b);
   }
+  report_stack(vc, w.tot);
+}
+
+// --------------------------------------------------------------------------------- k_optix
+// SPTR_INTEGRATOR_OPTIX: the shading of the reference's OptiX wavefront programs
+// (src/optix/device_programs.cu), restated path per thread — one path per pixel per frame, its
+// contributions added to accum in bounce order (the same order the reference's per-bounce
+// atomicAdds take for a pixel, since a pixel has one path per frame):
+//   raygen  computePrimaryRay / __raygen__gen_primary (:220-274): pixel centre, cam_u/v/w from
+//           OptixBackend::render (OptixBackend.cpp:1609-1620), seed wang_hash((pixel+1) ^ (frame*9781+1))
+//   trace   tmin 1e-3, tmax 1e16 (:297-309); closest-hit Ng = normalize(cross(v1-v0, v2-v0)) or
+//           normalize(P - C) (:761-820)
+//   shade   (:315-690) miss -> sky (w += 1); depth cap -> normal visualisation (w += 1); direct sun
+//           light without a shadow ray (GGX spec for metals, Lambert otherwise, none for
+//           dielectrics); delta dielectric; GGX-sampled metal with its fallbacks; cosine diffuse
+// The environment is the procedural sky (or the CPU cubemap sampling when a cubemap is set: the
+// reference's equirect texture fetch is not restated).  CUDA's approximate rsqrtf / sincosf /
+// __powf-class functions are replaced by correctly rounded normalize and the library sin/cos/pow.
+__device__ __forceinline__ vec3 ox_nrm(vec3 v) {  // f3_normalize (rsqrtf -> correctly rounded)
+  return v * inv_len(dot(v, v));
+}
+__device__ __forceinline__ void ox_onb(vec3 n, vec3& t, vec3& b) {  // make_onb (:213-218)
+  const vec3 up = (fabsf(n.z) < 0.999f) ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, 0.0f);
+  t = ox_nrm(v3(up.y * n.z - up.z * n.y, up.z * n.x - up.x * n.z, up.x * n.y - up.y * n.x));
+  b = v3(n.y * t.z - n.z * t.y, n.z * t.x - n.x * t.z, n.x * t.y - n.y * t.x);
+}
+__device__ __forceinline__ vec3 ox_cross(vec3 a, vec3 b) {  // f3_cross
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ vec3 ox_reflect(vec3 v, vec3 n) { return v + n * (-2.0f * dot(v, n)); }  // f3_reflect
+__device__ __forceinline__ vec3 ox_fresnel(float cosVH, vec3 F0) {  // fresnelSchlick (:170-176)
+  const float m = 1.0f - fminf(fmaxf(cosVH, 0.0f), 1.0f);
+  const float m2 = m * m;
+  const float m5 = m2 * m2 * m;
+  return F0 + v3(1.0f - F0.x, 1.0f - F0.y, 1.0f - F0.z) * m5;
+}
+__device__ __forceinline__ float ox_smith(float cosNL, float cosNV, float alpha) {  // smithGGX (:162-168)
+  const float a = alpha + 1.0f;
+  const float k = (a * a) * 0.125f;
+  return (cosNL / (cosNL * (1.0f - k) + k)) * (cosNV / (cosNV * (1.0f - k) + k));
+}
+__device__ __forceinline__ vec3 ox_fallback_reflect(vec3 d, vec3 n) {
+  vec3 R = ox_reflect(d, n);
+  const float l2 = dot(R, R);
+  return l2 > 0.0f ? R * inv_len(l2) : n;
+}
+
+template <bool kW4, bool kCube>
+__device__ void ox_path(const Staged& sc, const SceneView& sv, const ShadeView& sh, const DevMaterial* smat, uint32_t nm,
+                        const FrameView& f, vec3 o, vec3 d, uint32_t rng, vec3& acc, Visits& vc, LdsStack& ls,
+                        uint32_t& n_closest) {
+  constexpr float kPi = 3.14159265358979323846f;
+  vec3 thr = v3(1.0f, 1.0f, 1.0f);
+  for (uint32_t depth = 0; depth < f.max_depth; ++depth) {
+    ++n_closest;
+    float t = 1e16f;
+    uint32_t ref = kNoHit;
+    if (!traverse_w<kW4, false, false>(sc, sv, make_ray(o, d), 1e-3f, t, ref, vc, ls)) {
+      const vec3 c = env_color<kCube>(sh.env, ox_nrm(d));
+      acc = acc + v3(c.x * thr.x, c.y * thr.y, c.z * thr.z);
+      return;
+    }
+    const vec3 P = o + d * t;
+    const uint32_t idx = ref & kIndexMask;
+    vec3 ng;
+    uint32_t gid;
+    if (ref & kSphereBit) {
+      const float4 c = sc.sph[idx];
+      ng = ox_nrm(ox_nrm(v3(P.x - c.x, P.y - c.y, P.z - c.z)));
+      gid = sv.sph_geom[idx];
+    } else {
+      const float4 a = sc.tris[3 * idx + 0], b = sc.tris[3 * idx + 1], c = sc.tris[3 * idx + 2];
+      const vec3 e1 = -v3(a.w, b.x, b.y), e2 = v3(b.z, b.w, c.x);  // v1 - v0, v2 - v0 (stored e1 = v0 - v1)
+      ng = ox_nrm(ox_nrm(ox_cross(e1, e2)));
+      gid = sv.tri_geom[idx];
+    }
+    {  // the shade program renormalises the hit record's normal, (0, 1, 0) if degenerate (:424-433, :443-449)
+      const float l2 = dot(ng, ng);
+      ng = l2 > 0.0f ? ng * inv_len(l2) : v3(0.0f, 1.0f, 0.0f);
+    }
+    // material: clamp the id into the table, baseColor clamped to [0, 1] (:343-357)
+    uint32_t mid = sh.geom_mat[gid];
+    if (mid >= sh.num_mats) mid = sh.num_mats - 1u;
+    const DevMaterial& m = (mid < nm) ? smat[mid] : sh.mats[mid];
+    const vec3 base = v3(fminf(fmaxf(m.albedo[0], 0.0f), 1.0f), fminf(fmaxf(m.albedo[1], 0.0f), 1.0f),
+                         fminf(fmaxf(m.albedo[2], 0.0f), 1.0f));
+    const float metallic = m.metallic, rough = m.roughness, ior = m.ior;
+    const bool dielectric = m.type == 1;
+    const float omm = fminf(fmaxf(1.0f - metallic, 0.0f), 1.0f);
+    const vec3 diffuse = base * omm;
+    if (depth + 1u >= f.max_depth) {  // depth cap: normal visualisation (:424-440)
+      const vec3 nvis = (ng + v3(1.0f, 1.0f, 1.0f)) * 0.5f;
+      const vec3 shd = diffuse * nvis;
+      acc = acc + v3(shd.x * thr.x, shd.y * thr.y, shd.z * thr.z);
+      return;
+    }
+    const bool entering = dot(d, ng) < 0.0f;
+    const vec3 n = entering ? ng : -ng;
+    if (f.ox_has_light) {  // direct light, no shadow ray (:457-496)
+      const vec3 V = ox_nrm(-d);
+      const vec3 L = ox_nrm(-f.ox_light_dir);
+      const float NdotL = fmaxf(dot(n, L), 0.0f);
+      if (NdotL > 0.0f && !dielectric) {
+        vec3 fr = v3(0.0f, 0.0f, 0.0f);
+        if (metallic > 0.5f) {
+          const float r = fminf(fmaxf(rough, 0.02f), 1.0f);
+          const float alpha = r * r;
+          const vec3 H = ox_nrm(V + L);
+          const float cosNV = fmaxf(dot(n, V), 0.0f), cosNL = NdotL, cosVH = fmaxf(dot(V, H), 0.0f);
+          if (cosNV > 0.0f && cosNL > 0.0f) {
+            const float cosNH = fmaxf(dot(n, H), 0.0f);
+            const float a2 = alpha * alpha;
+            const float den = cosNH * cosNH * (a2 - 1.0f) + 1.0f;
+            const float D = a2 / (kPi * den * den);
+            const float G = ox_smith(cosNL, cosNV, alpha);
+            const vec3 F = ox_fresnel(cosVH, base);
+            const float dn = fmaxf(4.0f * cosNV * cosNL, 1e-6f);
+            fr = F * ((D * G) / dn);
+          }
+        } else {
+          fr = diffuse * (1.0f / kPi);
+        }
+        const vec3 Li = f.ox_light_rad;
+        acc = acc + ((thr * fr) * Li) * NdotL;
+      }
+    }
+    if (dielectric) {  // delta dielectric (:499-543)
+      const float xi = rand01(rng);
+      const float etaI = entering ? 1.0f : ior, etaT = entering ? ior : 1.0f;
+      const float eta = etaI / etaT;
+      const float cosI = fminf(fmaxf(-dot(d, n), -1.0f), 1.0f);
+      float R0 = (etaT - etaI) / (etaT + etaI);
+      R0 = R0 * R0;
+      const float mm = 1.0f - fminf(fmaxf(cosI, 0.0f), 1.0f);
+      const float Fr = R0 + (1.0f - R0) * (mm * mm * mm * mm * mm);
+      // f3_refract (:75-93)
+      const float ci = fminf(fmaxf(-dot(n, d), -1.0f), 1.0f);
+      const float sin2T = eta * eta * fmaxf(0.0f, 1.0f - ci * ci);
+      const bool can = !(sin2T > 1.0f);
+      vec3 refr = v3(0.0f, 0.0f, 0.0f);
+      if (can) {
+        const float cosT = sqrtf(fmaxf(0.0f, 1.0f - sin2T));
+        refr = d * eta + n * (eta * ci - cosT);
+        const float l2 = dot(refr, refr);
+        if (l2 > 0.0f) refr = refr * inv_len(l2);
+      }
+      vec3 nd = (!can || xi < Fr) ? ox_reflect(d, n) : refr;
+      nd = ox_nrm(nd);
+      o = P + nd * 1e-3f;
+      d = nd;
+      continue;
+    }
+    if (metallic > 0.5f) {  // GGX-sampled metal (:547-666)
+      const float r = fminf(fmaxf(rough, 0.02f), 1.0f);
+      const float alpha = r * r;
+      const vec3 V = ox_nrm(-d);
+      const float cosNV_raw = dot(n, V);
+      if (cosNV_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      const float u1 = rand01(rng), u2 = rand01(rng);
+      // ggx_sample_half_vector (:178-210)
+      const float a2 = alpha * alpha;
+      const float phi = 6.28318530717958647692f * u1;
+      const float den = 1.0f + (a2 - 1.0f) * u2;
+      const float cosT = sqrtf(fmaxf(0.0f, (1.0f - u2) / den));
+      const float sinT = sqrtf(fmaxf(0.0f, 1.0f - cosT * cosT));
+      const float sp = sinf(phi), cp = cosf(phi);
+      vec3 tb, bb;
+      ox_onb(n, tb, bb);
+      vec3 H = tb * (sinT * cp) + bb * (sinT * sp) + n * cosT;
+      const float hl2 = dot(H, H);
+      H = hl2 > 0.0f ? H * inv_len(hl2) : n;
+      const float cosNH_raw = dot(n, H);
+      if (cosNH_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      vec3 L = ox_reflect(-V, H);
+      const float ll2 = dot(L, L);
+      L = ll2 > 0.0f ? L * inv_len(ll2) : n;
+      const float cosNL_raw = dot(n, L);
+      if (cosNL_raw <= 0.0f) {
+        d = ox_fallback_reflect(d, n);
+        o = P + n * 1e-3f;
+        thr = thr * base;
+        continue;
+      }
+      const float cosNV = fmaxf(cosNV_raw, 1e-6f), cosNL = fmaxf(cosNL_raw, 1e-6f), cosNH = fmaxf(cosNH_raw, 1e-6f);
+      const float cosVH = fmaxf(dot(V, H), 0.0f);
+      const vec3 F = ox_fresnel(cosVH, base);
+      const float G = ox_smith(cosNL, cosNV, alpha);
+      float scale = (G * cosVH) / (cosNV * cosNH);
+      scale = fminf(scale, 50.0f);
+      if (scale < 0.0f) scale = 0.0f;
+      o = P + n * 1e-3f;
+      d = L;
+      thr = thr * (F * scale);
+      continue;
+    }
+    // Lambert, cosine-weighted (:668-689)
+    const float u1 = rand01(rng), u2 = rand01(rng);
+    const float rr = sqrtf(u1);
+    const float phi = 2.0f * 3.14159265358979323846f * u2;
+    const float sp = sinf(phi), cp = cosf(phi);
+    const vec3 loc = v3(rr * cp, rr * sp, sqrtf(fmaxf(0.0f, 1.0f - u1)));
+    vec3 tb, bb;
+    ox_onb(n, tb, bb);
+    d = ox_nrm(tb * loc.x + bb * loc.y + n * loc.z);
+    o = P + n * 1e-3f;
+    thr = thr * diffuse;
+  }
+}
+
+template <bool kLds, bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView f, WaveView w) {
+  __shared__ LdsStack s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ DevMaterial smat[32];
+  const uint32_t nm = stage_materials(sh, smat);
+  const Staged sc = stage_scene<kLds>(sv, lds);
+  __syncthreads();
+  const ImageDiv idiv = image_div(f);
+  Visits vc;
+  uint32_t n_closest = 0u;
+  const Sched sd = block_sched(f.P);
+  for (uint32_t l = sd.first + threadIdx.x; l < f.P; l += sd.step) {
+    int x = 0, y = 0;
+    if (!local_pixel(f, l, x, y)) continue;
+    const uint32_t pixel = (uint32_t)(y * f.W + x);
+    // computePrimaryRay (:220-234)
+    const float ndx = div_nrm(float(x) + 0.5f, idiv.w) * 2.0f - 1.0f;
+    const float ndy = 1.0f - div_nrm(float(y) + 0.5f, idiv.h) * 2.0f;
+    const vec3 dir = ox_nrm((f.ox_u * ndx + f.ox_v * ndy) + f.ox_w);
+    float4 a4 = f.reset ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : f.accum[l];
+    vec3 acc = xyz(a4);
+    for (uint32_t fr = 0; fr < f.k; ++fr) {
+      const uint32_t frame = f.acc0 + fr - 1u;  // OptixBackend's frame_index_ (0 after a reset)
+      const uint32_t rng = wang_hash((pixel + 1u) ^ (frame * 9781u + 1u));
+      ox_path<kW4, kCube>(sc, sv, sh, smat, nm, f, f.cam_pos, dir, rng, acc, vc, s_stack, n_closest);
+      a4.w = a4.w + 1.0f;
+    }
+    f.accum[l] = make_float4(acc.x, acc.y, acc.z, a4.w);
+  }
+  unsigned long long a = n_closest;
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+  if (lane_id() == 0u) atomicAdd(&w.tot[kTotClosest], a);
   report_stack(vc, w.tot);
 }
 
@@ -1833,6 +2101,21 @@ void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView
           const unsigned g = std::min<unsigned>(resident_grid((const void*)&k_pathtracer<Lc, Wc, Cube>, lb),
                                                 (unsigned)((f.P + kBlock - 1) / kBlock));
           hipLaunchKernelGGL((k_pathtracer<Lc, Wc, Cube>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
+}
+
+void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {
+  const bool L = sv.lds_bytes != 0;
+  const unsigned lb = L ? sv.lds_bytes : 16u;
+  dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
+          const unsigned g = std::min<unsigned>(resident_grid((const void*)&k_optix<Lc, Wc, Cube>, lb),
+                                                (unsigned)((f.P + kBlock - 1) / kBlock));
+          hipLaunchKernelGGL((k_optix<Lc, Wc, Cube>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w);
           return g;
         }(fl);
       },

@@ -340,15 +340,50 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   return SPTR_OK;
 }
 
-// PathTracer-mode render call (SPTR_INTEGRATOR_PATHTRACER): path-per-thread frames, no wavefront
-// streams.  Frames are launched kPtFramesPerLaunch at a time (bounded launch length); the
-// accumulation order is the frame order either way.
+// OptiX-compatible camera and light (OptixBackend::render, src/backends/OptixBackend.cpp:1515-1620):
+// cam_u / cam_v scaled from Camera::getRayDirection at the image edges, the first directional light
+// as direction FROM the light and colour * intensity.  Host float arithmetic in the reference's order.
+void optix_frame_params(const Context& c, const sptr_frame& f, FrameView& v) {
+  const sptr_camera& k = f.camera;
+  const vec3 fwd = normalize(v3(k.forward[0], k.forward[1], k.forward[2]));
+  const vec3 right = normalize(v3(k.right[0], k.right[1], k.right[2]));
+  const vec3 up = normalize(v3(k.up[0], k.up[1], k.up[2]));
+  const vec3 cf = v3(k.forward[0], k.forward[1], k.forward[2]), cr = v3(k.right[0], k.right[1], k.right[2]),
+             cu = v3(k.up[0], k.up[1], k.up[2]);
+  auto ray_dir = [&](float u, float vv) {  // Camera::getRayDirection (Camera.cpp:95-106)
+    const float nx = (u - 0.5f) * 2.0f, ny = -(vv - 0.5f) * 2.0f;
+    return normalize(cf + nx * k.half_width * cr + ny * k.half_height * cu);
+  };
+  const vec3 dx = ray_dir(1.0f, 0.5f), dy = ray_dir(0.5f, 0.0f);
+  const float den_x = dot(dx, fwd), den_y = dot(dy, fwd);
+  const float hw = den_x != 0.0f ? dot(dx, right) / den_x : 0.0f;
+  const float hh = den_y != 0.0f ? dot(dy, up) / den_y : 0.0f;
+  v.ox_u = right * hw;
+  v.ox_v = up * hh;
+  v.ox_w = fwd;
+  v.ox_has_light = 0u;
+  v.ox_light_dir = v3(0.0f, -1.0f, 0.0f);
+  v.ox_light_rad = v3(0.0f, 0.0f, 0.0f);
+  for (const DevLight& l : c.lights_host)
+    if (l.type == 0) {  // DevLight keeps the direction TO the light
+      v.ox_light_dir = -v3(l.v[0], l.v[1], l.v[2]);
+      v.ox_light_rad = v3(l.radiance[0], l.radiance[1], l.radiance[2]);
+      v.ox_has_light = 1u;
+      break;
+    }
+}
+
+// Path-per-thread render calls (SPTR_INTEGRATOR_PATHTRACER / _OPTIX): no wavefront streams.
+// Frames are launched kPtFramesPerLaunch at a time (bounded launch length); the accumulation order
+// is the frame order either way.
 constexpr uint32_t kPtFramesPerLaunch = 4;
 int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s, sptr_stats* stats) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
   WaveView w = wave_view(c);
   FrameView fv = frame_view(c, f);
+  const bool optix = f.integrator == SPTR_INTEGRATOR_OPTIX;
+  if (optix) optix_frame_params(c, f, fv);
   const bool timing = (f.flags & (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE)) != 0;
   StageTimer tm{c, timing, false, s};
   if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
@@ -359,7 +394,8 @@ int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s
     fv.acc0 = f.frame_begin + done;
     fv.reset = (reset && done == 0) ? 1u : 0u;
     tm.begin(7);
-    launch_pathtracer(sv, sh, fv, w, s);
+    if (optix) launch_optix(sv, sh, fv, w, s);
+    else launch_pathtracer(sv, sh, fv, w, s);
     tm.end();
     done += fv.k;
     ++launches;
@@ -377,7 +413,7 @@ int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s
   c.last_samples = total;
   ++c.pending;
   c.pending_stream = s;
-  c.pending_samples += (uint64_t)fv.valid * f.spp * fv.spf;
+  c.pending_samples += (uint64_t)fv.valid * f.spp * (optix ? 1u : fv.spf);
   c.pending_waves += launches;
   if (f.flags & SPTR_FRAME_ASYNC) {
     if (stats) std::memset(stats, 0, sizeof(*stats));
@@ -608,7 +644,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   if (f->width <= 0 || f->height <= 0 || f->spp == 0 || f->max_depth == 0 || f->max_depth > (uint32_t)kMaxDepth ||
       f->frame_begin == 0)
     return fail(c, SPTR_ERR_INVALID, "render: bad frame parameters");
-  if (f->integrator > SPTR_INTEGRATOR_PATHTRACER) return fail(c, SPTR_ERR_INVALID, "render: unknown integrator");
+  if (f->integrator > SPTR_INTEGRATOR_OPTIX) return fail(c, SPTR_ERR_INVALID, "render: unknown integrator");
   if (f->integrator == SPTR_INTEGRATOR_PATHTRACER && f->samples_per_frame > 4096)
     return fail(c, SPTR_ERR_INVALID, "render: samples_per_frame above 4096");
   const int G = f->shard_count > 0 ? f->shard_count : 1, R = f->shard_count > 0 ? f->shard_rank : 0;
@@ -625,7 +661,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const bool reset = f->frame_begin == 1;
   if (!reset && f->frame_begin != c.last_samples + 1)
     return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
-  if (f->integrator == SPTR_INTEGRATOR_PATHTRACER) return render_pathtracer(c, *f, reset, s, stats);
+  if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) return render_pathtracer(c, *f, reset, s, stats);
   uint64_t wave_paths = c.wave_paths;
   if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
     wave_paths = kDefaultWavePaths;

@@ -130,6 +130,9 @@ struct FrameView {
   uint32_t pixel_major;  // kFold*: bounce 0 folds each pixel's leading misses into accum (bounce0_pixel_major)
   uint32_t integrator;   // sptr_integrator
   uint32_t spf;          // PathTracer mode: samples per frame
+  vec3 ox_u, ox_v, ox_w; // OptiX mode: LaunchParams cam_u / cam_v / cam_w (OptixBackend.cpp:1609-1620)
+  vec3 ox_light_dir, ox_light_rad;  // OptiX mode: first directional light (direction FROM the light)
+  uint32_t ox_has_light;
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -259,6 +262,9 @@ void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_
                     hipStream_t s);
 // PathTracer-mode frames (the k frames of f from f.acc0), one launch: accum += tonemapped frames.
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
+// OptiX-compatible frames (the k frames of f from f.acc0), one launch: accum.xyz += contributions,
+// accum.w += samples.
+void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
                    hipStream_t s);
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,

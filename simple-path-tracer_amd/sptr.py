@@ -26,6 +26,7 @@ SPTR_FRAME_TIMING_TRACE = 16
 
 SPTR_INTEGRATOR_WAVEFRONT = 0   # WavefrontPathTracerCPU semantics (default)
 SPTR_INTEGRATOR_PATHTRACER = 1  # PathTracer (the reference's default CPU integrator) semantics
+SPTR_INTEGRATOR_OPTIX = 2       # the reference's OptiX device-program shading (GPU 'G' path)
 
 
 class SptrError(RuntimeError):

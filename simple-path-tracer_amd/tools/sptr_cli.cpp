@@ -4,7 +4,7 @@
 // one render() per frame, progressive accumulation.
 //   sptr_cli [--scene default|default_emitter|test_triangle|sphere_mesh:STACKS:SLICES|gltf:PATH]
 //            [--w 800] [--h 600] [--spp 4] [--depth 6] [--env sky|FILE.hdr] [--out image.ppm]
-//            [--warmup N] [--json] [--integrator wavefront|pathtracer] [--spf 4]
+//            [--warmup N] [--json] [--integrator wavefront|pathtracer|optix] [--spf 4]
 // --spp N renders N progressive frames of 1 spp each (GLRenderer's m_accumulated_samples loop);
 // --warmup N renders N untimed frames first (then restarts the accumulation by a camera change);
 // --json prints one line with per-frame wall-clock statistics (render + RGB8 read back, as the
@@ -85,6 +85,7 @@ int main(int argc, char** argv) {
   backends::HipBackend::Settings st;
   st.max_depth = uint32_t(depth);
   if (integrator == "pathtracer") st.integrator = SPTR_INTEGRATOR_PATHTRACER;
+  else if (integrator == "optix") st.integrator = SPTR_INTEGRATOR_OPTIX;
   else if (integrator != "wavefront") {
     std::fprintf(stderr, "unknown integrator %s\n", integrator.c_str());
     return 2;
