@@ -185,6 +185,11 @@ int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 2 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
+/* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
+ * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
+ * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument;
+ * 1: direct kernel launches for every call.  Results are identical either way. */
+int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
 /* Traversal width: 2 (the LBVH as built), 4 (collapsed to 128-B BVH4 nodes), or 0 = automatic (the
  * default: 2 for scenes staged in LDS, 4 otherwise). */
 int sptr_set_bvh_width(sptr_ctx* ctx, uint32_t width);

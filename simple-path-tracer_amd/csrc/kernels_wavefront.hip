@@ -165,6 +165,25 @@ __device__ __forceinline__ bool local_pixel(const FrameView& f, uint32_t l, int&
   return x < f.W && y < f.H;
 }
 
+// Per-call values that a captured launch graph must not bake in (sptr_api.cpp run_graph): the call's
+// first accumulation index and whether it restarts the accumulation, written by k_frame_dyn at the
+// head of every render call; the FrameView carries the batch's offset in acc0 and a candidate reset
+// flag (1 for the call's first batch).  f.dyn == null (query kernels): acc0 / reset are absolute.
+__device__ __forceinline__ FrameView frame_dyn(FrameView f) {
+  if (f.dyn) {
+    f.acc0 = f.dyn[0] + f.acc0;
+    f.reset = f.reset & f.dyn[1];
+  }
+  return f;
+}
+__global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total) {
+  if (threadIdx.x == 0) {
+    dyn[0] = frame_begin;
+    dyn[1] = reset;
+    dyn[2] = total;
+  }
+}
+
 // Camera::getRayDirection
 __device__ __forceinline__ vec3 camera_dir(const FrameView& f, float u, float v) {
   const float nx = (u - 0.5f) * 2.0f;
@@ -656,7 +675,8 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // its registers are allocated for this loop alone.
 template <bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
-    k_trace_pm(SceneView sv, EnvView sh, FrameView f, WaveView w) {
+    k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
+  const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
@@ -729,7 +749,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 template <bool kLds, bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
-    k_trace_wp(SceneView sv, EnvView sh, FrameView f, WaveView w) {
+    k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
+  const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
@@ -804,7 +825,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
 // rs[depth&1] written by the previous k_shade, addressed through its segment table.
 template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
-    k_trace(SceneView sv, EnvView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
+    k_trace(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
@@ -1030,7 +1052,8 @@ __device__ __forceinline__ uint32_t stage_materials(const ShadeView& sh, DevMate
 // point light is present).
 template <bool kPrimary>
 __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
-    k_shade(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth, uint32_t nseg_in) {
+    k_shade(SceneView sv, ShadeView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  const FrameView f = frame_dyn(fin);
   extern __shared__ uint32_t s_off[];
   __shared__ DevMaterial smat[32];
   __shared__ uint32_t s_cnt_n, s_cnt_s;
@@ -1279,7 +1302,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
 // accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
 // batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
 // slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
-__global__ void __launch_bounds__(kBlock) k_accum(FrameView f, WaveView w, float4* accum) {
+__global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, float4* accum) {
+  const FrameView f = frame_dyn(fin);
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     uint32_t s0 = 0u;
     vec3 a = v3(0.0f, 0.0f, 0.0f);
@@ -1360,8 +1384,9 @@ __device__ __forceinline__ uint32_t resolve_rgba_optix(float4 a) {
   return pack_rgba(v3(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f)));
 }
 
-__global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n, uint32_t* tiles,
+__global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n_arg, uint32_t* tiles,
                                                     uint8_t* image) {
+  const uint32_t n = f.dyn ? f.dyn[2] : n_arg;  // total frames of the accumulation
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     int x, y;
     const bool valid = local_pixel(f, l, x, y);
@@ -1522,7 +1547,8 @@ __device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 // += the frame's tonemapped colour (the reference's accumulation_buffer, GLRenderer's
 // m_accumulated_samples frames).
 template <bool kLds, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView f, WaveView w) {
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
+  const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
@@ -1785,7 +1811,8 @@ __device__ void ox_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 }
 
 template <bool kLds, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView f, WaveView w) {
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
+  const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
@@ -2121,6 +2148,11 @@ void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
       },
       Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
 }
+
+void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total);
+}
+const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s) {
   hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum);

@@ -110,6 +110,7 @@ int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_sl
   const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * 16;
   const bool grow = c.w_hrec.bytes < hrec_bytes || !(c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p);
   if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
+  if (grow) ++c.epoch;
   API_HIP(ensure_buf(c.w_hrec, hrec_bytes));
   if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
   // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
@@ -195,6 +196,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.accum = static_cast<float4*>(c.accum.p);
   v.reset = 0;
   v.pixel_major = 0;
+  v.dyn = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -229,7 +231,7 @@ struct StageTimer {
   hipError_t err = hipSuccess;
   size_t open = SIZE_MAX;   // index in c.marks of the stage being recorded
   size_t call = SIZE_MAX;   // index in c.marks of this call's stage-0 span
-  size_t next() {
+  size_t alloc() {  // a pool event for this call (not recorded)
     if (c.events_used == c.events.size()) {
       hipEvent_t e = nullptr;
       const hipError_t r = hipEventCreate(&e);
@@ -239,8 +241,13 @@ struct StageTimer {
       }
       c.events.push_back(e);
     }
-    const size_t i = c.events_used++;
-    if (err == hipSuccess) err = hipEventRecord(c.events[i], s);
+    return c.events_used++;
+  }
+  bool capturing = false;  // inside a graph capture: record as external event nodes (run_call)
+  size_t next() {
+    const size_t i = alloc();
+    if (i != SIZE_MAX && err == hipSuccess)
+      err = capturing ? hipEventRecordWithFlags(c.events[i], s, hipEventRecordExternal) : hipEventRecord(c.events[i], s);
     return i;
   }
   void begin(int stage) {
@@ -332,6 +339,7 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   API_HIP(ensure_buf(c.accum, (size_t)c.P * 16));
   API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
   API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
+  ++c.epoch;
   API_HIP(hipMemsetAsync(c.accum.p, 0, (size_t)c.P * 16, s));
   API_HIP(hipMemsetAsync(c.tiles.p, 0, (size_t)c.P * 4, s));
   API_HIP(hipMemsetAsync(c.image.p, 0, (size_t)W * H * 3, s));
@@ -377,22 +385,21 @@ void optix_frame_params(const Context& c, const sptr_frame& f, FrameView& v) {
 // Frames are launched kPtFramesPerLaunch at a time (bounded launch length); the accumulation order
 // is the frame order either way.
 constexpr uint32_t kPtFramesPerLaunch = 4;
-int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s, sptr_stats* stats) {
+// Launch sequence of a path-per-thread call on stream s (timer tm on s); returns the launch count.
+uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
   WaveView w = wave_view(c);
   FrameView fv = frame_view(c, f);
+  fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool optix = f.integrator == SPTR_INTEGRATOR_OPTIX;
   if (optix) optix_frame_params(c, f, fv);
-  const bool timing = (f.flags & (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE)) != 0;
-  StageTimer tm{c, timing, false, s};
-  if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
   tm.begin_call();
   uint32_t done = 0, launches = 0;
   while (done < f.spp) {
     fv.k = std::min<uint32_t>(kPtFramesPerLaunch, f.spp - done);
-    fv.acc0 = f.frame_begin + done;
-    fv.reset = (reset && done == 0) ? 1u : 0u;
+    fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
+    fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     tm.begin(7);
     if (optix) launch_optix(sv, sh, fv, w, s);
     else launch_pathtracer(sv, sh, fv, w, s);
@@ -400,26 +407,205 @@ int render_pathtracer(Context& c, const sptr_frame& f, bool reset, hipStream_t s
     done += fv.k;
     ++launches;
   }
-  const uint32_t total = f.frame_begin + f.spp - 1;
   if (!(f.flags & SPTR_FRAME_NO_RESOLVE)) {
     tm.begin(4);
-    launch_resolve(fv, static_cast<const float4*>(c.accum.p), total, static_cast<uint32_t*>(c.tiles.p),
+    launch_resolve(fv, static_cast<const float4*>(c.accum.p), 0u, static_cast<uint32_t*>(c.tiles.p),
                    static_cast<uint8_t*>(c.image.p), s);
     tm.end();
   }
   tm.end_call();
-  API_HIP(hipGetLastError());
-  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
-  c.last_samples = total;
-  ++c.pending;
-  c.pending_stream = s;
-  c.pending_samples += (uint64_t)fv.valid * f.spp * (optix ? 1u : fv.spf);
-  c.pending_waves += launches;
-  if (f.flags & SPTR_FRAME_ASYNC) {
-    if (stats) std::memset(stats, 0, sizeof(*stats));
+  return launches;
+}
+
+// Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
+uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
+  const SceneView sv = scene_view(c);
+  const ShadeView sh = shade_view(c);
+  const WaveView w = wave_view(c);
+  FrameView fv = frame_view(c, f);
+  fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
+  const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
+  tm.begin_call();
+  uint32_t done = 0, waves = 0;
+  const int D = (int)f.max_depth;
+  while (done < f.spp) {
+    const uint32_t kk = std::min<uint32_t>(k, f.spp - done);
+    fv.k = kk;
+    fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
+    fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
+    fv.pixel_major = bounce0_pixel_major(sv, fv);
+    // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
+    // its grid size = the number of segments its consumers scan
+    uint32_t g_shade = 0;
+    for (int d = 0; d < D; ++d) {
+      if (d >= T) {  // the remaining bounces, path per thread
+        tm.begin(7);
+        launch_tail(sv, sh, fv, w, d, g_shade, s);
+        tm.end();
+        break;
+      }
+      tm.begin(d == 0 ? 5 : 1);
+      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
+      tm.end();
+      tm.begin(d == 0 ? 6 : 2);
+      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, s);
+      tm.end();
+      tm.begin(3);
+      launch_shadow(sv, sh, w, d, count, g_shade, s);
+      tm.end();
+    }
+    tm.begin(4);
+    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), s);
+    tm.end();
+    done += kk;
+    ++waves;
+  }
+  if (!(f.flags & SPTR_FRAME_NO_RESOLVE)) {
+    tm.begin(4);
+    launch_resolve(fv, static_cast<const float4*>(c.accum.p), 0u, static_cast<uint32_t*>(c.tiles.p),
+                   static_cast<uint8_t*>(c.image.p), s);
+    tm.end();
+  }
+  tm.end_call();
+  return waves;
+}
+
+bool same_key(const GraphKey& a, const GraphKey& b) { return std::memcmp(&a, &b, sizeof(GraphKey)) == 0; }
+
+void drop_graph(Context& c) {
+  if (c.graph.exec) (void)hipGraphExecDestroy(c.graph.exec);
+  if (c.graph.graph) (void)hipGraphDestroy(c.graph.graph);
+  c.graph = GraphCache{};
+}
+
+// Enqueue one render call's launch sequence on s.  A call shape seen twice in a row is captured
+// once into a hipGraph (on the context's capture stream) and replayed from then on: one graph
+// launch instead of ~20 kernel launches, with the per-call values (frame_begin, reset, total) passed
+// as the arguments of the graph's k_frame_dyn node and the timing events re-pointed at fresh pool
+// events per replay.  The launch sequence itself is the same code either way.
+template <class Enqueue>
+int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, bool timing,
+             bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
+  const bool repeat = c.have_last_key && same_key(key, c.last_key);
+  c.last_key = key;
+  c.have_last_key = true;
+  if (c.launch_mode != 0 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+    StageTimer tm{c, timing, trace_only, s};
+    launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, s);
+    waves = enqueue(s, tm);
+    API_HIP(hipGetLastError());
+    if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
     return SPTR_OK;
   }
-  return collect_pending(c, stats);
+  if (!(c.graph.valid && same_key(key, c.graph.key))) {  // capture this shape
+    drop_graph(c);
+    const size_t m0 = c.marks.size(), e0 = c.events_used;
+    // the pool must not grow inside the capture (hipEventCreate is not a capturable call): every
+    // span of a call uses two events; 512 covers 255 spans (> 6 batches x 6 bounces x 3 stages)
+    while (c.events.size() < c.events_used + 512) {
+      hipEvent_t e = nullptr;
+      API_HIP(hipEventCreate(&e));
+      c.events.push_back(e);
+    }
+    API_HIP(hipStreamBeginCapture(c.cap_stream, hipStreamCaptureModeThreadLocal));
+    StageTimer tm{c, timing, trace_only, c.cap_stream};
+    tm.capturing = true;
+    const uint32_t nw = enqueue(c.cap_stream, tm);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(c.cap_stream, &g);
+    const std::vector<StageMark> cap_marks(c.marks.begin() + (std::ptrdiff_t)m0, c.marks.end());
+    c.marks.resize(m0);  // the capture executed nothing
+    c.events_used = e0;
+    if (ec != hipSuccess || tm.err != hipSuccess || !g) {
+      // not capturable (e.g. more stage spans than the pre-grown event pool): direct launches
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      StageTimer td{c, timing, trace_only, s};
+      launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, s);
+      waves = enqueue(s, td);
+      API_HIP(hipGetLastError());
+      if (td.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(td.err));
+      return SPTR_OK;
+    }
+    GraphCache gc;
+    gc.graph = g;
+    gc.key = key;
+    gc.waves = nw;
+    // the k_frame_dyn node heads the graph: every captured root depends on it
+    size_t nr = 0;
+    API_HIP(hipGraphGetRootNodes(g, nullptr, &nr));
+    std::vector<hipGraphNode_t> roots(nr);
+    API_HIP(hipGraphGetRootNodes(g, roots.data(), &nr));
+    void* dyn_ptr = c.dyn.p;
+    uint32_t a0 = frame_begin, a1 = reset, a2 = total;
+    void* args[4] = {&dyn_ptr, &a0, &a1, &a2};
+    hipKernelNodeParams kp{};
+    kp.func = const_cast<void*>(frame_dyn_kernel());
+    kp.gridDim = dim3(1);
+    kp.blockDim = dim3(64);
+    kp.sharedMemBytes = 0;
+    kp.kernelParams = args;
+    kp.extra = nullptr;
+    API_HIP(hipGraphAddKernelNode(&gc.dyn_node, g, nullptr, 0, &kp));
+    for (hipGraphNode_t r : roots) API_HIP(hipGraphAddDependencies(g, &gc.dyn_node, &r, 1));
+    gc.dyn_params = kp;
+    // event-record nodes of the stage spans, matched through the pool events they recorded
+    size_t n = 0;
+    API_HIP(hipGraphGetNodes(g, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    API_HIP(hipGraphGetNodes(g, nodes.data(), &n));
+    std::vector<std::pair<hipEvent_t, hipGraphNode_t>> ev_nodes;
+    for (hipGraphNode_t nd : nodes) {
+      hipGraphNodeType t;
+      API_HIP(hipGraphNodeGetType(nd, &t));
+      if (t != hipGraphNodeTypeEventRecord) continue;
+      hipEvent_t e = nullptr;
+      API_HIP(hipGraphEventRecordNodeGetEvent(nd, &e));
+      ev_nodes.emplace_back(e, nd);
+    }
+    auto node_of = [&](size_t ei) -> hipGraphNode_t {
+      for (auto& pr : ev_nodes)
+        if (ei < c.events.size() && pr.first == c.events[ei]) return pr.second;
+      return nullptr;
+    };
+    for (const StageMark& m : cap_marks) {
+      const GraphMark gm{m.stage, node_of(m.b), node_of(m.e)};
+      if (!gm.b || !gm.e) {
+        (void)hipGraphDestroy(g);
+        return fail(c, SPTR_ERR_HIP, "render: graph capture: stage event node not found (" +
+                                         std::to_string(ev_nodes.size()) + " event nodes)");
+      }
+      gc.marks.push_back(gm);
+    }
+    const hipError_t ei = hipGraphInstantiate(&gc.exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      return fail(c, SPTR_ERR_HIP, std::string("render: graph instantiate: ") + hipGetErrorString(ei));
+    }
+    gc.valid = true;
+    c.graph = gc;
+  }
+  // replay: the call's values into the k_frame_dyn node, fresh pool events into the event nodes
+  GraphCache& gc = c.graph;
+  void* dyn_ptr = c.dyn.p;
+  uint32_t a0 = frame_begin, a1 = reset, a2 = total;
+  void* args[4] = {&dyn_ptr, &a0, &a1, &a2};
+  hipKernelNodeParams p = gc.dyn_params;
+  p.kernelParams = args;
+  p.extra = nullptr;
+  API_HIP(hipGraphExecKernelNodeSetParams(gc.exec, gc.dyn_node, &p));
+  StageTimer tm{c, true, false, s};
+  for (const GraphMark& m : gc.marks) {
+    const size_t b = tm.alloc(), e = tm.alloc();
+    if (b == SIZE_MAX || e == SIZE_MAX) break;
+    API_HIP(hipGraphExecEventRecordNodeSetEvent(gc.exec, m.b, c.events[b]));
+    API_HIP(hipGraphExecEventRecordNodeSetEvent(gc.exec, m.e, c.events[e]));
+    c.marks.push_back(StageMark{m.stage, b, e});
+  }
+  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
+  API_HIP(hipGraphLaunch(gc.exec, s));
+  waves = gc.waves;
+  return SPTR_OK;
 }
 
 }  // namespace
@@ -440,12 +626,14 @@ int sptr_create(int device, sptr_ctx** out) {
   sptr_ctx* x = new sptr_ctx();
   Context& c = x->c;
   c.device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess) {
     delete x;
     return SPTR_ERR_HIP;
   }
   const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8;
   if (ensure_buf(c.w_seg, seg_bytes) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
+      ensure_buf(c.dyn, 64) != hipSuccess ||
       hipMemset(c.w_seg.p, 0, seg_bytes) != hipSuccess) {
     delete x;
     return SPTR_ERR_OOM;
@@ -466,8 +654,11 @@ int sptr_destroy(sptr_ctx* x) {
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& b : c.w_rs)
     for (DevBuf& x : b) free_buf(x);
+  drop_graph(c);
+  free_buf(c.dyn);
   for (hipEvent_t e : c.events) (void)hipEventDestroy(e);
   if (c.stream) (void)hipStreamDestroy(c.stream);
+  if (c.cap_stream) (void)hipStreamDestroy(c.cap_stream);
   delete x;
   return SPTR_OK;
 }
@@ -477,6 +668,7 @@ const char* sptr_last_error(const sptr_ctx* x) { return x ? x->c.err.c_str() : "
 int sptr_set_debug_mode(sptr_ctx* x, int mode) {
   if (!x) return SPTR_ERR_INVALID;
   x->c.debug_mode = mode;
+  ++x->c.epoch;
   return SPTR_OK;
 }
 
@@ -484,6 +676,7 @@ int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   if (!x) return SPTR_ERR_INVALID;
   if (n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 0 (automatic) or 1..32");
   x->c.leaf_size = n;
+  ++x->c.epoch;
   return SPTR_OK;
 }
 
@@ -491,6 +684,7 @@ int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
   if (!x) return SPTR_ERR_INVALID;
   if (width != 0 && width != 2 && width != 4) return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or 4");
   x->c.bvh_width = width;
+  ++x->c.epoch;
   return SPTR_OK;
 }
 
@@ -498,6 +692,7 @@ int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
   if (!x) return SPTR_ERR_INVALID;
   if (depth > (uint32_t)kMaxDepth) return fail(x->c, SPTR_ERR_INVALID, "tail depth must be 0 (automatic) or 1..32");
   x->c.tail_depth = depth;
+  ++x->c.epoch;
   return SPTR_OK;
 }
 
@@ -505,6 +700,7 @@ int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
   if (!x) return SPTR_ERR_INVALID;
   if (max_paths > (1ull << 30)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^30");
   x->c.wave_paths = max_paths;
+  ++x->c.epoch;
   return SPTR_OK;
 }
 
@@ -536,6 +732,7 @@ int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
                             s->num_tri_geoms);
   if (rc != SPTR_OK) return rc;
   c.have_scene = true;
+  ++c.epoch;
   return resolve_geom_materials(c);
 }
 
@@ -578,6 +775,7 @@ int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
   std::memcpy(c.mats_host.data(), m, sizeof(DevMaterial) * n);
   API_HIP(ensure_buf(c.mats, sizeof(DevMaterial) * n));
   API_HIP(hipMemcpy(c.mats.p, c.mats_host.data(), sizeof(DevMaterial) * n, hipMemcpyHostToDevice));
+  ++c.epoch;
   return resolve_geom_materials(c);
 }
 
@@ -586,6 +784,7 @@ int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
   Context& c = x->c;
   if (n > (uint32_t)kMaxLights) return fail(c, SPTR_ERR_INVALID, "too many lights");
   c.lights_host.resize(n);
+  ++c.epoch;
   for (uint32_t i = 0; i < n; ++i) {
     DevLight& d = c.lights_host[i];
     d.type = l[i].type;
@@ -611,6 +810,7 @@ int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
   API_HIP(hipSetDevice(c.device));
   if (!e || !e->faces) {
     free_buf(c.env);
+    ++c.epoch;
     c.env_size = 0;
     if (e) {
       c.env_intensity = e->intensity;
@@ -630,6 +830,7 @@ int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
   API_HIP(ensure_buf(c.env, texels * 16));
   API_HIP(hipMemcpy(c.env.p, tmp.data(), texels * 16, hipMemcpyHostToDevice));
   c.env_size = e->size;
+  ++c.epoch;
   c.env_intensity = e->intensity;
   c.env_clamp = e->max_clamp;
   return SPTR_OK;
@@ -661,100 +862,78 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   const bool reset = f->frame_begin == 1;
   if (!reset && f->frame_begin != c.last_samples + 1)
     return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
-  if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) return render_pathtracer(c, *f, reset, s, stats);
-  uint64_t wave_paths = c.wave_paths;
-  if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
-    wave_paths = kDefaultWavePaths;
-    if (c.wave_cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
-      size_t free_b = 0, total_b = 0;
-      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
-        const uint64_t held = c.wave_cap ? c.wave_cap * wave_path_bytes(c.wave_L, c.wave_ts) : 0ull;
-        const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
-        // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
-        const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
-                              (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u));
-        const uint64_t fit = budget > 0.0 ? (uint64_t)budget / wave_path_bytes(L, task_stride(c)) : 0ull;
-        wave_paths = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(wave_paths, fit));
-      }
-    }
-  }
-  uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
-  k = std::min<uint32_t>(k, f->spp);
-  const SceneView sv = scene_view(c);
-  {
-    // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
-    FrameView probe = frame_view(c, *f);
-    probe.k = k;
-    const uint32_t k_slack = bounce0_pixel_major(sv, probe) ? k : 1u;
-    rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
-    if (rc != SPTR_OK) return rc;
-  }
-
-  const ShadeView sh = shade_view(c);
-  const WaveView w = wave_view(c);
-  FrameView fv = frame_view(c, *f);
   const bool timing = (f->flags & SPTR_FRAME_TIMING) != 0;
-  const bool count = (f->flags & SPTR_FRAME_COUNT_VISITS) != 0;
   const bool trace_timing = (f->flags & SPTR_FRAME_TIMING_TRACE) != 0;
-  StageTimer tm{c, timing || trace_timing, !timing, s};
-  if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
-  tm.begin_call();
-  uint32_t done = 0, waves = 0;
-  const int D = (int)f->max_depth;
-  const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P)));
-  while (done < f->spp) {
-    const uint32_t kk = std::min<uint32_t>(k, f->spp - done);
-    fv.k = kk;
-    fv.acc0 = f->frame_begin + done;
-    fv.reset = (reset && done == 0) ? 1u : 0u;
-    fv.pixel_major = bounce0_pixel_major(sv, fv);
-    // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
-    // its grid size = the number of segments its consumers scan
-    uint32_t g_shade = 0;
-    for (int d = 0; d < D; ++d) {
-      if (d >= T) {  // the remaining bounces, path per thread
-        tm.begin(7);
-        launch_tail(sv, sh, fv, w, d, g_shade, s);
-        tm.end();
-        break;
-      }
-      tm.begin(d == 0 ? 5 : 1);
-      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
-      tm.end();
-      tm.begin(d == 0 ? 6 : 2);
-      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, s);
-      tm.end();
-      tm.begin(3);
-      launch_shadow(sv, sh, w, d, count, g_shade, s);
-      tm.end();
-    }
-    tm.begin(4);
-    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), s);
-    tm.end();
-    API_HIP(hipGetLastError());
-    done += kk;
-    ++waves;
-  }
   const uint32_t total = f->frame_begin + f->spp - 1;
-  if (!(f->flags & SPTR_FRAME_NO_RESOLVE)) {
-    tm.begin(4);
-    launch_resolve(fv, static_cast<const float4*>(c.accum.p), total, static_cast<uint32_t*>(c.tiles.p),
-                   static_cast<uint8_t*>(c.image.p), s);
-    tm.end();
+  GraphKey key{};
+  key.epoch = c.epoch;
+  key.frame = *f;
+  key.frame.frame_begin = 0;
+  key.frame.flags &= (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_COUNT_VISITS | SPTR_FRAME_NO_RESOLVE);
+  uint32_t waves = 0;
+  uint64_t samples = 0;
+  if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) {
+    if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+    const uint32_t spf = f->integrator == SPTR_INTEGRATOR_PATHTRACER ? (f->samples_per_frame ? f->samples_per_frame : 4u) : 1u;
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, timing || trace_timing, false, s,
+                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_path_per_thread(c, *f, cs, tm); }, waves);
+    if (rc != SPTR_OK) return rc;
+    samples = (uint64_t)frame_view(c, *f).valid * f->spp * spf;
+  } else {
+    uint64_t wave_paths = c.wave_paths;
+    if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
+      wave_paths = kDefaultWavePaths;
+      if (c.wave_cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
+          const uint64_t held = c.wave_cap ? c.wave_cap * wave_path_bytes(c.wave_L, c.wave_ts) : 0ull;
+          const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
+          // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
+          const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
+                                (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u));
+          const uint64_t fit = budget > 0.0 ? (uint64_t)budget / wave_path_bytes(L, task_stride(c)) : 0ull;
+          wave_paths = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(wave_paths, fit));
+        }
+      }
+    }
+    uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
+    k = std::min<uint32_t>(k, f->spp);
+    {
+      // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
+      const SceneView sv = scene_view(c);
+      FrameView probe = frame_view(c, *f);
+      probe.k = k;
+      const uint32_t k_slack = bounce0_pixel_major(sv, probe) ? k : 1u;
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
+      if (rc != SPTR_OK) return rc;
+    }
+    const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P)));
+    key.epoch = c.epoch;  // ensure_wave may have reallocated
+    key.k = k;
+    key.tail = (uint32_t)T;
+    if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, timing || trace_timing, !timing, s,
+                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
+    if (rc != SPTR_OK) return rc;
+    samples = (uint64_t)frame_view(c, *f).valid * f->spp;
   }
-  tm.end_call();
-  API_HIP(hipGetLastError());
-  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
   c.last_samples = total;
   ++c.pending;
   c.pending_stream = s;
-  c.pending_samples += (uint64_t)fv.valid * f->spp;
+  c.pending_samples += samples;
   c.pending_waves += waves;
   if (f->flags & SPTR_FRAME_ASYNC) {
     if (stats) std::memset(stats, 0, sizeof(*stats));
     return SPTR_OK;
   }
   return collect_pending(c, stats);
+}
+
+int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (mode > 1) return fail(x->c, SPTR_ERR_INVALID, "launch mode must be 0 (graphs) or 1 (direct)");
+  x->c.launch_mode = mode;
+  return SPTR_OK;
 }
 
 int sptr_collect_stats(sptr_ctx* x, sptr_stats* stats) {

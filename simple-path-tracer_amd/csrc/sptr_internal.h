@@ -127,6 +127,7 @@ struct FrameView {
   uint32_t ablate;  // SPTR_ABLATE environment variable: timing experiments only (0 in normal use)
   float4* accum;    // per local pixel: running sample sum (xyz) + resume slot (w bits), see k_accum
   uint32_t reset;   // this batch starts the accumulation (frame_begin == 1, first batch)
+  const uint32_t* dyn;  // device {frame_begin, reset, total} of the call (k_frame_dyn); see frame_dyn
   uint32_t pixel_major;  // kFold*: bounce 0 folds each pixel's leading misses into accum (bounce0_pixel_major)
   uint32_t integrator;   // sptr_integrator
   uint32_t spf;          // PathTracer mode: samples per frame
@@ -192,9 +193,40 @@ struct StageMark {
   size_t b, e;  // begin / end event indices in Context::events
 };
 
+// Launch-graph cache of one render-call shape (sptr_api.cpp run_graph).  The key is every input of
+// the call's launch sequence except the per-call device words (FrameView::dyn): the state epoch (bumped
+// by every scene/state upload and buffer reallocation), the frame with frame_begin zeroed and the
+// timing flags kept, and the batch plan.
+struct GraphKey {
+  uint64_t epoch;
+  sptr_frame frame;
+  uint32_t k, tail, pad0, pad1;
+};
+struct GraphMark {
+  int stage;
+  hipGraphNode_t b, e;  // event-record nodes of the stage span
+};
+struct GraphCache {
+  bool valid = false;
+  GraphKey key{};
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipGraphNode_t dyn_node = nullptr;  // k_frame_dyn: its arguments are the per-call values
+  hipKernelNodeParams dyn_params{};
+  std::vector<GraphMark> marks;  // stage spans in recording order (re-pointed at fresh events per replay)
+  uint32_t waves = 0;
+};
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t cap_stream = nullptr;  // launch-graph capture
+  uint32_t launch_mode = 0;          // 0: replay a captured graph for repeated call shapes; 1: direct launches
+  uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
+  DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
+  GraphCache graph;
+  GraphKey last_key{};               // the previous call's shape: a graph is captured when it repeats
+  bool have_last_key = false;
   std::string err;
   int debug_mode = 0;
   uint64_t wave_paths = 0;  // 0 = default
@@ -260,6 +292,9 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
+// Head of every render call: the per-call values kernels read through FrameView::dyn.
+void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, hipStream_t s);
+const void* frame_dyn_kernel();
 // PathTracer-mode frames (the k frames of f from f.acc0), one launch: accum += tonemapped frames.
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
 // OptiX-compatible frames (the k frames of f from f.acc0), one launch: accum.xyz += contributions,

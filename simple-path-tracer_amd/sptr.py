@@ -101,7 +101,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -129,6 +129,7 @@ def lib() -> C.CDLL:
         "sptr_last_error": (C.c_char_p, [vp]),
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
+        "sptr_set_launch_mode": (C.c_int, [vp, u32]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
@@ -388,6 +389,10 @@ class Renderer:
 
     def set_wave_paths(self, n: int):
         self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
+
+    def set_launch_mode(self, mode: int):
+        """0: replay captured launch graphs for repeated call shapes (default); 1: direct launches."""
+        self._check(self._L.sptr_set_launch_mode(self._h, mode), "set_launch_mode")
 
     def set_tail_depth(self, n: int):
         self._check(self._L.sptr_set_tail_depth(self._h, n), "set_tail_depth")

@@ -398,3 +398,36 @@ def test_wave_fold_vs_oracle(renderer):
     st, rgb, acc, orgb, oacc, ocnt = _render_pair(renderer, "default_emitter", 64, 48, 48)
     _image_close(rgb, orgb, acc, oacc)
     assert st.samples == ocnt["samples"]
+
+
+@pytest.mark.parametrize("integrator", [0, 1, 2])
+def test_launch_graph_replay_equals_direct(renderer, integrator):
+    """Repeated call shapes are captured into a hipGraph and replayed (sptr_set_launch_mode 0): the
+    accumulation, the stats and the stage timings must match direct launches call for call —
+    including progressive continuation (the per-call frame index is a graph-node argument), a
+    camera change (new shape: direct launches again) and asynchronous calls."""
+    W, H = 96, 64
+    sptr.setup_default(renderer, "default_emitter")
+    cams = [sptr.camera_lookat(aspect=W / H), sptr.camera_lookat(pos=(0.5, 3.0, 8.0), aspect=W / H)]
+    out = {}
+    try:
+        for mode in (1, 0):
+            renderer.set_launch_mode(mode)
+            seq = []
+            for cam in (cams[0], cams[0], cams[0], cams[1], cams[1], cams[1]):
+                fb = 1 if not seq or seq[-1][3] is not cam else seq[-1][4] + 2
+                st = renderer.render(cam, W, H, spp=2, frame_begin=fb, integrator=integrator,
+                                     flags=sptr.SPTR_FRAME_TIMING_TRACE)
+                seq.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, cam, fb, st.ms_total))
+            for fb in (1, 3, 5):  # asynchronous replays, one collection
+                renderer.render(cams[0], W, H, spp=2, frame_begin=fb, integrator=integrator,
+                                flags=sptr.SPTR_FRAME_ASYNC)
+            st = renderer.collect_stats()
+            seq.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, None, 0, st.ms_total))
+            out[mode] = seq
+    finally:
+        renderer.set_launch_mode(0)
+    for a, b in zip(out[1], out[0]):
+        assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+        assert (a[1], a[2]) == (b[1], b[2])
+        assert b[5] > 0.0  # the call span's events were re-pointed and recorded on replay
