@@ -54,6 +54,21 @@ __device__ __forceinline__ float div_nrm(float a, const DivBy& d) {
 // [2^-96, 2^100]: the squared length of a direction-like vector (callers: normalize_dir).
 __device__ __forceinline__ float inv_len_nrm(float l2) { return rcp_nrm(sqrt_nrm(l2)); }
 
+// 1 / sqrt(l2) as inv_len_nrm, in closed form when l2 lies within 1024 ulps of 1.0 — the squared
+// length of a vector that is already unit length up to rounding (re-normalized ray directions,
+// normals, reflections, cosine samples).  With l2 = 1 + d ulps: for d >= 0 (ulp 2^-23),
+// sqrt = 1 + floor(d/2) 2^-23 and its reciprocal 1 - floor(d/2) 2^-23, i.e. bits 0x3F800000 -
+// (d & ~1); for d < 0 (ulp 2^-24), sqrt = 1 - j 2^-24 with j = ceil(-d/2) and the reciprocal is
+// 1 + ceil(j/2) 2^-23.  The neglected second-order terms stay below a quarter ulp for |d| < 2900;
+// checked against 1.0f / sqrtf over the whole window on the CPU (tests/test_cr_math_cpu.py) and on
+// the GPU (tests/hip/crmath_check.hip).  Other l2 take the general sequence.
+__device__ __forceinline__ float inv_len_unit(float l2) {
+  const int d = (int)__float_as_uint(l2) - 0x3F800000;
+  if (__builtin_expect(d < -1024 || d > 1024, 0)) return inv_len_nrm(l2);
+  const int u = d >= 0 ? -(d & ~1) : (((-d + 1) >> 1) + 1) >> 1;
+  return __int_as_float(0x3F800000 + u);
+}
+
 // 1 / sqrt(l2) for every float l2 (bit-identical to 1.0f / sqrtf(l2), checked over all 2^32 inputs by
 // tests/hip/crmath_check.hip).  Out-of-domain inputs are scaled by an even power of two, which
 // commutes exactly with the correctly rounded sqrt (the scaled root stays normal), so there is no

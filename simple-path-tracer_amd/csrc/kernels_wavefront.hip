@@ -27,6 +27,9 @@
 #ifndef SPTR_TRACE_WAVES
 #define SPTR_TRACE_WAVES 7  // measured: 7 -> +6% on C2 (SGPR-limited to 6 otherwise)
 #endif
+#ifndef SPTR_TRACE_PM_WAVES
+#define SPTR_TRACE_PM_WAVES SPTR_TRACE_WAVES
+#endif
 #ifndef SPTR_TRACE4_WAVES
 #define SPTR_TRACE4_WAVES 6  // BVH4, bounces >= 1: 7 waves (72 VGPRs) spills; measured C5 12.7 -> 7.1 ms
                              // (bounce 0 stays at 7: coherent rays gain more from occupancy, 8.4 -> 5.4)
@@ -152,6 +155,16 @@ __device__ __forceinline__ vec3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
 __device__ __forceinline__ float4 f4(vec3 a, float w) { return make_float4(a.x, a.y, a.z, w); }
 __device__ __forceinline__ float clamp_std(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
 
+// SPTR_ABLATE timing experiments (sptr_api.cpp frame_view): compiled out of normal builds, so the
+// production kernels carry neither the field nor its branches.
+__device__ __forceinline__ uint32_t ablate(const FrameView& f) {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  return f.ablate;
+#else
+  (void)f;
+  return 0u;
+#endif
+}
 __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim.x; }
 
 // tile-packed local pixel -> image coordinates (interleaved 32x32 tile sharding)
@@ -544,7 +557,7 @@ __device__ __forceinline__ void primary_at(const FrameView& f, const ImageDiv& d
   const float jx = rand01(r);
   const float jy = rand01(r);
   const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, dv.w), div_nrm(float(y) + jy, dv.h));
-  out.d = safe_normalize_dir(dir);
+  out.d = safe_renormalize_dir(dir);
   out.rng = wang_hash((ps ^ acc) ^ 1u);
 }
 __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
@@ -598,7 +611,7 @@ __device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, i
 template <bool kCube>
 __device__ __forceinline__ vec3 env_color(const EnvView& sh, vec3 dir) {
   if (!kCube) return sky_color(dir);
-  const vec3 d = normalize_dir(dir);
+  const vec3 d = renormalize_dir(dir);
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
   float ma, uc, vc;
   int face;
@@ -674,7 +687,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // resumes there (accum.w = resume slot).  A kernel of its own (not a branch of k_trace), so that
 // its registers are allocated for this loop alone.
 template <bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE_PM_WAVES)
     k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
@@ -709,15 +722,15 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
         const Ray r = make_ray(f.cam_pos, pr.d);
         // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
         // 1 = constant environment, 4 = primary misses add no radiance
-        if (!(f.ablate & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!(ablate(f) & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
           if (sh.debug_mode != 1) {
-            const vec3 e = (f.ablate & 1u) ? pr.d : env_color<kCube>(sh, safe_normalize_dir(pr.d));
+            const vec3 e = (ablate(f) & 1u) ? pr.d : env_color<kCube>(sh, safe_renormalize_dir(pr.d));
             rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           }
           if (!fold) w.rad[p] = f4(rv, 0.0f);
-          else if (!(f.ablate & 4u)) a = a + rv;
+          else if (!(ablate(f) & 4u)) a = a + rv;
         } else if (fold) {
           fold = false;
           resume = smp;
@@ -790,7 +803,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         const Ray r = make_ray(f.cam_pos, pr.d);
         hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_normalize_dir(pr.d));
+        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
       }
       // this pixel group's hits of the round -> number of leading misses still to fold
       const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
@@ -872,13 +885,13 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       const Ray r = make_ray(o, d);
       // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
       // 1 = constant environment, 4 = primary misses write no radiance
-      if (!(kPrimary && (f.ablate & 2u))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-      if (kPrimary && !hit && (f.ablate & 4u)) {
+      if (!(kPrimary && (ablate(f) & 2u))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+      if (kPrimary && !hit && (ablate(f) & 4u)) {
       } else if (!hit) {
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = (f.ablate & 1u) ? d : env_color<kCube>(sh, safe_normalize_dir(d));
+          const vec3 e = (ablate(f) & 1u) ? d : env_color<kCube>(sh, safe_renormalize_dir(d));
           vec3 rv;
           if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -977,7 +990,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   const vec3 albedo = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
   if (m.metallic > 0.5f) {
     no = P + nrm * 1e-4f;
-    nd = safe_normalize_dir(reflect(rd, nrm));
+    nd = safe_renormalize_dir(reflect(rd, nrm));
     thr = thr * (albedo * m.metallic);
     return true;
   }
@@ -993,7 +1006,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
     const float xi = rand01(rng);
     if (xi < F) {
       no = P + nrm * 1e-4f;
-      nd = safe_normalize_dir(reflect(rd, nrm));
+      nd = safe_renormalize_dir(reflect(rd, nrm));
       thr = thr * v3(1.0f - tr, 1.0f - tr, 1.0f - tr);
     } else {
       const float ci = -dot(nrm, rd);
@@ -1002,11 +1015,11 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
       if (!(kk < 0.0f)) refr = eta * rd + (eta * ci - sqrtf(kk)) * nrm;
       if (dot(refr, refr) > 0.0f) {
         no = P - nrm * 1e-4f;
-        nd = safe_normalize_dir(refr);
+        nd = safe_renormalize_dir(refr);
         thr = thr * v3(tr, tr, tr);
       } else {
         no = P + nrm * 1e-4f;
-        nd = safe_normalize_dir(reflect(rd, nrm));
+        nd = safe_renormalize_dir(reflect(rd, nrm));
       }
     }
     return true;
@@ -1017,11 +1030,11 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   const float rr = sqrtf(r2);
   const float lx = rr * cosf(phi), ly = rr * sinf(phi);
   const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
-  const vec3 nn = safe_normalize_dir(nrm);
+  const vec3 nn = safe_renormalize_dir(nrm);
   const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize_dir(cross(nn, v3(0.0f, 0.0f, 1.0f)))
                                          : normalize_dir(cross(nn, v3(0.0f, 1.0f, 0.0f)));
   const vec3 bt = cross(tg, nn);
-  const vec3 sdir = safe_normalize_dir(tg * lx + bt * ly + nn * lz);
+  const vec3 sdir = safe_renormalize_dir(tg * lx + bt * ly + nn * lz);
   no = P + nrm * 1e-4f;
   const float surv = fmax_g(fmax_g(albedo.x, albedo.y), albedo.z);
   const float xi = rand01(rng);
@@ -1032,7 +1045,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   } else {
     thr = thr * albedo;
   }
-  nd = safe_normalize_dir(sdir);
+  nd = safe_renormalize_dir(sdir);
   return cont;
 }
 
@@ -1257,7 +1270,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
         loaded = true;
       }
       if (!hit) {
-        radv = radv + thr * env_color<kCube>(sh.env, safe_normalize_dir(rd));
+        radv = radv + thr * env_color<kCube>(sh.env, safe_renormalize_dir(rd));
         break;
       }
       const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
@@ -1451,7 +1464,7 @@ __device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& 
     float t = __builtin_huge_valf();
     uint32_t ref = kNoHit;
     if (!traverse_w<kW4, false, false>(sc, sv, make_ray(o, d), 1e-4f, t, ref, vc, ls)) {
-      rad = rad + thr * env_color<kCube>(sh.env, normalize_dir(d));
+      rad = rad + thr * env_color<kCube>(sh.env, renormalize_dir(d));
       break;
     }
     const vec3 P = o + t * d;
@@ -1902,7 +1915,7 @@ __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, ui
     const float jx = rand01(r);
     const float jy = rand01(r);
     const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, idiv.w), div_nrm(float(y) + jy, idiv.h));  // as primary_path
-    const vec3 d = safe_normalize_dir(dir);
+    const vec3 d = safe_renormalize_dir(dir);
     dirs[(size_t)i * 3 + 0] = d.x;
     dirs[(size_t)i * 3 + 1] = d.y;
     dirs[(size_t)i * 3 + 2] = d.z;
@@ -1995,15 +2008,29 @@ static unsigned trace_lds(const SceneView& sv, bool lds, bool primary, uint32_t 
 // on C2 (profiles/r01h_pixel_major.txt): 1 GPU, 4.5 pixels/thread: 4.17 -> 3.74 ms; 2-way shard,
 // 2.3: 2.26 -> 2.24-2.28; 4-way, 1.1: 1.20 -> 1.28-1.29; 8-way: 0.72 -> 0.99.
 constexpr uint32_t kPixelMajorItems = 4;
+constexpr uint32_t kPixelMajorMaxK = 128;  // samples per batch above which < 8 pixels/thread go lane-group
 // Lane-group bounce 0 (k_trace_wp) from this many samples per batch: 8 lanes take 8 samples of one
 // pixel per round, so smaller batches would leave lanes idle.
 constexpr uint32_t kWaveFoldMinK = 16;
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  if (const char* e = getenv("SPTR_FOLD")) {  // timing experiments: force kFoldNone/Thread/Wave
+    const uint32_t m = (uint32_t)atoi(e);
+    if (m == kFoldNone || (sv.lds_bytes != 0 && (m == kFoldThread || (m == kFoldWave && f.k >= kWaveFoldMinK)))) return m;
+  }
+#endif
   if (sv.lds_bytes != 0) {
     const unsigned lb = trace_lds(sv, true, true, 0);
     const unsigned g = sv.width == 4u ? resident_grid((const void*)&k_trace_pm<false, true, false>, lb)
                                       : resident_grid((const void*)&k_trace_pm<false, false, false>, lb);
-    if ((uint64_t)f.P >= (uint64_t)g * kBlock * kPixelMajorItems) return kFoldThread;
+    const uint64_t threads = (uint64_t)g * kBlock;
+    // a thread's pixels are serial loops of k samples: with few pixels per thread and long loops the
+    // last round's tail costs more than the lane-group fold (measured r02, emulated 4K shards at
+    // 4.5 pixels/thread: k = 64 (C2, 1 GPU) thread 1.45 vs lanes 1.53 ms; k = 259 (C4, 4-way)
+    // thread 27.9 vs lanes 22.9 ms; 9 pixels/thread, k = 129 (C4, 2-way): 41.2 vs 45.4 ms)
+    if ((uint64_t)f.P >= threads * kPixelMajorItems &&
+        ((uint64_t)f.P >= threads * 2u * kPixelMajorItems || f.k <= kPixelMajorMaxK))
+      return kFoldThread;
   }
   // L2/HBM scenes stay path-major: measured on MI355X (r02l), the lane-group kernel's fold state
   // costs the BVH4 traversal its registers (33 VGPR spills at 7 waves) and more than the saved

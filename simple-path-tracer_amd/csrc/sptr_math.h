@@ -57,9 +57,11 @@ inline float sq_root(float x) { return std::sqrt(x); }
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ float inv_length(float l2) { return inv_len(l2); }
 __device__ __forceinline__ float inv_length_dir(float l2) { return inv_len_nrm(l2); }
+__device__ __forceinline__ float inv_length_unit(float l2) { return inv_len_unit(l2); }
 #else
 SPTR_HD float inv_length(float l2) { return 1.0f / sq_root(l2); }
 SPTR_HD float inv_length_dir(float l2) { return 1.0f / sq_root(l2); }
+SPTR_HD float inv_length_unit(float l2) { return 1.0f / sq_root(l2); }
 #endif
 SPTR_HD vec3 normalize(vec3 v) { return v * inv_length(dot(v, v)); }
 SPTR_HD vec3 safe_normalize(vec3 v) {
@@ -75,6 +77,15 @@ SPTR_HD vec3 safe_normalize_dir(vec3 v) {
   const float l2 = dot(v, v);
   if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
   return v * inv_length_dir(l2);
+}
+// The same results again, for vectors that are unit length up to a few roundings already (ray
+// directions looked up in the environment, face-forwarded normals, reflections, refractions and
+// cosine samples of unit vectors): the device takes cr_math.h's closed form near |v| = 1.
+SPTR_HD vec3 renormalize_dir(vec3 v) { return v * inv_length_unit(dot(v, v)); }
+SPTR_HD vec3 safe_renormalize_dir(vec3 v) {
+  const float l2 = dot(v, v);
+  if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
+  return v * inv_length_unit(l2);
 }
 
 // normalize(vec3(0.3, 0.6, -0.8)), the sun direction of EnvironmentManager::getSkyColor

@@ -2,7 +2,8 @@
 // simple-path-tracer_amd/csrc/cr_math.h are bit-identical to the compiler's IEEE operators on
 // gfx950 over their stated domains.  Built and run by tests/test_gpu_crmath.py.
 //   sqrt_nrm : every float in [2^-96, 2^100]
-//   rcp_nrm  : every float in [2^-100, 2^100]
+//   rcp_nrm  : every float in [2^-100, 2^100]; inv_len_nrm and inv_len_unit (closed form within
+//              1024 ulps of 1.0, general sequence elsewhere) over the same floats
 //   inv_len  : every one of the 2^32 float bit patterns (NaN == NaN), against 1.0f / sqrtf(x)
 //   div_nrm  : divisors 1..8192 and the bench/test image sizes, 2^22 dividends each of the form
 //              float(x) + j (x integer pixel coordinate < b, j a 24-bit jitter), plus random floats
@@ -33,7 +34,9 @@ __global__ void k_rcp(uint32_t lo, uint32_t hi) {
   for (uint64_t u = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= hi; u += (uint64_t)gridDim.x * blockDim.x) {
     const float y = __uint_as_float((uint32_t)u);
     const float ref = 1.0f / y;
-    if (__float_as_uint(rcp_nrm(y)) != __float_as_uint(ref) || __float_as_uint(inv_len_nrm(y)) != __float_as_uint(1.0f / sqrtf(y))) {
+    const uint32_t il = __float_as_uint(1.0f / sqrtf(y));
+    if (__float_as_uint(rcp_nrm(y)) != __float_as_uint(ref) || __float_as_uint(inv_len_nrm(y)) != il ||
+        __float_as_uint(inv_len_unit(y)) != il) {
       atomicAdd(&g_bad[1], 1ull);
       atomicMin(&g_first[1], (uint32_t)u);
     }
@@ -105,7 +108,7 @@ int main() {
   unsigned int first[4];
   (void)hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad));
   (void)hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first));
-  const char* names[4] = {"sqrt_nrm", "rcp_nrm/inv_len_nrm", "div_nrm", "inv_len (all 2^32)"};
+  const char* names[4] = {"sqrt_nrm", "rcp_nrm/inv_len_nrm/inv_len_unit", "div_nrm", "inv_len (all 2^32)"};
   int rc = 0;
   for (int i = 0; i < 4; ++i) {
     std::printf("%s: %llu mismatches%s", names[i], bad[i], bad[i] ? "" : "\n");
