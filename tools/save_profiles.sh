@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# Copy one tools/gpu_round.sh session's summaries from gpurun_out/<run>/ into profiles/<tag>_* (the
+# tracked evidence bench.py's roofline reads: r*_pmc_<wl>_trace.json, r*_sq_<wl>_trace.json).
+#   usage: tools/save_profiles.sh <run> <tag> <workload> ...
+set -euo pipefail
+cd "$(dirname "$0")/.."
+run=gpurun_out/$1; tag=$2; shift 2
+for wl in "$@"; do
+  tail -1 $run/bench_$wl.json > profiles/${tag}_bench_$wl.json
+  [ -f $run/bench_${wl}_stages.json ] && tail -1 $run/bench_${wl}_stages.json > profiles/${tag}_bench_${wl}_stages.json
+  cp $run/summary_$wl.txt profiles/${tag}_summary_$wl.txt
+  cp $run/stats_$wl/run_kernel_stats.csv profiles/${tag}_kernel_stats_$wl.csv
+  cp $run/pmc_${wl}_trace.json profiles/${tag}_pmc_${wl}_trace.json
+  if [ -f $run/sq_${wl}_trace.json ]; then
+    cp $run/sq_${wl}_trace.json profiles/${tag}_sq_${wl}_trace.json
+    cp $run/sq_$wl.txt profiles/${tag}_sq_$wl.txt
+  fi
+done
+ls profiles/${tag}_*
