@@ -294,15 +294,69 @@ __global__ void k_depth4(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_
   }
 }
 
-__device__ __forceinline__ void put_child(Bvh4Node& o, int k, float lx, float hx, float ly, float hy, float lz, float hz,
+struct Box4 {
+  float lo[3][4], hi[3][4];
+  uint32_t link[4];
+};
+__device__ __forceinline__ void put_child(Box4& o, int k, float lx, float hx, float ly, float hy, float lz, float hz,
                                           uint32_t link) {
-  reinterpret_cast<float*>(&o.lox)[k] = lx;
-  reinterpret_cast<float*>(&o.hix)[k] = hx;
-  reinterpret_cast<float*>(&o.loy)[k] = ly;
-  reinterpret_cast<float*>(&o.hiy)[k] = hy;
-  reinterpret_cast<float*>(&o.loz)[k] = lz;
-  reinterpret_cast<float*>(&o.hiz)[k] = hz;
-  reinterpret_cast<uint32_t*>(&o.link)[k] = link;
+  o.lo[0][k] = lx;
+  o.hi[0][k] = hx;
+  o.lo[1][k] = ly;
+  o.hi[1][k] = hy;
+  o.lo[2][k] = lz;
+  o.hi[2][k] = hz;
+  o.link[k] = link;
+}
+
+// Quantise the n child boxes of one BVH4 node (Bvh4Node): per axis, org = the smallest lower
+// plane, step 2^e the smallest power of two (e in [-100, 60]) with extent <= 255 * 2^e, qlo =
+// floor((lo - org) / 2^e) and qhi = ceil((hi - org) / 2^e) evaluated in double (exact for the
+// scene's float coordinates), so the decoded box always contains the child box.
+__device__ __forceinline__ Bvh4Node quantize4(const Box4& b, int n, uint32_t parent) {
+  Bvh4Node o;
+  float org[3];
+  uint32_t ex = (uint32_t)n << 24, qlo[3] = {0u, 0u, 0u}, qhi[3] = {0u, 0u, 0u};
+  for (int a = 0; a < 3; ++a) {
+    float mn = b.lo[a][0], mx = b.hi[a][0];
+    for (int k = 1; k < n; ++k) {
+      mn = fminf(mn, b.lo[a][k]);
+      mx = fmaxf(mx, b.hi[a][k]);
+    }
+    org[a] = mn;
+    const double ext = (double)mx - (double)mn;
+    int e = -100;
+    if (ext > 0.0) {
+      int x;
+      (void)frexp(ext / 255.0, &x);  // ext / 255 in (2^(x-1), 2^x]
+      e = x;
+      if (ext <= 255.0 * ldexp(1.0, e - 1)) --e;
+      e = e < -100 ? -100 : (e > 60 ? 60 : e);
+    }
+    ex |= (uint32_t)(e + 127) << (8 * a);
+    const double inv_step = ldexp(1.0, -e);
+    for (int k = 0; k < n; ++k) {
+      double l = floor(((double)b.lo[a][k] - (double)mn) * inv_step), h = ceil(((double)b.hi[a][k] - (double)mn) * inv_step);
+      l = l < 0.0 ? 0.0 : (l > 255.0 ? 255.0 : l);
+      h = h < 0.0 ? 0.0 : (h > 255.0 ? 255.0 : h);
+      qlo[a] |= (uint32_t)l << (8 * k);
+      qhi[a] |= (uint32_t)h << (8 * k);
+    }
+  }
+  o.ox = org[0];
+  o.oy = org[1];
+  o.oz = org[2];
+  o.ex = ex;
+  o.qlox = qlo[0];
+  o.qhix = qhi[0];
+  o.qloy = qlo[1];
+  o.qhiy = qhi[1];
+  o.qloz = qlo[2];
+  o.qhiz = qhi[2];
+  o.parent = parent;
+  o.pad = 0u;
+  o.link = make_uint4(b.link[0], b.link[1], b.link[2], b.link[3]);
+  return o;
 }
 
 // BVH4 collapse, pass 2: node i (kept) -> BVH4 node idx[i]; an internal child (odd depth, not kept)
@@ -311,9 +365,11 @@ __global__ void k_collapse4(int N, const BvhNode* nodes, const uint32_t* keep, c
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
     if (!keep[i]) continue;
     const BvhNode nd = nodes[i];
-    Bvh4Node o;
-    o.link = make_uint4(kNoHit, kNoHit, kNoHit, kNoHit);
-    o.lox = o.hix = o.loy = o.hiy = o.loz = o.hiz = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    Box4 o;
+    for (int k = 0; k < 4; ++k) {
+      o.link[k] = kNoHit;
+      for (int a = 0; a < 3; ++a) o.lo[a][k] = o.hi[a][k] = 0.0f;
+    }
     int k = 0;
     const uint32_t links[2] = {nd.link.x, nd.link.y};
     for (int side = 0; side < 2; ++side) {
@@ -333,8 +389,7 @@ __global__ void k_collapse4(int N, const BvhNode* nodes, const uint32_t* keep, c
       const uint32_t p1 = nd.link.z;  // odd-depth parent
       par = idx[nodes[p1].link.z];    // its parent is kept
     }
-    o.meta = make_uint4(par, (uint32_t)k, 0u, 0u);
-    out[idx[i]] = o;
+    out[idx[i]] = quantize4(o, k, par);
   }
 }
 

@@ -421,8 +421,41 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
   return hit;
 }
 
-// BVH4 traversal: four slab tests per 128-B node; leaf children are tested as soon as their box is
-// hit; the nearest internal child is visited next and the other hit children are pushed.
+// One axis of a quantised BVH4 node (Bvh4Node) in the ray's frame: the plane org + q * 2^e maps to
+// t = q * A + B with A = 2^e * inv (exact) and B = (org - o) * inv.  The fma evaluation errs by at
+// most ~2^-22 (|B| + 255 |A|) against (plane - o) * inv; the pad of 2^-20 (|B| + 256 |A|) pushes
+// near planes down and far planes up by more than that, so the decoded slab contains the exact
+// one.  qn / qf: the plane bytes that are near / far for this ray direction.
+struct QAxis {
+  float A, Bn, Bf;
+  uint32_t qn, qf;
+};
+__device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, uint32_t qlo, uint32_t qhi, float ro, float inv) {
+  QAxis a;
+  a.A = __uint_as_float(ebyte << 23) * inv;
+  const float B = (org - ro) * inv;
+  const float pad = __builtin_fmaf(fabsf(a.A), 256.0f, fabsf(B)) * 0x1p-20f;
+  a.Bn = B - pad;
+  a.Bf = B + pad;
+  const bool pos = inv >= 0.0f;
+  a.qn = pos ? qlo : qhi;
+  a.qf = pos ? qhi : qlo;
+  return a;
+}
+__device__ __forceinline__ float q_byte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
+template <int K>
+__device__ __forceinline__ bool q_slab(const QAxis& x, const QAxis& y, const QAxis& z, float tnear, float tfar, float& tent) {
+  const float tnx = __builtin_fmaf(q_byte(x.qn, K), x.A, x.Bn), tfx = __builtin_fmaf(q_byte(x.qf, K), x.A, x.Bf);
+  const float tny = __builtin_fmaf(q_byte(y.qn, K), y.A, y.Bn), tfy = __builtin_fmaf(q_byte(y.qf, K), y.A, y.Bf);
+  const float tnz = __builtin_fmaf(q_byte(z.qn, K), z.A, z.Bn), tfz = __builtin_fmaf(q_byte(z.qf, K), z.A, z.Bf);
+  const float tmin = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tnear));
+  const float tmax = fminf(fminf(tfx, tfy), fminf(tfz, tfar));
+  tent = tmin;
+  return tmin <= tmax * 1.00000095f;
+}
+
+// BVH4 traversal: four slab tests per 64-B quantised node; leaf children are tested as soon as their
+// box is hit; the nearest internal child is visited next and the other hit children are pushed.
 template <bool kAny, bool kCount>
 __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t* prim_ref, const float4* tris,
                                           const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
@@ -435,15 +468,19 @@ __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t*
   uint32_t cur = root;
   bool hit = false;
   for (;;) {
-    const Bvh4Node* nd = nodes + cur;
-    const float4 lx = nd->lox, hx = nd->hix, ly = nd->loy, hy = nd->hiy, lz = nd->loz, hz = nd->hiz;
-    const uint4 ln = nd->link;
+    const uint4* nq = reinterpret_cast<const uint4*>(nodes + cur);
+    const uint4 h0 = nq[0], h1 = nq[1];
+    const uint2 h2 = *reinterpret_cast<const uint2*>(nq + 2);
+    const uint4 ln = nq[3];
     if (kCount) ++vc.nodes;
+    const QAxis ax = q_axis(__uint_as_float(h0.x), h0.w & 0xFFu, h1.x, h1.y, r.o.x, r.inv.x);
+    const QAxis ay = q_axis(__uint_as_float(h0.y), (h0.w >> 8) & 0xFFu, h1.z, h1.w, r.o.y, r.inv.y);
+    const QAxis az = q_axis(__uint_as_float(h0.z), (h0.w >> 16) & 0xFFu, h2.x, h2.y, r.o.z, r.inv.z);
     float t0, t1, t2, t3;
-    bool h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tnear, tfar, t0) && ln.x != kNoHit;
-    bool h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tnear, tfar, t1) && ln.y != kNoHit;
-    bool h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tnear, tfar, t2) && ln.z != kNoHit;
-    bool h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tnear, tfar, t3) && ln.w != kNoHit;
+    bool h0_ = q_slab<0>(ax, ay, az, tnear, tfar, t0) && ln.x != kNoHit;
+    bool h1_ = q_slab<1>(ax, ay, az, tnear, tfar, t1) && ln.y != kNoHit;
+    bool h2_ = q_slab<2>(ax, ay, az, tnear, tfar, t2) && ln.z != kNoHit;
+    bool h3_ = q_slab<3>(ax, ay, az, tnear, tfar, t3) && ln.w != kNoHit;
     uint32_t c0 = ln.x, c1 = ln.y, c2 = ln.z, c3 = ln.w;
 #define SPTR_LEAF4(H, C)                                                                      \
   if (H && (C & kLeafBit)) {                                                                  \
@@ -453,24 +490,24 @@ __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t*
     }                                                                                         \
     H = false;                                                                                \
   }
-    SPTR_LEAF4(h0, c0)
-    SPTR_LEAF4(h1, c1)
-    SPTR_LEAF4(h2, c2)
-    SPTR_LEAF4(h3, c3)
+    SPTR_LEAF4(h0_, c0)
+    SPTR_LEAF4(h1_, c1)
+    SPTR_LEAF4(h2_, c2)
+    SPTR_LEAF4(h3_, c3)
 #undef SPTR_LEAF4
-    if (h0 || h1 || h2 || h3) {
+    if (h0_ || h1_ || h2_ || h3_) {
       // continue with the nearest hit child (lowest slot on ties); push the others, farthest last-in
-      float tn = h0 ? t0 : __builtin_huge_valf();
+      float tn = h0_ ? t0 : __builtin_huge_valf();
       uint32_t cn = c0, kn = 0u;
-      if (h1 && (!h0 || t1 < tn)) { tn = t1; cn = c1; kn = 1u; }
-      if (h2 && ((!h0 && !h1) || t2 < tn)) { tn = t2; cn = c2; kn = 2u; }
-      if (h3 && ((!h0 && !h1 && !h2) || t3 < tn)) { tn = t3; cn = c3; kn = 3u; }
-      const uint32_t npush = (h0 && kn != 0u) + (h1 && kn != 1u) + (h2 && kn != 2u) + (h3 && kn != 3u);
+      if (h1_ && (!h0_ || t1 < tn)) { tn = t1; cn = c1; kn = 1u; }
+      if (h2_ && ((!h0_ && !h1_) || t2 < tn)) { tn = t2; cn = c2; kn = 2u; }
+      if (h3_ && ((!h0_ && !h1_ && !h2_) || t3 < tn)) { tn = t3; cn = c3; kn = 3u; }
+      const uint32_t npush = (h0_ && kn != 0u) + (h1_ && kn != 1u) + (h2_ && kn != 2u) + (h3_ && kn != 3u);
       if (sp + (int)npush > kStack) vc.stack_overflow = 1u;
-      if (h3 && kn != 3u && sp < kStack) stack.put(sp++, c3);
-      if (h2 && kn != 2u && sp < kStack) stack.put(sp++, c2);
-      if (h1 && kn != 1u && sp < kStack) stack.put(sp++, c1);
-      if (h0 && kn != 0u && sp < kStack) stack.put(sp++, c0);
+      if (h3_ && kn != 3u && sp < kStack) stack.put(sp++, c3);
+      if (h2_ && kn != 2u && sp < kStack) stack.put(sp++, c2);
+      if (h1_ && kn != 1u && sp < kStack) stack.put(sp++, c1);
+      if (h0_ && kn != 0u && sp < kStack) stack.put(sp++, c0);
       cur = cn;
     } else {
       if (sp == 0) break;
@@ -493,7 +530,8 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
   Staged s{sv.nodes, sv.nodes4, sv.prim_ref, sv.tris, sv.sph};
   if (kLds) {
     const bool w4 = sv.width == 4u;
-    const uint32_t nn = w4 ? sv.num_nodes4 * 8u : sv.num_nodes * 4u, nt = sv.num_tris * 3u, ns = sv.num_sph;
+    const uint32_t nn = (w4 ? sv.num_nodes4 * (uint32_t)sizeof(Bvh4Node) : sv.num_nodes * (uint32_t)sizeof(BvhNode)) / 16u,
+                   nt = sv.num_tris * 3u, ns = sv.num_sph;
     const uint32_t np = (sv.num_tris + sv.num_sph + 3u) / 4u;  // prim refs, in float4 units
     const float4* gn = w4 ? reinterpret_cast<const float4*>(sv.nodes4) : reinterpret_cast<const float4*>(sv.nodes);
     const float4* gp = reinterpret_cast<const float4*>(sv.prim_ref);

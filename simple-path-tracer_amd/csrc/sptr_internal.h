@@ -58,12 +58,19 @@ static_assert(sizeof(BvhNode) == 64, "node size");
 // BVH4 node, 128 B (one cache line): four child boxes stored SoA so the four slab tests vectorise,
 // four child links (BVH4 node index, leaf range, or kNoHit for an empty slot).  Built by collapsing
 // the LBVH: the BVH2 nodes at even depth become BVH4 nodes whose children are their grandchildren.
-struct Bvh4Node {
-  float4 lox, hix, loy, hiy, loz, hiz;
+// BVH4 node, 64 B (half a 128-B cache line): the four child boxes quantised to 8 bits per plane on
+// a per-node, per-axis power-of-two grid anchored at the node's lower corner (org).  Child k's box
+// is [org + qlo_k * 2^e, org + qhi_k * 2^e] per axis, rounded outwards at build time (k_collapse4),
+// so it contains the exact child box; traverse4 decodes the planes in the ray's frame with an error
+// pad, so the test stays conservative.  Byte k of each q word belongs to child k.
+struct alignas(16) Bvh4Node {
+  float ox, oy, oz;
+  uint32_t ex;                     // biased exponent bytes of the x / y / z grid steps; byte 3: child count
+  uint32_t qlox, qhix, qloy, qhiy;
+  uint32_t qloz, qhiz, parent, pad;  // parent: BVH4 index (build bookkeeping, not traversed)
   uint4 link;
-  uint4 meta;  // parent (BVH4 index), child count, -, -
 };
-static_assert(sizeof(Bvh4Node) == 128, "node size");
+static_assert(sizeof(Bvh4Node) == 64, "node size");
 
 struct DevMaterial {  // == sptr_material
   float albedo[3];
