@@ -41,8 +41,11 @@
 #define SPTR_TAIL_WAVES 1
 #endif
 #ifndef SPTR_SHADOW_WAVES
-#define SPTR_SHADOW_WAVES 6  // C5 (BVH4 from HBM): 5 -> 6 waves, shadow 8.34 -> 7.19 ms/step; 7 waves
-#endif                       // spills more and loses it again (8.06)
+#define SPTR_SHADOW_WAVES 6  // LDS-staged BVH2 scenes: 7 waves measured slower on C2 (0.409 -> 0.426 ms)
+#endif
+#ifndef SPTR_SHADOW4_WAVES
+#define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
+#endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
 
 namespace sptr {
 
@@ -725,7 +728,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // resumes there (accum.w = resume slot).  A kernel of its own (not a branch of k_trace), so that
 // its registers are allocated for this loop alone.
 template <bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE_PM_WAVES)
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_PM_WAVES)
     k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
@@ -799,7 +802,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TRACE_PM_WAVES)
 // 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 template <bool kLds, bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE_WAVES)
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
@@ -1210,7 +1213,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount, bool kW4>
-__global__ void __launch_bounds__(kBlock, SPTR_SHADOW_WAVES) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW_WAVES) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
@@ -2033,6 +2036,7 @@ SceneView scene_view(const Context& c) {
   const uint64_t bytes = node_bytes + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
+  s.scene_bytes = bytes;
   return s;
 }
 
@@ -2054,7 +2058,7 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
 #ifdef SPTR_EXPERIMENT_KNOBS
   if (const char* e = getenv("SPTR_FOLD")) {  // timing experiments: force kFoldNone/Thread/Wave
     const uint32_t m = (uint32_t)atoi(e);
-    if (m == kFoldNone || (sv.lds_bytes != 0 && (m == kFoldThread || (m == kFoldWave && f.k >= kWaveFoldMinK)))) return m;
+    if (m == kFoldNone || (m == kFoldWave && f.k >= kWaveFoldMinK) || (m == kFoldThread && sv.lds_bytes != 0)) return m;
   }
 #endif
   if (sv.lds_bytes != 0) {
@@ -2070,9 +2074,10 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
         ((uint64_t)f.P >= threads * 2u * kPixelMajorItems || f.k <= kPixelMajorMaxK))
       return kFoldThread;
   }
-  // L2/HBM scenes stay path-major: measured on MI355X (r02l), the lane-group kernel's fold state
-  // costs the BVH4 traversal its registers (33 VGPR spills at 7 waves) and more than the saved
-  // radiance round trip (C3 trace0 + k_accum 10.0 -> 10.9 ms, C5 7.3 -> 10.6 ms)
+  // L2/HBM scenes stay path-major.  Lane groups at the BVH4 occupancy (r02, production build):
+  // C3 trace0 8.07 -> 10.41 ms against k_accum 1.47 -> 0.07 ms, 12.18 -> 13.08 ms/step; C5
+  // 23.3 -> 24.1 ms/step (knobs build).  The fold's per-round shuffles and fold state cost the
+  // BVH4 traversal more than the radiance round trip it saves.
   return (sv.lds_bytes != 0 && f.k >= kWaveFoldMinK) ? kFoldWave : kFoldNone;
 }
 

@@ -102,6 +102,7 @@ struct SceneView {
   uint32_t num_nodes4, root4;
   uint32_t width;      // 2: BVH2 traversal, 4: BVH4 traversal
   uint32_t lds_bytes;  // 0: traverse from global memory
+  uint64_t scene_bytes;  // traversed nodes + triangles + spheres + refs
 };
 
 struct EnvView {

@@ -97,6 +97,33 @@ def test_c3_chair_hdr_vs_oracle(renderer):
     renderer.set_environment(None)
 
 
+def test_c3_batches_bit_exact(renderer):
+    """C3's L2-resident BVH4 + cubemap in one 32-sample batch: bit-identical to 8-sample batches
+    (and, with the experiment knob SPTR_FOLD=2, the non-LDS lane-group kernel k_trace_wp), and close
+    to the oracle."""
+    wl = workloads.WORKLOADS["c3"]
+    faces = workloads.hdr_env_faces()
+    flat = sptr.setup_default(renderer, wl.scene, wl.p0, wl.p1, env_faces=faces)
+    W, H, S = 96, 64, 32
+    cam = sptr.camera_lookat(aspect=W / H)
+    st = renderer.render(cam, W, H, spp=S)
+    assert st.waves == 1
+    acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
+    renderer.set_wave_paths(3 * 2 * 1024 * 8)
+    try:
+        st8 = renderer.render(cam, W, H, spp=S)
+    finally:
+        renderer.set_wave_paths(0)
+    assert st8.waves == S // 8
+    assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
+    assert np.array_equal(rgb, renderer.read_rgb8())
+    P = oracle.Prepared(_flat_dict(flat), bvh=True)
+    oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
+                                frames=S, env_faces=faces, threads=THREADS)
+    _image_close(rgb, orgb, acc, oacc)
+    renderer.set_environment(None)
+
+
 # --------------------------------------------------------------------------------------------- C4
 @pytest.fixture(scope="module")
 def c4_frame(renderer):
