@@ -343,39 +343,49 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
 // wave's pushes at equal depth hit 64 distinct banks); deeper entries spill to a private array
 // (scratch), which only very deep traversals touch.  Scratch-only stacks put a ~500-cycle
 // dependent load on every pop.
-constexpr int kLdsStack = 12;
-#ifdef SPTR_EXPERIMENT_NO_SPILL  // timing experiment only: drops pushes beyond kLdsStack (wrong hits)
+constexpr int kLdsStack = 12;  // kernels that also stage the scene in LDS
+#ifndef SPTR_LDS_STACK_G
+#define SPTR_LDS_STACK_G 12
+#endif
+constexpr int kLdsStackG = SPTR_LDS_STACK_G;  // kernels traversing from L2/HBM (LDS holds only the stack)
+#ifdef SPTR_EXPERIMENT_NO_SPILL  // timing experiment only: drops pushes beyond the LDS part (wrong hits)
+template <int N>
 struct TravStack {
   uint32_t* lds;
   __device__ __forceinline__ void put(int i, uint32_t v) {
-    if (i < kLdsStack) lds[i * kBlock] = v;
+    if (i < N) lds[i * kBlock] = v;
   }
-  __device__ __forceinline__ uint32_t get(int i) const { return i < kLdsStack ? lds[i * kBlock] : 0u; }
+  __device__ __forceinline__ uint32_t get(int i) const { return i < N ? lds[i * kBlock] : 0u; }
 };
 #else
+template <int N>
 struct TravStack {
   uint32_t* lds;  // &s_stack[0][threadIdx.x]
-  uint32_t spill[kStack - kLdsStack];
+  uint32_t spill[kStack - N];
   __device__ __forceinline__ void put(int i, uint32_t v) {
-    if (i < kLdsStack) lds[i * kBlock] = v;
-    else spill[i - kLdsStack] = v;
+    if (i < N) lds[i * kBlock] = v;
+    else spill[i - N] = v;
   }
-  __device__ __forceinline__ uint32_t get(int i) const { return i < kLdsStack ? lds[i * kBlock] : spill[i - kLdsStack]; }
+  __device__ __forceinline__ uint32_t get(int i) const { return i < N ? lds[i * kBlock] : spill[i - N]; }
 };
 #endif
-struct alignas(16) LdsStack {
-  uint32_t e[kLdsStack][kBlock];
+template <int N>
+struct alignas(16) LdsStackN {
+  uint32_t e[N][kBlock];
 };
-static_assert(sizeof(LdsStack) % 16 == 0, "keeps the dynamic-LDS base aligned");
+using LdsStack = LdsStackN<kLdsStack>;
+template <bool kLds>
+using KernelStack = LdsStackN<kLds ? kLdsStack : kLdsStackG>;
+static_assert(sizeof(LdsStack) % 16 == 0 && sizeof(LdsStackN<kLdsStackG>) % 16 == 0, "keeps the dynamic-LDS base aligned");
 
 // BVH2 stack traversal: nearest child first; leaf children are tested as soon as their box is hit.
-template <bool kAny, bool kCount>
+template <bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* prim_ref, const float4* tris,
                                          const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                         uint32_t& ref, Visits& vc, LdsStack& ls) {
+                                         uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
   if (root == kNoHit) return false;
   if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-  TravStack stack;
+  TravStack<N> stack;
   stack.lds = &ls.e[0][threadIdx.x];
   int sp = 0;
   uint32_t cur = root;
@@ -459,13 +469,13 @@ __device__ __forceinline__ bool q_slab(const QAxis& x, const QAxis& y, const QAx
 
 // BVH4 traversal: four slab tests per 64-B quantised node; leaf children are tested as soon as their
 // box is hit; the nearest internal child is visited next and the other hit children are pushed.
-template <bool kAny, bool kCount>
+template <bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t* prim_ref, const float4* tris,
                                           const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                          uint32_t& ref, Visits& vc, LdsStack& ls) {
+                                          uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
   if (root == kNoHit) return false;
   if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-  TravStack stack;
+  TravStack<N> stack;
   stack.lds = &ls.e[0][threadIdx.x];
   int sp = 0;
   uint32_t cur = root;
@@ -552,9 +562,9 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
   return s;
 }
 
-template <bool kW4, bool kAny, bool kCount>
+template <bool kW4, bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv, const Ray& r, float tnear, float& tfar,
-                                           uint32_t& ref, Visits& vc, LdsStack& ls) {
+                                           uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
   if (kW4) return traverse4<kAny, kCount>(sc.nodes4, sc.prim_ref, sc.tris, sc.sph, sv.root4, r, tnear, tfar, ref, vc, ls);
   return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
 }
@@ -805,7 +815,7 @@ template <bool kLds, bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   if (threadIdx.x == 0) s_cnt = 0u;
@@ -881,7 +891,7 @@ template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
   const FrameView f = frame_dyn(fin);
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
@@ -1104,15 +1114,28 @@ __device__ __forceinline__ uint32_t stage_materials(const ShadeView& sh, DevMate
 // one shadow record per path with >= 1 lit light: L tasks {origin.xyz, tfar} {contrib.xyz, p}
 // [{dir.xyz}] (valid = contrib slot w != 0 is encoded by p+1; the direction slot exists only when a
 // point light is present).
-template <bool kPrimary>
+//
+// kFuse (LDS-staged scenes with one light): the shadow ray is traced in place instead — the scene is
+// staged into LDS next to the segment table, the lit light's any-hit query runs in this thread and
+// its contribution is added to the radiance held in registers after the emission, exactly the
+// update k_shadow would make next (Light::isOccluded), without the shadow-task stream, the
+// radiance round trip and one launch per bounce.  Any-hit queries are tallied per block in bstat,
+// as k_shadow does.
+constexpr int kFuseStack = 6;  // LDS part of the in-shade traversal stack (C2's BVH2 is 9 deep)
+template <bool kPrimary, bool kFuse>
 __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     k_shade(SceneView sv, ShadeView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
   const FrameView f = frame_dyn(fin);
-  extern __shared__ uint32_t s_off[];
+  extern __shared__ float4 lds[];
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kFuse ? sv.lds_bytes / 16u : 0u));
   __shared__ DevMaterial smat[32];
-  __shared__ uint32_t s_cnt_n, s_cnt_s;
+  __shared__ uint32_t s_cnt_n, s_cnt_s, s_rays;
+  __shared__ LdsStackN<kFuse ? kFuseStack : 1> s_stack;
   const uint32_t nm = stage_materials(sh, smat);
-  if (threadIdx.x == 0) s_cnt_n = s_cnt_s = 0u;
+  if (threadIdx.x == 0) s_cnt_n = s_cnt_s = s_rays = 0u;
+  const Staged sc = stage_scene<kFuse>(sv, lds);
+  Visits vc;
+  uint32_t rays = 0u;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segH, nseg_in, s_off, per_in);
 
@@ -1163,7 +1186,17 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
           if (light_faces(sh.lights[li], sf)) shadow = true;
       }
     }
-    const uint32_t js = block_append(&s_cnt_s, shadow);
+    // kFuse (one light): the shadow ray's query is prepared now, with the throughput before the
+    // continuation, and traced after the continuation ray is written, so that little state lives
+    // across the traversal
+    vec3 so, ldir, contrib;
+    float stfar = 0.0f;
+    bool lit = false;
+    if (kFuse) {
+      if (shadow) lit = light_term(sh.lights[0], sf, -rd, thr, so, ldir, stfar, contrib);
+      shadow = false;
+    }
+    const uint32_t js = kFuse ? 0u : block_append(&s_cnt_s, shadow);
     if (shadow && sd.seg0 + js >= w.seg_cap) {
       shadow = false;
       w.tot[kTotOverflow] = 1ull;
@@ -1185,7 +1218,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       }
     }
     if (active && sh.debug_mode != 1) cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
-    if (active && dirty) w.rad[p] = f4(radv, 0.0f);
+    if (!kFuse && active && dirty) w.rad[p] = f4(radv, 0.0f);
     const uint32_t jn = block_append(&s_cnt_n, cont);
     if (cont && sd.seg0 + jn >= w.seg_cap) {
       cont = false;
@@ -1196,11 +1229,30 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       rout.d[sd.seg0 + jn] = f4(nd, __uint_as_float(p));
       rout.thr[sd.seg0 + jn] = f4(thr, 0.0f);
     }
+    if (kFuse) {
+      if (lit) {
+        const Ray r = make_ray(so, ldir);
+        uint32_t ref = kNoHit;
+        ++rays;
+        if (!traverse_w<false, true, false>(sc, sv, r, 1e-4f, stfar, ref, vc, s_stack)) {
+          if (!dirty) radv = xyz(w.rad[p]);  // kPrimary starts dirty at zero radiance
+          dirty = true;
+          radv = radv + contrib;
+        }
+      }
+      if (active && dirty) w.rad[p] = f4(radv, 0.0f);
+    }
+  }
+  if (kFuse) {
+    for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+    if (lane_id() == 0u) atomicAdd(&s_rays, rays);
+    report_stack(vc, w.tot);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     w.segN.cnt[logical_block()] = s_cnt_n;
     w.segS.cnt[logical_block()] = s_cnt_s;
+    if (kFuse) w.bstat[blockIdx.x] += s_rays;
     if (blockIdx.x == 0) {
       *w.segN.per = sd.per;
       *w.segS.per = sd.per;
@@ -1214,7 +1266,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount, bool kW4>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW_WAVES) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
@@ -1273,7 +1325,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
 template <bool kLds, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
                                                  uint32_t nseg_in) {
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
   __shared__ uint32_t s_rays[2];
@@ -1495,9 +1547,9 @@ __device__ __forceinline__ uint32_t pt_seed(uint32_t ps, uint32_t acc, uint32_t 
   return wang_hash(wang_hash(ps ^ (acc * 9781u)) ^ (s * 0x9E3779B9u + 0x68E31DA4u));
 }
 
-template <bool kW4, bool kCube>
+template <bool kW4, bool kCube, int N>
 __device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& sh, const DevMaterial* smat, uint32_t nm,
-                        vec3 o, vec3 d, uint32_t depth, uint32_t& rng, Visits& vc, LdsStack& ls, uint32_t& n_closest,
+                        vec3 o, vec3 d, uint32_t depth, uint32_t& rng, Visits& vc, LdsStackN<N>& ls, uint32_t& n_closest,
                         uint32_t& n_shadow) {
   vec3 rad = v3(0.0f, 0.0f, 0.0f), thr = v3(1.0f, 1.0f, 1.0f);
   for (uint32_t lvl = 0; lvl < depth; ++lvl) {
@@ -1603,7 +1655,7 @@ __device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 template <bool kLds, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
   const uint32_t nm = stage_materials(sh, smat);
@@ -1692,9 +1744,9 @@ __device__ __forceinline__ vec3 ox_fallback_reflect(vec3 d, vec3 n) {
   return l2 > 0.0f ? R * inv_len(l2) : n;
 }
 
-template <bool kW4, bool kCube>
+template <bool kW4, bool kCube, int N>
 __device__ void ox_path(const Staged& sc, const SceneView& sv, const ShadeView& sh, const DevMaterial* smat, uint32_t nm,
-                        const FrameView& f, vec3 o, vec3 d, uint32_t rng, vec3& acc, Visits& vc, LdsStack& ls,
+                        const FrameView& f, vec3 o, vec3 d, uint32_t rng, vec3& acc, Visits& vc, LdsStackN<N>& ls,
                         uint32_t& n_closest) {
   constexpr float kPi = 3.14159265358979323846f;
   vec3 thr = v3(1.0f, 1.0f, 1.0f);
@@ -1867,7 +1919,7 @@ __device__ void ox_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 template <bool kLds, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
-  __shared__ LdsStack s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
   const uint32_t nm = stage_materials(sh, smat);
@@ -2137,18 +2189,27 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
       Flags<>{}, L, count, P, W, cube);
 }
 
+bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count) {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  if (getenv("SPTR_NO_FUSE")) return false;
+#endif
+  // the visit-count pass keeps k_shadow (shadow visit tallies); several lights keep their task
+  // records (in light order) in the shadow stream; the in-shade traversal is the LDS BVH2 one
+  return sv.lds_bytes != 0 && sv.width == 2u && sh.num_lights == 1u && !count;
+}
+
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
-                      uint32_t nseg, hipStream_t s) {
-  const unsigned lb = (4u * (nseg + 1u) + 15u) / 16u * 16u;
-  unsigned g;
-  if (depth == 0) {
-    g = resident_grid((const void*)&k_shade<true>, lb);
-    hipLaunchKernelGGL(k_shade<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
-  } else {
-    g = resident_grid((const void*)&k_shade<false>, lb);
-    hipLaunchKernelGGL(k_shade<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
-  }
-  return g;
+                      uint32_t nseg, bool fuse, hipStream_t s) {
+  const unsigned lb = (fuse ? sv.lds_bytes : 0u) + (4u * (nseg + 1u) + 15u) / 16u * 16u;
+  return dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Pc, bool Fc>(Flags<Pc, Fc>) {
+          const unsigned g = resident_grid((const void*)&k_shade<Pc, Fc>, lb);
+          hipLaunchKernelGGL((k_shade<Pc, Fc>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, depth == 0, fuse);
 }
 
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count,

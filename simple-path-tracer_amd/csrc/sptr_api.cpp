@@ -425,6 +425,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
+  const bool fuse = shade_fuses_shadows(sv, sh, count);
   tm.begin_call();
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
@@ -448,11 +449,13 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
       tm.begin(d == 0 ? 6 : 2);
-      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, s);
+      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
       tm.end();
-      tm.begin(3);
-      launch_shadow(sv, sh, w, d, count, g_shade, s);
-      tm.end();
+      if (!fuse) {
+        tm.begin(3);
+        launch_shadow(sv, sh, w, d, count, g_shade, s);
+        tm.end();
+      }
     }
     tm.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), s);

@@ -290,8 +290,10 @@ SceneView scene_view(const Context& c);
 // Stage launchers return their (resident) grid size: the segment count their consumer scans.
 unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth, bool count,
                   uint32_t nseg_in, hipStream_t s);
+// k_shade traces the shadow ray in place (LDS-staged one-light scenes outside the visit-count pass)
+bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count);
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
-                  uint32_t nseg_in, hipStream_t s);
+                      uint32_t nseg, bool fuse, hipStream_t s);
 unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth0,
                      uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,

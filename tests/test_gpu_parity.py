@@ -431,3 +431,19 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
         assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
         assert (a[1], a[2]) == (b[1], b[2])
         assert b[5] > 0.0  # the call span's events were re-pointed and recorded on replay
+
+
+@pytest.mark.parametrize("scene", ["default", "default_emitter"])
+def test_fused_shadow_equals_shadow_stage(renderer, scene):
+    """LDS-staged one-light scenes trace the shadow ray inside k_shade; the visit-count pass keeps the
+    separate k_shadow stage.  Both must accumulate the same bits and count the same any-hit queries
+    (the in-shade query adds its contribution after the emission, as k_shadow's update does)."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, scene)
+    st = renderer.render(cam, W, H, spp=6)
+    fused = renderer.read_accum().copy()
+    st2 = renderer.render(cam, W, H, spp=6, flags=sptr.SPTR_FRAME_COUNT_VISITS)
+    assert st2.shadow_node_visits > 0  # the separate stage ran
+    assert np.array_equal(fused.view(np.uint32), renderer.read_accum().view(np.uint32))
+    assert (st.rays_closest, st.rays_shadow) == (st2.rays_closest, st2.rays_shadow)
