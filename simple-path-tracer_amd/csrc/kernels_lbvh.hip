@@ -11,8 +11,9 @@
 //   k_refit       : bottom-up box propagation; the second child to arrive at a node finishes it
 //                   (agent-scope release/acquire, write-through box stores — the hand-off recipe of
 //                   the gfx950 guide, Guideline 16)
-//   k_depth4 + scan + k_collapse4 : BVH4 — every reachable BVH2 node at even depth becomes a
-//                   BVH4 node whose (up to four) children are its grandchildren; leaves stay ranges
+//   k_depth_wide + scan + k_collapse_wide : wide BVH (4 or 8 children) — every reachable BVH2 node
+//                   at a depth that is a multiple of kWideLevels becomes a wide node whose children
+//                   are its descendants kWideLevels levels down; leaves stay ranges
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -277,9 +278,9 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
   }
 }
 
-// BVH4 collapse, pass 1: keep[i] = 1 for BVH2 nodes that are reachable through internal links
-// (covering more than leaf_max primitives) and lie at even depth.
-__global__ void k_depth4(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep) {
+// Wide collapse, pass 1: keep[i] = 1 for BVH2 nodes that are reachable through internal links
+// (covering more than leaf_max primitives) and lie at a depth that is a multiple of kWideLevels.
+__global__ void k_depth_wide(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
     uint32_t k = 0u;
     if (nodes[i].link.w > leaf_max) {
@@ -288,35 +289,27 @@ __global__ void k_depth4(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_
         q = nodes[q].link.z;
         ++dep;
       }
-      k = (dep & 1u) ? 0u : 1u;
+      k = (dep % (uint32_t)kWideLevels) ? 0u : 1u;
     }
     keep[i] = k;
   }
 }
 
-struct Box4 {
-  float lo[3][4], hi[3][4];
-  uint32_t link[4];
+struct WideBoxes {
+  float lo[3][kWide], hi[3][kWide];
+  uint32_t link[kWide];
 };
-__device__ __forceinline__ void put_child(Box4& o, int k, float lx, float hx, float ly, float hy, float lz, float hz,
-                                          uint32_t link) {
-  o.lo[0][k] = lx;
-  o.hi[0][k] = hx;
-  o.lo[1][k] = ly;
-  o.hi[1][k] = hy;
-  o.lo[2][k] = lz;
-  o.hi[2][k] = hz;
-  o.link[k] = link;
-}
 
-// Quantise the n child boxes of one BVH4 node (Bvh4Node): per axis, org = the smallest lower
+// Quantise the n child boxes of one wide node (WideNode): per axis, org = the smallest lower
 // plane, step 2^e the smallest power of two (e in [-100, 60]) with extent <= 255 * 2^e, qlo =
 // floor((lo - org) / 2^e) and qhi = ceil((hi - org) / 2^e) evaluated in double (exact for the
 // scene's float coordinates), so the decoded box always contains the child box.
-__device__ __forceinline__ Bvh4Node quantize4(const Box4& b, int n, uint32_t parent) {
-  Bvh4Node o;
+__device__ __forceinline__ WideNode quantize_wide(const WideBoxes& b, int n, uint32_t parent) {
+  WideNode o;
   float org[3];
-  uint32_t ex = (uint32_t)n << 24, qlo[3] = {0u, 0u, 0u}, qhi[3] = {0u, 0u, 0u};
+  uint32_t ex = (uint32_t)n << 24;
+  for (int w = 0; w < 6; ++w)
+    for (int j = 0; j < kQWords; ++j) o.q[w][j] = 0u;
   for (int a = 0; a < 3; ++a) {
     float mn = b.lo[a][0], mx = b.hi[a][0];
     for (int k = 1; k < n; ++k) {
@@ -339,57 +332,83 @@ __device__ __forceinline__ Bvh4Node quantize4(const Box4& b, int n, uint32_t par
       double l = floor(((double)b.lo[a][k] - (double)mn) * inv_step), h = ceil(((double)b.hi[a][k] - (double)mn) * inv_step);
       l = l < 0.0 ? 0.0 : (l > 255.0 ? 255.0 : l);
       h = h < 0.0 ? 0.0 : (h > 255.0 ? 255.0 : h);
-      qlo[a] |= (uint32_t)l << (8 * k);
-      qhi[a] |= (uint32_t)h << (8 * k);
+      o.q[2 * a][k / 4] |= (uint32_t)l << (8 * (k % 4));
+      o.q[2 * a + 1][k / 4] |= (uint32_t)h << (8 * (k % 4));
     }
   }
   o.ox = org[0];
   o.oy = org[1];
   o.oz = org[2];
   o.ex = ex;
-  o.qlox = qlo[0];
-  o.qhix = qhi[0];
-  o.qloy = qlo[1];
-  o.qhiy = qhi[1];
-  o.qloz = qlo[2];
-  o.qhiz = qhi[2];
+  for (int k = 0; k < kWide; ++k) o.link[k] = b.link[k];
   o.parent = parent;
-  o.pad = 0u;
-  o.link = make_uint4(b.link[0], b.link[1], b.link[2], b.link[3]);
+  for (uint32_t& x : o.pad) x = 0u;
   return o;
 }
 
-// BVH4 collapse, pass 2: node i (kept) -> BVH4 node idx[i]; an internal child (odd depth, not kept)
-// is replaced by its two children, in left-to-right order.
-__global__ void k_collapse4(int N, const BvhNode* nodes, const uint32_t* keep, const uint32_t* idx, Bvh4Node* out) {
+// Wide collapse, pass 2: node i (kept) -> wide node idx[i]; its children are the BVH2 nodes
+// kWideLevels levels down (kept themselves), or the leaf ranges met on the way, in left-to-right
+// order.
+__global__ void k_collapse_wide(int N, const BvhNode* nodes, const uint32_t* keep, const uint32_t* idx, WideNode* out) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
     if (!keep[i]) continue;
+    WideBoxes b;
+    for (int k = 0; k < kWide; ++k) {
+      b.link[k] = kNoHit;
+      for (int a = 0; a < 3; ++a) b.lo[a][k] = b.hi[a][k] = 0.0f;
+    }
+    // level 1: the two children of node i
     const BvhNode nd = nodes[i];
-    Box4 o;
-    for (int k = 0; k < 4; ++k) {
-      o.link[k] = kNoHit;
-      for (int a = 0; a < 3; ++a) o.lo[a][k] = o.hi[a][k] = 0.0f;
-    }
-    int k = 0;
-    const uint32_t links[2] = {nd.link.x, nd.link.y};
-    for (int side = 0; side < 2; ++side) {
-      const uint32_t c = links[side];
-      if (c & kLeafBit) {
-        if (side == 0) put_child(o, k++, nd.lxy.x, nd.lxy.y, nd.lxy.z, nd.lxy.w, nd.z.x, nd.z.y, c);
-        else put_child(o, k++, nd.rxy.x, nd.rxy.y, nd.rxy.z, nd.rxy.w, nd.z.z, nd.z.w, c);
-        continue;
+    int n = 2;
+    b.link[0] = nd.link.x;
+    b.lo[0][0] = nd.lxy.x; b.hi[0][0] = nd.lxy.y; b.lo[1][0] = nd.lxy.z; b.hi[1][0] = nd.lxy.w;
+    b.lo[2][0] = nd.z.x;   b.hi[2][0] = nd.z.y;
+    b.link[1] = nd.link.y;
+    b.lo[0][1] = nd.rxy.x; b.hi[0][1] = nd.rxy.y; b.lo[1][1] = nd.rxy.z; b.hi[1][1] = nd.rxy.w;
+    b.lo[2][1] = nd.z.z;   b.hi[2][1] = nd.z.w;
+    // further levels: every internal entry is replaced by its two children, in place order
+    for (int lev = 1; lev < kWideLevels; ++lev) {
+      WideBoxes nb;
+      int m = 0;
+      for (int e = 0; e < n; ++e) {
+        const uint32_t c = b.link[e];
+        if (c & kLeafBit) {
+          nb.link[m] = c;
+          for (int a = 0; a < 3; ++a) {
+            nb.lo[a][m] = b.lo[a][e];
+            nb.hi[a][m] = b.hi[a][e];
+          }
+          ++m;
+          continue;
+        }
+        const BvhNode cn = nodes[c];
+        nb.link[m] = cn.link.x;
+        nb.lo[0][m] = cn.lxy.x; nb.hi[0][m] = cn.lxy.y; nb.lo[1][m] = cn.lxy.z; nb.hi[1][m] = cn.lxy.w;
+        nb.lo[2][m] = cn.z.x;   nb.hi[2][m] = cn.z.y;
+        ++m;
+        nb.link[m] = cn.link.y;
+        nb.lo[0][m] = cn.rxy.x; nb.hi[0][m] = cn.rxy.y; nb.lo[1][m] = cn.rxy.z; nb.hi[1][m] = cn.rxy.w;
+        nb.lo[2][m] = cn.z.z;   nb.hi[2][m] = cn.z.w;
+        ++m;
       }
-      const BvhNode cn = nodes[c];
-      const uint32_t g0 = cn.link.x, g1 = cn.link.y;
-      put_child(o, k++, cn.lxy.x, cn.lxy.y, cn.lxy.z, cn.lxy.w, cn.z.x, cn.z.y, (g0 & kLeafBit) ? g0 : idx[g0]);
-      put_child(o, k++, cn.rxy.x, cn.rxy.y, cn.rxy.z, cn.rxy.w, cn.z.z, cn.z.w, (g1 & kLeafBit) ? g1 : idx[g1]);
+      for (int e = 0; e < m; ++e) {
+        b.link[e] = nb.link[e];
+        for (int a = 0; a < 3; ++a) {
+          b.lo[a][e] = nb.lo[a][e];
+          b.hi[a][e] = nb.hi[a][e];
+        }
+      }
+      n = m;
     }
+    for (int e = 0; e < n; ++e)
+      if (!(b.link[e] & kLeafBit)) b.link[e] = idx[b.link[e]];  // kept nodes kWideLevels below
     uint32_t par = kNoHit;
     if (i != 0) {
-      const uint32_t p1 = nd.link.z;  // odd-depth parent
-      par = idx[nodes[p1].link.z];    // its parent is kept
+      uint32_t q = (uint32_t)i;
+      for (int l = 0; l < kWideLevels; ++l) q = nodes[q].link.z;
+      par = idx[q];
     }
-    out[idx[i]] = quantize4(o, k, par);
+    out[idx[i]] = quantize_wide(b, n, par);
   }
 }
 
@@ -537,11 +556,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     LB_CHECK(hipStreamSynchronize(s));
     c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;
-    // a BVH2 node at depth d holds at most d pushed entries and pushes one more; a BVH4 node (BVH2
-    // depth 2*d4) holds at most 3*d4 and pushes up to three more; internal nodes lie at BVH2 depth
-    // <= dep - 1
+    // a BVH2 node at depth d holds at most d pushed entries and pushes one more; a wide node (BVH2
+    // depth kWideLevels*dw) holds at most (kWide-1)*dw and pushes up to kWide-1 more; internal nodes
+    // lie at BVH2 depth <= dep - 1
     c.stack_need2 = dep;
-    c.stack_need4 = 3u * ((dep > 0u ? dep - 1u : 0u) / 2u + 1u);
+    c.stack_need4 = (uint32_t)(kWide - 1) * ((dep > 0u ? dep - 1u : 0u) / (uint32_t)kWideLevels + 1u);
     if (c.stack_need2 > (uint32_t)kStack) {
       c.err = "lbvh: tree depth " + std::to_string(dep) + " exceeds the traversal stack";
       return SPTR_ERR_INVALID;
@@ -551,7 +570,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       c.root4 = c.root;
     } else {
       // BVH4: keep flags -> exclusive scan -> collapse (reusing flag/slot scratch arrays)
-      hipLaunchKernelGGL(k_depth4, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag);
+      hipLaunchKernelGGL(k_depth_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag);
       LB_CHECK(hipGetLastError());
       size_t s4 = 0;
       LB_CHECK(rocprim::exclusive_scan(nullptr, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
@@ -563,9 +582,9 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       LB_CHECK(hipMemcpyAsync(&last_slot, slot + (N - 2), 4, hipMemcpyDeviceToHost, s));
       LB_CHECK(hipStreamSynchronize(s));
       c.num_nodes4 = last_slot + last_keep;
-      LB_CHECK(realloc_buf(c.nodes4, (size_t)c.num_nodes4 * sizeof(Bvh4Node)));
-      hipLaunchKernelGGL(k_collapse4, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
-                         static_cast<Bvh4Node*>(c.nodes4.p));
+      LB_CHECK(realloc_buf(c.nodes4, (size_t)c.num_nodes4 * sizeof(WideNode)));
+      hipLaunchKernelGGL(k_collapse_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
+                         static_cast<WideNode*>(c.nodes4.p));
       LB_CHECK(hipGetLastError());
       c.root4 = 0u;  // node 0 (depth 0) is kept and scans to index 0
     }

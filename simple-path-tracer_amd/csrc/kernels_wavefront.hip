@@ -434,16 +434,17 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
   return hit;
 }
 
-// One axis of a quantised BVH4 node (Bvh4Node) in the ray's frame: the plane org + q * 2^e maps to
+// One axis of a quantised wide node (WideNode) in the ray's frame: the plane org + q * 2^e maps to
 // t = q * A + B with A = 2^e * inv (exact) and B = (org - o) * inv.  The fma evaluation errs by at
 // most ~2^-22 (|B| + 255 |A|) against (plane - o) * inv; the pad of 2^-20 (|B| + 256 |A|) pushes
 // near planes down and far planes up by more than that, so the decoded slab contains the exact
-// one.  qn / qf: the plane bytes that are near / far for this ray direction.
+// one.  qn / qf: the plane words that are near / far for this ray direction.
 struct QAxis {
   float A, Bn, Bf;
-  uint32_t qn, qf;
+  uint32_t qn[kQWords], qf[kQWords];
 };
-__device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, uint32_t qlo, uint32_t qhi, float ro, float inv) {
+__device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, const uint32_t* qlo, const uint32_t* qhi, float ro,
+                                        float inv) {
   QAxis a;
   a.A = __uint_as_float(ebyte << 23) * inv;
   const float B = (org - ro) * inv;
@@ -451,28 +452,32 @@ __device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, uint32_t qlo,
   a.Bn = B - pad;
   a.Bf = B + pad;
   const bool pos = inv >= 0.0f;
-  a.qn = pos ? qlo : qhi;
-  a.qf = pos ? qhi : qlo;
+#pragma unroll
+  for (int j = 0; j < kQWords; ++j) {
+    a.qn[j] = pos ? qlo[j] : qhi[j];
+    a.qf[j] = pos ? qhi[j] : qlo[j];
+  }
   return a;
 }
-__device__ __forceinline__ float q_byte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
-template <int K>
-__device__ __forceinline__ bool q_slab(const QAxis& x, const QAxis& y, const QAxis& z, float tnear, float tfar, float& tent) {
-  const float tnx = __builtin_fmaf(q_byte(x.qn, K), x.A, x.Bn), tfx = __builtin_fmaf(q_byte(x.qf, K), x.A, x.Bf);
-  const float tny = __builtin_fmaf(q_byte(y.qn, K), y.A, y.Bn), tfy = __builtin_fmaf(q_byte(y.qf, K), y.A, y.Bf);
-  const float tnz = __builtin_fmaf(q_byte(z.qn, K), z.A, z.Bn), tfz = __builtin_fmaf(q_byte(z.qf, K), z.A, z.Bf);
+__device__ __forceinline__ float q_byte(const uint32_t* w, int k) { return (float)((w[k / 4] >> (8 * (k % 4))) & 0xFFu); }
+__device__ __forceinline__ bool q_slab(int k, const QAxis& x, const QAxis& y, const QAxis& z, float tnear, float tfar,
+                                       float& tent) {
+  const float tnx = __builtin_fmaf(q_byte(x.qn, k), x.A, x.Bn), tfx = __builtin_fmaf(q_byte(x.qf, k), x.A, x.Bf);
+  const float tny = __builtin_fmaf(q_byte(y.qn, k), y.A, y.Bn), tfy = __builtin_fmaf(q_byte(y.qf, k), y.A, y.Bf);
+  const float tnz = __builtin_fmaf(q_byte(z.qn, k), z.A, z.Bn), tfz = __builtin_fmaf(q_byte(z.qf, k), z.A, z.Bf);
   const float tmin = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tnear));
   const float tmax = fminf(fminf(tfx, tfy), fminf(tfz, tfar));
   tent = tmin;
   return tmin <= tmax * 1.00000095f;
 }
 
-// BVH4 traversal: four slab tests per 64-B quantised node; leaf children are tested as soon as their
-// box is hit; the nearest internal child is visited next and the other hit children are pushed.
+// Wide-BVH traversal: kWide slab tests per quantised node; leaf children are tested as soon as their
+// box is hit; the nearest internal child is visited next (lowest slot on ties) and the other hit
+// children are pushed, highest slot first.
 template <bool kAny, bool kCount, int N>
-__device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t* prim_ref, const float4* tris,
-                                          const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                          uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
+__device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint32_t* prim_ref, const float4* tris,
+                                              const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
+                                              uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
   if (root == kNoHit) return false;
   if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
   TravStack<N> stack;
@@ -482,46 +487,59 @@ __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t*
   bool hit = false;
   for (;;) {
     const uint4* nq = reinterpret_cast<const uint4*>(nodes + cur);
-    const uint4 h0 = nq[0], h1 = nq[1];
-    const uint2 h2 = *reinterpret_cast<const uint2*>(nq + 2);
-    const uint4 ln = nq[3];
+    const uint4 h = nq[0];
+    uint32_t ln[kWide], qw[6 * kQWords];
+#pragma unroll
+    for (int j = 0; j < kWide / 4; ++j) {
+      const uint4 v = nq[1 + j];
+      ln[4 * j] = v.x; ln[4 * j + 1] = v.y; ln[4 * j + 2] = v.z; ln[4 * j + 3] = v.w;
+    }
+    if (kWide == 4) {
+      const uint4 v = nq[2];
+      const uint2 u = *reinterpret_cast<const uint2*>(nq + 3);
+      qw[0] = v.x; qw[1] = v.y; qw[2] = v.z; qw[3] = v.w; qw[4] = u.x; qw[5] = u.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const uint4 v = nq[1 + kWide / 4 + j];
+        qw[4 * j] = v.x; qw[4 * j + 1] = v.y; qw[4 * j + 2] = v.z; qw[4 * j + 3] = v.w;
+      }
+    }
     if (kCount) ++vc.nodes;
-    const QAxis ax = q_axis(__uint_as_float(h0.x), h0.w & 0xFFu, h1.x, h1.y, r.o.x, r.inv.x);
-    const QAxis ay = q_axis(__uint_as_float(h0.y), (h0.w >> 8) & 0xFFu, h1.z, h1.w, r.o.y, r.inv.y);
-    const QAxis az = q_axis(__uint_as_float(h0.z), (h0.w >> 16) & 0xFFu, h2.x, h2.y, r.o.z, r.inv.z);
-    float t0, t1, t2, t3;
-    bool h0_ = q_slab<0>(ax, ay, az, tnear, tfar, t0) && ln.x != kNoHit;
-    bool h1_ = q_slab<1>(ax, ay, az, tnear, tfar, t1) && ln.y != kNoHit;
-    bool h2_ = q_slab<2>(ax, ay, az, tnear, tfar, t2) && ln.z != kNoHit;
-    bool h3_ = q_slab<3>(ax, ay, az, tnear, tfar, t3) && ln.w != kNoHit;
-    uint32_t c0 = ln.x, c1 = ln.y, c2 = ln.z, c3 = ln.w;
-#define SPTR_LEAF4(H, C)                                                                      \
-  if (H && (C & kLeafBit)) {                                                                  \
-    if (leaf_test<kAny, kCount>(C, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {           \
-      hit = true;                                                                             \
-      if (kAny) return true;                                                                  \
-    }                                                                                         \
-    H = false;                                                                                \
-  }
-    SPTR_LEAF4(h0_, c0)
-    SPTR_LEAF4(h1_, c1)
-    SPTR_LEAF4(h2_, c2)
-    SPTR_LEAF4(h3_, c3)
-#undef SPTR_LEAF4
-    if (h0_ || h1_ || h2_ || h3_) {
-      // continue with the nearest hit child (lowest slot on ties); push the others, farthest last-in
-      float tn = h0_ ? t0 : __builtin_huge_valf();
-      uint32_t cn = c0, kn = 0u;
-      if (h1_ && (!h0_ || t1 < tn)) { tn = t1; cn = c1; kn = 1u; }
-      if (h2_ && ((!h0_ && !h1_) || t2 < tn)) { tn = t2; cn = c2; kn = 2u; }
-      if (h3_ && ((!h0_ && !h1_ && !h2_) || t3 < tn)) { tn = t3; cn = c3; kn = 3u; }
-      const uint32_t npush = (h0_ && kn != 0u) + (h1_ && kn != 1u) + (h2_ && kn != 2u) + (h3_ && kn != 3u);
-      if (sp + (int)npush > kStack) vc.stack_overflow = 1u;
-      if (h3_ && kn != 3u && sp < kStack) stack.put(sp++, c3);
-      if (h2_ && kn != 2u && sp < kStack) stack.put(sp++, c2);
-      if (h1_ && kn != 1u && sp < kStack) stack.put(sp++, c1);
-      if (h0_ && kn != 0u && sp < kStack) stack.put(sp++, c0);
-      cur = cn;
+    const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0 * kQWords, qw + 1 * kQWords, r.o.x, r.inv.x);
+    const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2 * kQWords, qw + 3 * kQWords, r.o.y, r.inv.y);
+    const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4 * kQWords, qw + 5 * kQWords, r.o.z, r.inv.z);
+    float t[kWide];
+    bool hc[kWide];
+#pragma unroll
+    for (int k = 0; k < kWide; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) && ln[k] != kNoHit;
+#pragma unroll
+    for (int k = 0; k < kWide; ++k) {
+      if (hc[k] && (ln[k] & kLeafBit)) {
+        if (leaf_test<kAny, kCount>(ln[k], prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
+          hit = true;
+          if (kAny) return true;
+        }
+        hc[k] = false;
+      }
+    }
+    int kn = kWide;
+    float tn = __builtin_huge_valf();
+    uint32_t npush = 0u;
+#pragma unroll
+    for (int k = 0; k < kWide; ++k) {
+      if (hc[k] && (kn == kWide || t[k] < tn)) {
+        tn = t[k];
+        kn = k;
+      }
+      npush += hc[k] ? 1u : 0u;
+    }
+    if (kn < kWide) {
+      if (sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
+#pragma unroll
+      for (int k = kWide - 1; k >= 0; --k)
+        if (hc[k] && k != kn && sp < kStack) stack.put(sp++, ln[k]);
+      cur = ln[kn];
     } else {
       if (sp == 0) break;
       cur = stack.get(--sp);
@@ -533,7 +551,7 @@ __device__ __forceinline__ bool traverse4(const Bvh4Node* nodes, const uint32_t*
 // Stage the whole scene (nodes, triangles, spheres) into LDS when it fits (SceneView::lds_bytes).
 struct Staged {
   const BvhNode* nodes;
-  const Bvh4Node* nodes4;
+  const WideNode* nodes4;
   const uint32_t* prim_ref;
   const float4* tris;
   const float4* sph;
@@ -542,8 +560,8 @@ template <bool kLds>
 __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) {
   Staged s{sv.nodes, sv.nodes4, sv.prim_ref, sv.tris, sv.sph};
   if (kLds) {
-    const bool w4 = sv.width == 4u;
-    const uint32_t nn = (w4 ? sv.num_nodes4 * (uint32_t)sizeof(Bvh4Node) : sv.num_nodes * (uint32_t)sizeof(BvhNode)) / 16u,
+    const bool w4 = sv.width == (uint32_t)kWide;
+    const uint32_t nn = (w4 ? sv.num_nodes4 * (uint32_t)sizeof(WideNode) : sv.num_nodes * (uint32_t)sizeof(BvhNode)) / 16u,
                    nt = sv.num_tris * 3u, ns = sv.num_sph;
     const uint32_t np = (sv.num_tris + sv.num_sph + 3u) / 4u;  // prim refs, in float4 units
     const float4* gn = w4 ? reinterpret_cast<const float4*>(sv.nodes4) : reinterpret_cast<const float4*>(sv.nodes);
@@ -554,7 +572,7 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[nn + nt + ns + i] = gp[i];
     __syncthreads();
     s.nodes = reinterpret_cast<const BvhNode*>(lds);
-    s.nodes4 = reinterpret_cast<const Bvh4Node*>(lds);
+    s.nodes4 = reinterpret_cast<const WideNode*>(lds);
     s.tris = lds + nn;
     s.sph = lds + nn + nt;
     s.prim_ref = reinterpret_cast<const uint32_t*>(lds + nn + nt + ns);
@@ -565,7 +583,7 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
 template <bool kW4, bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv, const Ray& r, float tnear, float& tfar,
                                            uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
-  if (kW4) return traverse4<kAny, kCount>(sc.nodes4, sc.prim_ref, sc.tris, sc.sph, sv.root4, r, tnear, tfar, ref, vc, ls);
+  if (kW4) return traverse_wide<kAny, kCount>(sc.nodes4, sc.prim_ref, sc.tris, sc.sph, sv.root4, r, tnear, tfar, ref, vc, ls);
   return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
 }
 
@@ -1966,13 +1984,13 @@ __global__ void __launch_bounds__(kBlock) k_query(SceneView sv, const uint32_t* 
     float tfar = rr[7];
     uint32_t ref = kNoHit;
     if (anyhit) {
-      occ[i] = (sv.width == 4u ? traverse_w<true, true, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
+      occ[i] = (sv.width == (uint32_t)kWide ? traverse_w<true, true, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
                                : traverse_w<false, true, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack))
                    ? 1
                    : 0;
       continue;
     }
-    const bool hit = sv.width == 4u ? traverse_w<true, false, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
+    const bool hit = sv.width == (uint32_t)kWide ? traverse_w<true, false, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack)
                                     : traverse_w<false, false, false>(sg, sv, r, rr[6], tfar, ref, vc, s_stack);
     // report (type bit | original primitive index) so the host can map to (geomID, primID)
     ref_out[i] = hit ? ((ref & kSphereBit) | ((ref & kSphereBit) ? sph_orig[ref & kIndexMask] : tri_orig[ref & kIndexMask]))
@@ -2064,7 +2082,7 @@ static unsigned resident_grid(const void* fn, uint32_t lds_bytes) {
 SceneView scene_view(const Context& c) {
   SceneView s;
   s.nodes = static_cast<const BvhNode*>(c.nodes.p);
-  s.nodes4 = static_cast<const Bvh4Node*>(c.nodes4.p);
+  s.nodes4 = static_cast<const WideNode*>(c.nodes4.p);
   s.tris = static_cast<const float4*>(c.tris.p);
   s.sph = static_cast<const float4*>(c.sph.p);
   s.tri_geom = static_cast<const uint32_t*>(c.tri_geom.p);
@@ -2079,12 +2097,12 @@ SceneView scene_view(const Context& c) {
   // node cost more than the saved steps), BVH4 for everything traversed from L2/HBM
   const uint64_t bytes2 = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
                           ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
-  s.width = c.bvh_width ? c.bvh_width : (bytes2 <= kLdsSceneBytes ? 2u : 4u);
+  s.width = c.bvh_width ? c.bvh_width : (bytes2 <= kLdsSceneBytes ? 2u : (uint32_t)kWide);
   // never a width whose worst-case traversal stack exceeds kStack (build_lbvh rejects trees that
   // even BVH2 cannot traverse)
-  if (s.width == 4u && c.stack_need4 > (uint32_t)kStack) s.width = 2u;
+  if (s.width == (uint32_t)kWide && c.stack_need4 > (uint32_t)kStack) s.width = 2u;
   s.prim_ref = static_cast<const uint32_t*>(c.prim_ref.p);
-  const uint64_t node_bytes = s.width == 4u ? (uint64_t)c.num_nodes4 * sizeof(Bvh4Node) : (uint64_t)c.num_nodes * 64;
+  const uint64_t node_bytes = s.width == (uint32_t)kWide ? (uint64_t)c.num_nodes4 * sizeof(WideNode) : (uint64_t)c.num_nodes * 64;
   const uint64_t bytes = node_bytes + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
@@ -2115,7 +2133,7 @@ uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
 #endif
   if (sv.lds_bytes != 0) {
     const unsigned lb = trace_lds(sv, true, true, 0);
-    const unsigned g = sv.width == 4u ? resident_grid((const void*)&k_trace_pm<false, true, false>, lb)
+    const unsigned g = sv.width == (uint32_t)kWide ? resident_grid((const void*)&k_trace_pm<false, true, false>, lb)
                                       : resident_grid((const void*)&k_trace_pm<false, false, false>, lb);
     const uint64_t threads = (uint64_t)g * kBlock;
     // a thread's pixels are serial loops of k samples: with few pixels per thread and long loops the
@@ -2152,7 +2170,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
   const bool P = depth == 0;
-  const bool W = sv.width == 4u;
+  const bool W = sv.width == (uint32_t)kWide;
   const bool cube = sh.env.env != nullptr;
   const unsigned lb = trace_lds(sv, L, P, nseg);
   const EnvView ev = sh.env;
@@ -2216,7 +2234,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
                        uint32_t nseg, hipStream_t s) {
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
-  const bool W = sv.width == 4u;
+  const bool W = sv.width == (uint32_t)kWide;
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
 #define SPTR_SHADOW(Lc, C, Wc)                                                                      \
@@ -2247,7 +2265,7 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
           return g;
         }(fl);
       },
-      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
+      Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
 }
 
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {
@@ -2262,7 +2280,7 @@ void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView
           return g;
         }(fl);
       },
-      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
+      Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
 }
 
 void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {
@@ -2277,7 +2295,7 @@ void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
           return g;
         }(fl);
       },
-      Flags<>{}, L, sv.width == 4u, sh.env.env != nullptr);
+      Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
 }
 
 void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, hipStream_t s) {

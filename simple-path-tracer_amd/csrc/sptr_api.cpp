@@ -685,7 +685,8 @@ int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
 
 int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
   if (!x) return SPTR_ERR_INVALID;
-  if (width != 0 && width != 2 && width != 4) return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or 4");
+  if (width != 0 && width != 2 && width != (uint32_t)kWide)
+    return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or " + std::to_string(kWide));
   x->c.bvh_width = width;
   ++x->c.epoch;
   return SPTR_OK;
@@ -760,8 +761,8 @@ int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
   out->bvh_depth = c.bvh_depth;
   out->lds_bytes = sv.lds_bytes;
   out->bvh_width = sv.width;
-  out->num_nodes = sv.width == 4u ? c.num_nodes4 : c.num_nodes;
-  out->node_bytes = sv.width == 4u ? (uint64_t)c.num_nodes4 * sizeof(Bvh4Node) : (uint64_t)c.num_nodes * sizeof(BvhNode);
+  out->num_nodes = sv.width == (uint32_t)kWide ? c.num_nodes4 : c.num_nodes;
+  out->node_bytes = sv.width == (uint32_t)kWide ? (uint64_t)c.num_nodes4 * sizeof(WideNode) : (uint64_t)c.num_nodes * sizeof(BvhNode);
   out->tri_bytes = (uint64_t)c.num_tris * 48u;
   out->sphere_bytes = (uint64_t)c.num_sph * 16u;
   out->prim_ref_bytes = ((uint64_t)c.num_tris + c.num_sph) * 4u;

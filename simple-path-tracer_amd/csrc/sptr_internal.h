@@ -38,11 +38,12 @@ constexpr int kTile = 32;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kMaxLights = 8;
 constexpr int kMaxDepth = 32;
-// Traversal stack entries.  BVH2 pushes at most one entry per internal level, BVH4 at most three,
-// so a tree of height h needs h (BVH2) or 3 * ((h - 1) / 2 + 1) (BVH4) entries; build_lbvh records
-// both bounds, scene_view never picks a width whose bound exceeds kStack, and a push that would
-// still overflow is dropped and reported (kTotStackOverflow), never silent.
-constexpr int kStack = 96;
+// Traversal stack entries.  BVH2 pushes at most one entry per internal level, a wide BVH at most
+// kWide - 1, so a tree of height h needs h (BVH2) or (kWide - 1) * ((h - 1) / kWideLevels + 1)
+// (wide) entries; build_lbvh records both bounds, scene_view never picks a width whose bound
+// exceeds kStack, and a push that would still overflow is dropped and reported
+// (kTotStackOverflow), never silent.
+constexpr int kStack = kWide == 8 ? 112 : 96;
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;  // scenes up to this size are staged whole into LDS
 
@@ -58,19 +59,29 @@ static_assert(sizeof(BvhNode) == 64, "node size");
 // BVH4 node, 128 B (one cache line): four child boxes stored SoA so the four slab tests vectorise,
 // four child links (BVH4 node index, leaf range, or kNoHit for an empty slot).  Built by collapsing
 // the LBVH: the BVH2 nodes at even depth become BVH4 nodes whose children are their grandchildren.
-// BVH4 node, 64 B (half a 128-B cache line): the four child boxes quantised to 8 bits per plane on
-// a per-node, per-axis power-of-two grid anchored at the node's lower corner (org).  Child k's box
-// is [org + qlo_k * 2^e, org + qhi_k * 2^e] per axis, rounded outwards at build time (k_collapse4),
-// so it contains the exact child box; traverse4 decodes the planes in the ray's frame with an error
-// pad, so the test stays conservative.  Byte k of each q word belongs to child k.
-struct alignas(16) Bvh4Node {
+// Collapsed ("wide") BVH: every kWideLevels-th level of the LBVH, kWide children per node.
+#ifndef SPTR_WIDE
+#define SPTR_WIDE 4
+#endif
+constexpr int kWide = SPTR_WIDE;
+static_assert(kWide == 4 || kWide == 8, "wide BVH: 4 or 8 children");
+constexpr int kWideLevels = kWide == 8 ? 3 : 2;  // BVH2 levels per wide level
+constexpr int kQWords = kWide / 4;               // u32 words per quantised plane, one byte per child
+
+// Wide BVH node (64 B for 4 children = half a 128-B cache line; 128 B for 8): the child boxes
+// quantised to 8 bits per plane on a per-node, per-axis power-of-two grid anchored at the node's
+// lower corner (org).  Child k's box is [org + qlo_k * 2^e, org + qhi_k * 2^e] per axis, rounded
+// outwards at build time (k_collapse_wide), so it contains the exact child box; traverse_wide
+// decodes the planes in the ray's frame with an error pad, so the test stays conservative.
+struct alignas(16) WideNode {
   float ox, oy, oz;
-  uint32_t ex;                     // biased exponent bytes of the x / y / z grid steps; byte 3: child count
-  uint32_t qlox, qhix, qloy, qhiy;
-  uint32_t qloz, qhiz, parent, pad;  // parent: BVH4 index (build bookkeeping, not traversed)
-  uint4 link;
+  uint32_t ex;               // biased exponent bytes of the x / y / z grid steps; byte 3: child count
+  uint32_t link[kWide];      // child: internal node index | leaf range (kLeafBit) | kNoHit
+  uint32_t q[6][kQWords];    // planes lo x, hi x, lo y, hi y, lo z, hi z; byte k % 4 of word k / 4
+  uint32_t parent;           // wide-node index (build bookkeeping, not traversed)
+  uint32_t pad[kWide == 8 ? 7 : 1];
 };
-static_assert(sizeof(Bvh4Node) == 64, "node size");
+static_assert(sizeof(WideNode) == (kWide == 8 ? 128 : 64), "node size");
 
 struct DevMaterial {  // == sptr_material
   float albedo[3];
@@ -92,7 +103,7 @@ struct DevLight {  // host-precomputed per Light::getRadiance (Light.cpp:43-79)
 
 struct SceneView {
   const BvhNode* nodes;
-  const Bvh4Node* nodes4;  // used when width == 4
+  const WideNode* nodes4;  // used when width == 4
   const uint32_t* prim_ref;  // sorted primitive refs (leaf ranges index this)
   const float4* tris;  // 3 float4 per sorted triangle: v0.xyz e1.x | e1.yz e2.xy | e2.z Ng.xyz
   const float4* sph;   // sorted spheres: c.xyz r
