@@ -108,8 +108,10 @@ enum sptr_frame_flags {
   SPTR_FRAME_COUNT_VISITS = 4u, /* one instrumented trace pass: count BVH node / primitive fetches */
   SPTR_FRAME_ASYNC = 8u, /* enqueue only: return without waiting; stats are left zero and the call's
                             counters and stage times accumulate until sptr_collect_stats */
-  SPTR_FRAME_TIMING_TRACE = 16u /* HIP events around the trace launches only (ms_trace, ms_trace0,
+  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace launches only (ms_trace, ms_trace0,
                                    trace_launches): the other stages run back to back */
+  SPTR_FRAME_NO_CULL = 32u /* diagnostic: bounce 0 traverses every camera ray, without the pixel-frustum
+                              cull (the image is the same either way) */
 };
 
 /* Integrators (sptr_frame.integrator).  The reference selects between them per frame in

@@ -629,12 +629,90 @@ __device__ __forceinline__ void primary_at(const FrameView& f, const ImageDiv& d
   out.d = safe_renormalize_dir(dir);
   out.rng = wang_hash((ps ^ acc) ^ 1u);
 }
-__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
-  const uint32_t s = fast_div(f.div_P, p), l = p - s * f.P;
+__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out,
+                                             uint32_t& l) {
+  const uint32_t s = fast_div(f.div_P, p);
+  l = p - s * f.P;
   int x, y;
   if (!local_pixel(f, l, x, y)) return false;
   primary_at(f, dv, x, y, (uint32_t)(y * f.W + x), f.acc0 + s, out);
   return true;
+}
+__device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out) {
+  uint32_t l;
+  return primary_path(f, dv, p, out, l);
+}
+
+// --------------------------------------------------------------------------------- pixel culling
+// Bounce-0 pixel-frustum culling.  All camera rays of local pixel (x, y) — any jitter — start at the
+// camera and run inside the pyramid spanned by the pixel's corner directions (Camera::getRayDirection
+// at u in [x, x+1] / W, v in [y, y+1] / H).  When that pyramid, widened by kCullMarginPx pixels, lies
+// outside every box of the BVH's top two levels, no such ray can hit any primitive, and bounce 0
+// skips their traversal: it would return no hit.  The test is a separating-plane test against the
+// pyramid's four side planes (the box's corner farthest along each inward normal), with a relative
+// margin of kCullSlack on the plane distance.  Both margins are orders of magnitude above the
+// rounding of the per-sample ray directions (~1e-6 relative, vs 1/64 pixel = 7.5e-6 rad at 4K) and of
+// this test itself, so a pixel is culled only when its rays certainly miss.
+constexpr float kCullMarginPx = 1.0f / 64.0f;
+constexpr float kCullSlack = 1e-4f;
+struct Box {
+  vec3 lo, hi;
+};
+__device__ __forceinline__ bool box_outside(const Box& b, const vec3 n[4], vec3 o) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const vec3 p = v3(n[k].x >= 0.0f ? b.hi.x : b.lo.x, n[k].y >= 0.0f ? b.hi.y : b.lo.y,
+                      n[k].z >= 0.0f ? b.hi.z : b.lo.z);
+    const vec3 q = p - o;
+    const float d = n[k].x * q.x + n[k].y * q.y + n[k].z * q.z;
+    const float mag = fabsf(n[k].x * q.x) + fabsf(n[k].y * q.y) + fabsf(n[k].z * q.z);
+    if (d < -kCullSlack * mag) return true;
+  }
+  return false;
+}
+__device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const FrameView& f, int x, int y) {
+  if (sv.num_nodes == 0u || (sv.root & kLeafBit)) return false;
+  const float u0 = (float(x) - kCullMarginPx) / float(f.W), u1 = (float(x) + 1.0f + kCullMarginPx) / float(f.W);
+  const float v0 = (float(y) - kCullMarginPx) / float(f.H), v1 = (float(y) + 1.0f + kCullMarginPx) / float(f.H);
+  auto dir = [&](float u, float v) {
+    return f.cam_f + ((u - 0.5f) * 2.0f * f.half_w) * f.cam_r + (-(v - 0.5f) * 2.0f * f.half_h) * f.cam_u;
+  };
+  const vec3 c[4] = {dir(u0, v0), dir(u1, v0), dir(u1, v1), dir(u0, v1)};
+  vec3 n[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    n[k] = cross(c[k], c[(k + 1) & 3]);
+    if (dot(n[k], c[(k + 2) & 3]) < 0.0f) n[k] = -n[k];  // inward
+  }
+  // the top two BVH2 levels: the root's children, internal ones replaced by their children
+  const BvhNode r = sv.nodes[0];
+  const uint32_t links[2] = {r.link.x, r.link.y};
+  const Box kid[2] = {Box{v3(r.lxy.x, r.lxy.z, r.z.x), v3(r.lxy.y, r.lxy.w, r.z.y)},
+                      Box{v3(r.rxy.x, r.rxy.z, r.z.z), v3(r.rxy.y, r.rxy.w, r.z.w)}};
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (links[side] & kLeafBit) {
+      if (!box_outside(kid[side], n, f.cam_pos)) return false;
+      continue;
+    }
+    if (box_outside(kid[side], n, f.cam_pos)) continue;
+    const BvhNode g = sv.nodes[links[side]];
+    if (!box_outside(Box{v3(g.lxy.x, g.lxy.z, g.z.x), v3(g.lxy.y, g.lxy.w, g.z.y)}, n, f.cam_pos)) return false;
+    if (!box_outside(Box{v3(g.rxy.x, g.rxy.z, g.z.z), v3(g.rxy.y, g.rxy.w, g.z.w)}, n, f.cam_pos)) return false;
+  }
+  return true;
+}
+// bit l of mask: pixel l is culled (see above); one ballot word pair per wave
+__global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  int x = 0, y = 0;
+  const bool culled = l < f.P && local_pixel(f, l, x, y) && pixel_frustum_misses(sv, f, x, y);
+  const unsigned long long b = __ballot(culled);
+  const uint32_t lane = lane_id();
+  if ((lane & 31u) == 0u && l < f.P) mask[l >> 5] = (uint32_t)(b >> lane);
+}
+__device__ __forceinline__ bool pixel_culled(const FrameView& f, uint32_t l) {
+  return f.cull != nullptr && ((f.cull[l >> 5] >> (l & 31u)) & 1u) != 0u;
 }
 
 // --------------------------------------------------------------------------------- shading math
@@ -776,6 +854,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
+    const bool culled = valid && pixel_culled(f, l);
     vec3 a = v3(0.0f, 0.0f, 0.0f);
     if (valid && !f.reset) a = xyz(f.accum[l]);
     bool fold = true;
@@ -791,7 +870,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
         const Ray r = make_ray(f.cam_pos, pr.d);
         // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
         // 1 = constant environment, 4 = primary misses add no radiance
-        if (!(ablate(f) & 2u)) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!(ablate(f) & 2u) && !culled) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
           if (sh.debug_mode != 1) {
@@ -855,6 +934,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
+    const bool culled = valid && pixel_culled(f, l);
     vec3 a = v3(0.0f, 0.0f, 0.0f);
     if (valid && !f.reset) a = xyz(f.accum[l]);
     bool fold = true;
@@ -871,7 +951,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
         Primary pr;
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         const Ray r = make_ray(f.cam_pos, pr.d);
-        hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!culled) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
         if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
       }
       // this pixel group's hits of the round -> number of leading misses still to fold
@@ -931,15 +1011,17 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   const Sched sd = block_sched(n);
   for (uint32_t base = sd.first; base < n; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
-    bool active = i < n, hit = false;
+    bool active = i < n, hit = false, culled = false;
     uint32_t id = 0u, pid = 0u, ref = kNoHit;
     float tfar = __builtin_huge_valf();
     vec3 o, d;
     if (active) {
       if (kPrimary) {
         Primary pr;
+        uint32_t l;
         id = pid = i;
-        active = primary_path(f, idiv, i, pr);
+        active = primary_path(f, idiv, i, pr, l);
+        culled = pixel_culled(f, l);
         o = f.cam_pos;
         d = pr.d;
       } else {
@@ -954,7 +1036,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       const Ray r = make_ray(o, d);
       // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
       // 1 = constant environment, 4 = primary misses write no radiance
-      if (!(kPrimary && (ablate(f) & 2u))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+      if (!(kPrimary && ((ablate(f) & 2u) || culled))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
       if (kPrimary && !hit && (ablate(f) & 4u)) {
       } else if (!hit) {
         if (sh.debug_mode == 1) {
@@ -2228,6 +2310,11 @@ unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView&
         }(fl);
       },
       Flags<>{}, depth == 0, fuse);
+}
+
+void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s) {
+  if (f.P == 0u) return;
+  hipLaunchKernelGGL(k_cull, dim3(f.P / kBlock), dim3(kBlock), 0, s, sv, f, mask);
 }
 
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count,

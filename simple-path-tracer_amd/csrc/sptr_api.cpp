@@ -197,6 +197,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.reset = 0;
   v.pixel_major = 0;
   v.dyn = nullptr;
+  v.cull = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -339,6 +340,7 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   API_HIP(ensure_buf(c.accum, (size_t)c.P * 16));
   API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
   API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
+  API_HIP(ensure_buf(c.cull, (size_t)c.P / 32u * 4u + 4u));
   ++c.epoch;
   API_HIP(hipMemsetAsync(c.accum.p, 0, (size_t)c.P * 16, s));
   API_HIP(hipMemsetAsync(c.tiles.p, 0, (size_t)c.P * 4, s));
@@ -426,6 +428,11 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
   const bool fuse = shade_fuses_shadows(sv, sh, count);
+  // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it)
+  if (!(f.flags & SPTR_FRAME_NO_CULL)) {
+    launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), s);
+    fv.cull = static_cast<const uint32_t*>(c.cull.p);
+  }
   tm.begin_call();
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
@@ -653,7 +660,7 @@ int sptr_destroy(sptr_ctx* x) {
   (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_hrec, &c.w_rad,   &c.w_stask,
-                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf};
+                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf, &c.nodes4, &c.cull};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& b : c.w_rs)
     for (DevBuf& x : b) free_buf(x);
@@ -873,7 +880,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   key.epoch = c.epoch;
   key.frame = *f;
   key.frame.frame_begin = 0;
-  key.frame.flags &= (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_COUNT_VISITS | SPTR_FRAME_NO_RESOLVE);
+  key.frame.flags &= (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_COUNT_VISITS | SPTR_FRAME_NO_RESOLVE |
+                      SPTR_FRAME_NO_CULL);
   uint32_t waves = 0;
   uint64_t samples = 0;
   if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) {

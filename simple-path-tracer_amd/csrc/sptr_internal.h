@@ -154,6 +154,7 @@ struct FrameView {
   vec3 ox_u, ox_v, ox_w; // OptiX mode: LaunchParams cam_u / cam_v / cam_w (OptixBackend.cpp:1609-1620)
   vec3 ox_light_dir, ox_light_rad;  // OptiX mode: first directional light (direction FROM the light)
   uint32_t ox_has_light;
+  const uint32_t* cull;  // bit l: camera rays through local pixel l cannot hit the scene (k_cull); may be null
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -280,6 +281,7 @@ struct Context {
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;
   DevBuf accum, tiles, image;
+  DevBuf cull;  // bounce-0 pixel-frustum cull mask, 1 bit per local pixel (k_cull)
   uint32_t last_samples = 0;  // accumulation count after the last render
   // query scratch
   DevBuf qbuf;
@@ -312,6 +314,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
                    hipStream_t s);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
+void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.

@@ -23,6 +23,7 @@ SPTR_FRAME_NO_RESOLVE = 2
 SPTR_FRAME_COUNT_VISITS = 4
 SPTR_FRAME_ASYNC = 8
 SPTR_FRAME_TIMING_TRACE = 16
+SPTR_FRAME_NO_CULL = 32
 
 SPTR_INTEGRATOR_WAVEFRONT = 0   # WavefrontPathTracerCPU semantics (default)
 SPTR_INTEGRATOR_PATHTRACER = 1  # PathTracer (the reference's default CPU integrator) semantics

@@ -447,3 +447,22 @@ def test_fused_shadow_equals_shadow_stage(renderer, scene):
     assert st2.shadow_node_visits > 0  # the separate stage ran
     assert np.array_equal(fused.view(np.uint32), renderer.read_accum().view(np.uint32))
     assert (st.rays_closest, st.rays_shadow) == (st2.rays_closest, st2.rays_shadow)
+
+
+@pytest.mark.parametrize("scene,p0,p1,spp,W,H", [("default_emitter", 0, 0, 64, 256, 144), ("default", 0, 0, 3, 96, 64),
+                                                 ("sphere_mesh", 60, 120, 4, 96, 64)])
+def test_pixel_cull_invisible(renderer, scene, p0, p1, spp, W, H):
+    """Bounce-0 pixel-frustum culling (k_cull) skips the traversal of camera rays that cannot hit the
+    top BVH boxes: the accumulation and the ray counts equal a render without it (SPTR_FRAME_NO_CULL)
+    bit for bit — in the thread-per-pixel, path-major and BVH4 bounce-0 kernels — while the
+    instrumented pass shows fewer node visits."""
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, scene, p0, p1)
+    st = renderer.render(cam, W, H, spp=spp)
+    acc = renderer.read_accum().copy()
+    st0 = renderer.render(cam, W, H, spp=spp, flags=sptr.SPTR_FRAME_NO_CULL)
+    assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
+    assert (st.rays_closest, st.rays_shadow) == (st0.rays_closest, st0.rays_shadow)
+    c1 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS)
+    c0 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS | sptr.SPTR_FRAME_NO_CULL)
+    assert c1.node_visits < c0.node_visits
