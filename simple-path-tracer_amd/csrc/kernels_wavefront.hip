@@ -647,7 +647,7 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv&
 // Bounce-0 pixel-frustum culling.  All camera rays of local pixel (x, y) — any jitter — start at the
 // camera and run inside the pyramid spanned by the pixel's corner directions (Camera::getRayDirection
 // at u in [x, x+1] / W, v in [y, y+1] / H).  When that pyramid, widened by kCullMarginPx pixels, lies
-// outside every box of the BVH's top two levels, no such ray can hit any primitive, and bounce 0
+// outside every box of the BVH's top kCullDepth levels, no such ray can hit any primitive, and bounce 0
 // skips their traversal: it would return no hit.  The test is a separating-plane test against the
 // pyramid's four side planes (the box's corner farthest along each inward normal), with a relative
 // margin of kCullSlack on the plane distance.  Both margins are orders of magnitude above the
@@ -655,6 +655,10 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv&
 // this test itself, so a pixel is culled only when its rays certainly miss.
 constexpr float kCullMarginPx = 1.0f / 64.0f;
 constexpr float kCullSlack = 1e-4f;
+#ifndef SPTR_CULL_DEPTH
+#define SPTR_CULL_DEPTH 4  // r02 A/B: 2 -> 4 levels, C2 primary trace 1.12 -> 1.09 ms; deeper gains nothing
+#endif
+constexpr int kCullDepth = SPTR_CULL_DEPTH;  // BVH2 levels below the root whose boxes the test visits
 struct Box {
   vec3 lo, hi;
 };
@@ -684,21 +688,26 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
     n[k] = cross(c[k], c[(k + 1) & 3]);
     if (dot(n[k], c[(k + 2) & 3]) < 0.0f) n[k] = -n[k];  // inward
   }
-  // the top two BVH2 levels: the root's children, internal ones replaced by their children
-  const BvhNode r = sv.nodes[0];
-  const uint32_t links[2] = {r.link.x, r.link.y};
-  const Box kid[2] = {Box{v3(r.lxy.x, r.lxy.z, r.z.x), v3(r.lxy.y, r.lxy.w, r.z.y)},
-                      Box{v3(r.rxy.x, r.rxy.z, r.z.z), v3(r.rxy.y, r.rxy.w, r.z.w)}};
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    if (links[side] & kLeafBit) {
-      if (!box_outside(kid[side], n, f.cam_pos)) return false;
-      continue;
-    }
-    if (box_outside(kid[side], n, f.cam_pos)) continue;
-    const BvhNode g = sv.nodes[links[side]];
-    if (!box_outside(Box{v3(g.lxy.x, g.lxy.z, g.z.x), v3(g.lxy.y, g.lxy.w, g.z.y)}, n, f.cam_pos)) return false;
-    if (!box_outside(Box{v3(g.rxy.x, g.rxy.z, g.z.z), v3(g.rxy.y, g.rxy.w, g.z.w)}, n, f.cam_pos)) return false;
+  // the BVH2's top kCullDepth levels, depth first: a box outside the pyramid prunes its subtree;
+  // a box that may intersect it at the cut depth (or a leaf's box) means the pixel is not culled
+  struct Entry {
+    uint32_t link, depth;
+    Box b;
+  };
+  Entry st[2 * kCullDepth + 2];
+  int sp = 0;
+  {
+    const BvhNode r = sv.nodes[0];
+    st[sp++] = Entry{r.link.y, 1u, Box{v3(r.rxy.x, r.rxy.z, r.z.z), v3(r.rxy.y, r.rxy.w, r.z.w)}};
+    st[sp++] = Entry{r.link.x, 1u, Box{v3(r.lxy.x, r.lxy.z, r.z.x), v3(r.lxy.y, r.lxy.w, r.z.y)}};
+  }
+  while (sp > 0) {
+    const Entry e = st[--sp];
+    if (box_outside(e.b, n, f.cam_pos)) continue;
+    if ((e.link & kLeafBit) || e.depth >= (uint32_t)kCullDepth) return false;
+    const BvhNode g = sv.nodes[e.link];
+    st[sp++] = Entry{g.link.y, e.depth + 1u, Box{v3(g.rxy.x, g.rxy.z, g.z.z), v3(g.rxy.y, g.rxy.w, g.z.w)}};
+    st[sp++] = Entry{g.link.x, e.depth + 1u, Box{v3(g.lxy.x, g.lxy.z, g.z.x), v3(g.lxy.y, g.lxy.w, g.z.y)}};
   }
   return true;
 }
@@ -1022,6 +1031,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         id = pid = i;
         active = primary_path(f, idiv, i, pr, l);
         culled = pixel_culled(f, l);
+        if (culled && f.sky_fold) active = false;  // summed by k_sky
         o = f.cam_pos;
         d = pr.d;
       } else {
@@ -1502,9 +1512,39 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, 
   report_stack(vc, w.tot);
 }
 
+// --------------------------------------------------------------------------------- k_sky
+// Path-major bounce 0 with a cull mask (f.sky_fold): the culled pixels' camera rays all miss, so
+// their samples are nothing but raygen + environment.  One thread per culled pixel sums them into
+// accum in sample order — the adds k_trace (rad[p] = 0 + 1 * env) and k_accum would make, in the
+// same order — and marks the pixel complete (resume slot k); k_trace skips those paths and writes no
+// radiance for them, k_accum no longer reads it.  Other pixels get resume slot 0.
+template <bool kCube>
+__global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
+  const FrameView f = frame_dyn(fin);
+  const ImageDiv idiv = image_div(f);
+  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
+    vec3 a = v3(0.0f, 0.0f, 0.0f);
+    if (!f.reset) a = xyz(f.accum[l]);
+    int x, y;
+    uint32_t resume = 0u;
+    if (pixel_culled(f, l) && local_pixel(f, l, x, y)) {
+      const uint32_t ps = (uint32_t)(y * f.W + x);
+      for (uint32_t smp = 0; smp < f.k; ++smp) {
+        Primary pr;
+        primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
+        vec3 rv = v3(0.0f, 0.0f, 0.0f);
+        if (sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+        a = a + rv;
+      }
+      resume = f.k;
+    }
+    f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
+  }
+}
+
 // --------------------------------------------------------------------------------- k_accum / resolve
 // Per-pixel sample sums in sample order.  A folding bounce 0 (f.pixel_major: thread or lane group
-// per pixel) began them:
+// per pixel; f.sky_fold: k_sky for the culled pixels of a path-major bounce 0) began them:
 // accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
 // batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
 // slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
@@ -1513,7 +1553,7 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     uint32_t s0 = 0u;
     vec3 a = v3(0.0f, 0.0f, 0.0f);
-    if (f.pixel_major) {
+    if (f.pixel_major || f.sky_fold) {
       const float4 a4 = accum[l];
       s0 = __float_as_uint(a4.w);
       if (s0 >= f.k) continue;
@@ -2389,6 +2429,12 @@ void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint3
   hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total);
 }
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
+
+void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
+  const unsigned g = std::min<unsigned>((f.P + kBlock - 1u) / kBlock, 16384u);
+  if (sh.env.env != nullptr) hipLaunchKernelGGL(k_sky<true>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  else hipLaunchKernelGGL(k_sky<false>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
+}
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s) {
   hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum);

@@ -198,6 +198,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.pixel_major = 0;
   v.dyn = nullptr;
   v.cull = nullptr;
+  v.sky_fold = 0u;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -442,6 +443,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
     fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     fv.pixel_major = bounce0_pixel_major(sv, fv);
+    fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
@@ -453,6 +455,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         break;
       }
       tm.begin(d == 0 ? 5 : 1);
+      if (d == 0 && fv.sky_fold) launch_sky(sh, fv, s);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
       tm.begin(d == 0 ? 6 : 2);

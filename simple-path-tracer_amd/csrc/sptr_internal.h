@@ -155,6 +155,7 @@ struct FrameView {
   vec3 ox_light_dir, ox_light_rad;  // OptiX mode: first directional light (direction FROM the light)
   uint32_t ox_has_light;
   const uint32_t* cull;  // bit l: camera rays through local pixel l cannot hit the scene (k_cull); may be null
+  uint32_t sky_fold;     // path-major bounce 0 with a cull mask: k_sky sums culled pixels into accum
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -315,6 +316,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s);
+void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.
