@@ -1529,13 +1529,24 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
     uint32_t resume = 0u;
     if (pixel_culled(f, l) && local_pixel(f, l, x, y)) {
       const uint32_t ps = (uint32_t)(y * f.W + x);
-      for (uint32_t smp = 0; smp < f.k; ++smp) {
+      auto sample = [&](uint32_t smp) {
         Primary pr;
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         vec3 rv = v3(0.0f, 0.0f, 0.0f);
         if (sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
-        a = a + rv;
+        return rv;
+      };
+      // four independent samples (their environment fetches in flight together), then their adds in
+      // sample order
+      uint32_t smp = 0;
+      for (; smp + 4u <= f.k; smp += 4u) {
+        vec3 rv[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) rv[j] = sample(smp + j);
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) a = a + rv[j];
       }
+      for (; smp < f.k; ++smp) a = a + sample(smp);
       resume = f.k;
     }
     f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
