@@ -431,7 +431,12 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   const bool fuse = shade_fuses_shadows(sv, sh, count);
   // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it)
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
-    launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), s);
+    // the mask depends on the scene, the pixel layout (both covered by the epoch) and the camera
+    if (c.cull_epoch != c.epoch || std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) != 0) {
+      launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), s);
+      c.cull_epoch = c.epoch;
+      c.cull_cam = f.camera;
+    }
     fv.cull = static_cast<const uint32_t*>(c.cull.p);
   }
   tm.begin_call();

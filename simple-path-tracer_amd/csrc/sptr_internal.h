@@ -283,6 +283,9 @@ struct Context {
   uint32_t P = 0, local_tiles = 0;
   DevBuf accum, tiles, image;
   DevBuf cull;  // bounce-0 pixel-frustum cull mask, 1 bit per local pixel (k_cull)
+  // what the mask was computed for (state epoch, camera): k_cull reruns only when these change
+  uint64_t cull_epoch = 0;
+  sptr_camera cull_cam{};
   uint32_t last_samples = 0;  // accumulation count after the last render
   // query scratch
   DevBuf qbuf;
