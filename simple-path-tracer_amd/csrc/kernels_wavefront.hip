@@ -37,6 +37,9 @@
 #ifndef SPTR_SHADE_WAVES
 #define SPTR_SHADE_WAVES 5  // 111 -> 96 VGPRs, 4 -> 5 waves, no spills: C2 shade 0.971 -> 0.907 ms
 #endif                      // (6 waves spills 48-76 B/lane; profiles/r01f_variants.txt)
+#ifndef SPTR_BOUNCE_WAVES
+#define SPTR_BOUNCE_WAVES 5
+#endif
 #ifndef SPTR_TAIL_WAVES
 #define SPTR_TAIL_WAVES 1
 #endif
@@ -1370,6 +1373,101 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   }
 }
 
+// --------------------------------------------------------------------------------- k_bounce
+// One whole bounce d >= 1 of an LDS-staged one-light scene in one launch: k_trace (closest hit; a
+// miss adds thr * env to rad[p]) and k_shade with its in-place shadow ray (emission, the light's
+// contribution if unoccluded, continuation) per queued ray, with the per-path operations and the
+// order of the radiance updates of the two kernels — so no hit-record stream and one launch less
+// per bounce.  Input: the rays of w.segN / rs[d & 1]; output: the continuation rays in this
+// block's segment of w.segH / rs[(d + 1) & 1] (the host alternates the two tables between bounces).
+template <bool kCube>
+__global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
+    k_bounce(SceneView sv, ShadeView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  const FrameView f = frame_dyn(fin);
+  extern __shared__ float4 lds[];
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + sv.lds_bytes / 16u);
+  __shared__ DevMaterial smat[32];
+  __shared__ uint32_t s_cnt_n, s_rays;
+  __shared__ LdsStack s_stack;
+  const uint32_t nm = stage_materials(sh, smat);
+  if (threadIdx.x == 0) s_cnt_n = s_rays = 0u;
+  const Staged sc = stage_scene<true>(sv, lds);
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += n;
+  const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
+  const bool last = (uint32_t)(depth + 1) >= f.max_depth;
+  Visits vc;
+  uint32_t rays = 0u;
+  const Sched sd = block_sched(n);
+  for (uint32_t base = sd.first; base < n; base += sd.step) {
+    const uint32_t i = base + threadIdx.x;
+    bool cont = false, dirty = false, lit = false;
+    uint32_t p = 0u, rng = 0u;
+    vec3 thr, radv = v3(0.0f, 0.0f, 0.0f), no, nd, so, ldir, contrib;
+    float stfar = 0.0f;
+    if (i < n) {
+      const uint32_t id = seg_slot(s_off, nseg_in, per_in, i);
+      const float4 o4 = rin.o[id], d4 = rin.d[id];
+      const vec3 ro = xyz(o4), rd = xyz(d4);
+      p = __float_as_uint(d4.w);
+      rng = __float_as_uint(o4.w);
+      thr = xyz(rin.thr[id]);
+      float tfar = __builtin_huge_valf();
+      uint32_t ref = kNoHit;
+      if (!traverse_w<false, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack)) {
+        if (sh.debug_mode == 1) {
+          w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+          const vec3 e = env_color<kCube>(sh.env, safe_renormalize_dir(rd));
+          w.rad[p] = f4(xyz(w.rad[p]) + thr * e, 0.0f);
+        }
+      } else if (sh.debug_mode == 1) {
+        radv = v3(1.0f, 1.0f, 1.0f);
+        dirty = true;
+      } else {
+        const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
+        const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
+        if (dot(emission, emission) > 0.0f) {
+          radv = xyz(w.rad[p]) + thr * emission;
+          dirty = true;
+        }
+        if (light_faces(sh.lights[0], sf)) lit = light_term(sh.lights[0], sf, -rd, thr, so, ldir, stfar, contrib);
+        cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
+      }
+    }
+    const uint32_t jn = block_append(&s_cnt_n, cont);
+    if (cont && sd.seg0 + jn >= w.seg_cap) {
+      cont = false;
+      w.tot[kTotOverflow] = 1ull;
+    }
+    if (cont) {
+      rout.o[sd.seg0 + jn] = f4(no, __uint_as_float(rng));
+      rout.d[sd.seg0 + jn] = f4(nd, __uint_as_float(p));
+      rout.thr[sd.seg0 + jn] = f4(thr, 0.0f);
+    }
+    if (lit) {
+      uint32_t ref = kNoHit;
+      ++rays;
+      if (!traverse_w<false, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, stfar, ref, vc, s_stack)) {
+        if (!dirty) radv = xyz(w.rad[p]);
+        dirty = true;
+        radv = radv + contrib;
+      }
+    }
+    if (dirty) w.rad[p] = f4(radv, 0.0f);
+  }
+  for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+  if (lane_id() == 0u) atomicAdd(&s_rays, rays);
+  report_stack(vc, w.tot);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    w.segH.cnt[logical_block()] = s_cnt_n;
+    w.bstat[blockIdx.x] += s_rays;
+    if (blockIdx.x == 0) *w.segH.per = sd.per;
+  }
+}
+
 // --------------------------------------------------------------------------------- k_shadow
 // One thread per shadow record: any-hit test of each of its light tasks in light order; the
 // unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
@@ -2366,6 +2464,20 @@ unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView&
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s) {
   if (f.P == 0u) return;
   hipLaunchKernelGGL(k_cull, dim3(f.P / kBlock), dim3(kBlock), 0, s, sv, f, mask);
+}
+
+unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                       uint32_t nseg, hipStream_t s) {
+  const unsigned lb = sv.lds_bytes + (4u * (nseg + 1u) + 15u) / 16u * 16u;
+  unsigned g;
+  if (sh.env.env != nullptr) {
+    g = resident_grid((const void*)&k_bounce<true>, lb);
+    hipLaunchKernelGGL(k_bounce<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+  } else {
+    g = resident_grid((const void*)&k_bounce<false>, lb);
+    hipLaunchKernelGGL(k_bounce<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+  }
+  return g;
 }
 
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count,

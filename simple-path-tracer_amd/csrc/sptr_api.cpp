@@ -420,6 +420,8 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
   return launches;
 }
 
+constexpr uint64_t kFuseBouncePaths = 1ull << 26;
+
 // Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
 uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
@@ -429,6 +431,11 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
   const bool fuse = shade_fuses_shadows(sv, sh, count);
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static const bool no_bounce = getenv("SPTR_NO_BOUNCE") != nullptr;
+#else
+  constexpr bool no_bounce = false;
+#endif
   // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it)
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
     // the mask depends on the scene, the pixel layout (both covered by the epoch) and the camera
@@ -449,15 +456,33 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     fv.pixel_major = bounce0_pixel_major(sv, fv);
     fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
+    // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
+    // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
+    // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
+    const bool fuse_bounce = fuse && !no_bounce && (uint64_t)fv.P * kk <= kFuseBouncePaths;
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
+    // fused bounces alternate the ray tables: the table holding the current rays, and the other
+    SegTable rays_tab = w.segN, spare_tab = w.segH;
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
+        WaveView wt = w;
+        wt.segN = rays_tab;
         tm.begin(7);
-        launch_tail(sv, sh, fv, w, d, g_shade, s);
+        launch_tail(sv, sh, fv, wt, d, g_shade, s);
         tm.end();
         break;
+      }
+      if (d >= 1 && fuse_bounce) {  // trace + shade (+ shadow) of this bounce in one launch
+        WaveView wf = w;
+        wf.segN = rays_tab;
+        wf.segH = spare_tab;
+        tm.begin(2);
+        g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, s);
+        tm.end();
+        std::swap(rays_tab, spare_tab);
+        continue;
       }
       tm.begin(d == 0 ? 5 : 1);
       if (d == 0 && fv.sky_fold) launch_sky(sh, fv, s);

@@ -312,6 +312,9 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
 bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count);
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                       uint32_t nseg, bool fuse, hipStream_t s);
+// one fused bounce (k_bounce): rays of w.segN in, continuation rays of w.segH out
+unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                       uint32_t nseg, hipStream_t s);
 unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth0,
                      uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
