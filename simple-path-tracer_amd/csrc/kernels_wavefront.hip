@@ -715,13 +715,23 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   return true;
 }
 // bit l of mask: pixel l is culled (see above); one ballot word pair per wave
-__global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask) {
+// plist: the valid pixels that are not culled, appended per wave (count at plist[P], zeroed before)
+__global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   int x = 0, y = 0;
-  const bool culled = l < f.P && local_pixel(f, l, x, y) && pixel_frustum_misses(sv, f, x, y);
+  const bool valid = l < f.P && local_pixel(f, l, x, y);
+  const bool culled = valid && pixel_frustum_misses(sv, f, x, y);
   const unsigned long long b = __ballot(culled);
   const uint32_t lane = lane_id();
   if ((lane & 31u) == 0u && l < f.P) mask[l >> 5] = (uint32_t)(b >> lane);
+  const unsigned long long m = __ballot(valid && !culled);
+  if (m) {
+    const int leader = __ffsll(m) - 1;
+    uint32_t base = 0u;
+    if ((int)lane == leader) base = atomicAdd(&plist[f.P], (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (valid && !culled) plist[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = l;
+  }
 }
 __device__ __forceinline__ bool pixel_culled(const FrameView& f, uint32_t l) {
   return f.cull != nullptr && ((f.cull[l >> 5] >> (l & 31u)) & 1u) != 0u;
@@ -1009,9 +1019,12 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   const Staged sc = stage_scene<kLds>(sv, lds);
   // Bounce 0 path-major (thread <- path slot): batches of fewer than kWaveFoldMinK samples (e.g.
   // the interactive 1 spp per call).  Later bounces: thread <- queued ray.
-  uint32_t n, per_in = 0u;
+  uint32_t n, per_in = 0u, nlist = 0u;
   if (kPrimary) {
-    n = f.P * f.k;
+    // with a cull list (f.plist, path-major + k_sky) only the unculled pixels' paths are traced:
+    // compacted item i -> sample i / Q of listed pixel i % Q, so waves hold no culled lanes
+    nlist = f.plist ? f.plist[f.P] : 0u;
+    n = f.plist ? nlist * f.k : f.P * f.k;
     __syncthreads();
   } else {
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
@@ -1030,11 +1043,14 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     if (active) {
       if (kPrimary) {
         Primary pr;
-        uint32_t l;
-        id = pid = i;
-        active = primary_path(f, idiv, i, pr, l);
-        culled = pixel_culled(f, l);
-        if (culled && f.sky_fold) active = false;  // summed by k_sky
+        uint32_t l, p = i;
+        if (f.plist) {
+          const uint32_t smp = i / nlist;
+          p = smp * f.P + f.plist[i - smp * nlist];
+        }
+        id = pid = p;
+        active = primary_path(f, idiv, p, pr, l);
+        culled = !f.plist && pixel_culled(f, l);
         o = f.cam_pos;
         d = pr.d;
       } else {
@@ -2461,9 +2477,9 @@ unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView&
       Flags<>{}, depth == 0, fuse);
 }
 
-void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s) {
+void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s) {
   if (f.P == 0u) return;
-  hipLaunchKernelGGL(k_cull, dim3(f.P / kBlock), dim3(kBlock), 0, s, sv, f, mask);
+  hipLaunchKernelGGL(k_cull, dim3(f.P / kBlock), dim3(kBlock), 0, s, sv, f, mask, plist);
 }
 
 unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,

@@ -199,6 +199,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.dyn = nullptr;
   v.cull = nullptr;
   v.sky_fold = 0u;
+  v.plist = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -342,6 +343,7 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
   API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
   API_HIP(ensure_buf(c.cull, (size_t)c.P / 32u * 4u + 4u));
+  API_HIP(ensure_buf(c.plist, ((size_t)c.P + 1u) * 4u));
   ++c.epoch;
   API_HIP(hipMemsetAsync(c.accum.p, 0, (size_t)c.P * 16, s));
   API_HIP(hipMemsetAsync(c.tiles.p, 0, (size_t)c.P * 4, s));
@@ -440,7 +442,8 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
     // the mask depends on the scene, the pixel layout (both covered by the epoch) and the camera
     if (c.cull_epoch != c.epoch || std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) != 0) {
-      launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), s);
+      API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 4, s));
+      launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
       c.cull_epoch = c.epoch;
       c.cull_cam = f.camera;
     }
@@ -456,6 +459,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     fv.pixel_major = bounce0_pixel_major(sv, fv);
     fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
+    fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
@@ -693,7 +697,7 @@ int sptr_destroy(sptr_ctx* x) {
   (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_hrec, &c.w_rad,   &c.w_stask,
-                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf, &c.nodes4, &c.cull};
+                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf, &c.nodes4, &c.cull, &c.plist};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& b : c.w_rs)
     for (DevBuf& x : b) free_buf(x);

@@ -156,6 +156,7 @@ struct FrameView {
   uint32_t ox_has_light;
   const uint32_t* cull;  // bit l: camera rays through local pixel l cannot hit the scene (k_cull); may be null
   uint32_t sky_fold;     // path-major bounce 0 with a cull mask: k_sky sums culled pixels into accum
+  const uint32_t* plist; // with sky_fold: the unculled local pixels (count at plist[P]), bounce 0's paths
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -282,7 +283,8 @@ struct Context {
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;
   DevBuf accum, tiles, image;
-  DevBuf cull;  // bounce-0 pixel-frustum cull mask, 1 bit per local pixel (k_cull)
+  DevBuf cull;   // bounce-0 pixel-frustum cull mask, 1 bit per local pixel (k_cull)
+  DevBuf plist;  // the local pixels k_cull did not cull, in no particular order; their count at [P]
   // what the mask was computed for (state epoch, camera): k_cull reruns only when these change
   uint64_t cull_epoch = 0;
   sptr_camera cull_cam{};
@@ -321,7 +323,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
                    hipStream_t s);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
-void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, hipStream_t s);
+void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s);
 void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
