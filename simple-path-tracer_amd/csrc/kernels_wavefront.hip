@@ -67,6 +67,8 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* s_cnt, bool pred) {
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+// Block-local work counter: every lane with pred takes the next index (one LDS atomic per wave).
+__device__ __forceinline__ uint32_t block_take(uint32_t* s_next, bool pred) { return block_append(s_next, pred); }
 // XCD-aware logical block index.  Workgroups are dispatched round-robin over the 8 XCDs, so with
 // the identity mapping neighbouring slices (neighbouring image regions for bounce 0) land on
 // different XCDs and every XCD's private 4 MB L2 has to hold the BVH working set of the whole
@@ -476,20 +478,22 @@ __device__ __forceinline__ bool q_slab(int k, const QAxis& x, const QAxis& y, co
 
 // Wide-BVH traversal: kWide slab tests per quantised node; leaf children are tested as soon as their
 // box is hit; the nearest internal child is visited next (lowest slot on ties) and the other hit
-// children are pushed, highest slot first.
+// children are pushed, highest slot first.  Written as a resumable walk (WideWalk: the node to
+// visit next, the stack depth, whether a hit was found) so that the refilling kernels
+// (k_trace_dyn, k_shadow_dyn) can run a ray a few node visits at a time; traverse_wide runs it to
+// the end in one go.
+struct WideWalk {
+  uint32_t cur;
+  int sp;
+  bool hit;
+};
+// up to `steps` node visits; true when the traversal is over
 template <bool kAny, bool kCount, int N>
-__device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint32_t* prim_ref, const float4* tris,
-                                              const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                              uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
-  if (root == kNoHit) return false;
-  if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-  TravStack<N> stack;
-  stack.lds = &ls.e[0][threadIdx.x];
-  int sp = 0;
-  uint32_t cur = root;
-  bool hit = false;
-  for (;;) {
-    const uint4* nq = reinterpret_cast<const uint4*>(nodes + cur);
+__device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes,
+                                          const uint32_t* prim_ref, const float4* tris, const float4* sph, const Ray& r,
+                                          float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  for (int it = 0; it < steps; ++it) {
+    const uint4* nq = reinterpret_cast<const uint4*>(nodes + wk.cur);
     const uint4 h = nq[0];
     uint32_t ln[kWide], qw[6 * kQWords];
 #pragma unroll
@@ -520,7 +524,7 @@ __device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint3
     for (int k = 0; k < kWide; ++k) {
       if (hc[k] && (ln[k] & kLeafBit)) {
         if (leaf_test<kAny, kCount>(ln[k], prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
-          hit = true;
+          wk.hit = true;
           if (kAny) return true;
         }
         hc[k] = false;
@@ -538,17 +542,43 @@ __device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint3
       npush += hc[k] ? 1u : 0u;
     }
     if (kn < kWide) {
-      if (sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
+      if (wk.sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
 #pragma unroll
       for (int k = kWide - 1; k >= 0; --k)
-        if (hc[k] && k != kn && sp < kStack) stack.put(sp++, ln[k]);
-      cur = ln[kn];
+        if (hc[k] && k != kn && wk.sp < kStack) stack.put(wk.sp++, ln[k]);
+      wk.cur = ln[kn];
     } else {
-      if (sp == 0) break;
-      cur = stack.get(--sp);
+      if (wk.sp == 0) return true;
+      wk.cur = stack.get(--wk.sp);
     }
   }
-  return hit;
+  return false;
+}
+// Starts a walk at root; true when it is already over (empty scene, or a root leaf tested here).
+template <bool kAny, bool kCount>
+__device__ __forceinline__ bool wide_start(WideWalk& wk, uint32_t root, const uint32_t* prim_ref, const float4* tris,
+                                           const float4* sph, const Ray& r, float tnear, float& tfar, uint32_t& ref,
+                                           Visits& vc) {
+  wk.cur = root;
+  wk.sp = 0;
+  wk.hit = false;
+  if (root == kNoHit) return true;
+  if (root & kLeafBit) {
+    wk.hit = leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
+    return true;
+  }
+  return false;
+}
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint32_t* prim_ref, const float4* tris,
+                                              const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
+                                              uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
+  WideWalk wk;
+  if (wide_start<kAny, kCount>(wk, root, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) return wk.hit;
+  TravStack<N> stack;
+  stack.lds = &ls.e[0][threadIdx.x];
+  (void)wide_walk<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc, 0x7FFFFFFF);
+  return wk.hit;
 }
 
 // Stage the whole scene (nodes, triangles, spheres) into LDS when it fits (SceneView::lds_bytes).
@@ -1090,6 +1120,123 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
+// --------------------------------------------------------------------------------- refilling trace
+// k_trace for wide BVHs traversed from L2/HBM (C3, C5): the same per-ray work, but each lane takes
+// a new ray from the block's items as soon as its current one is done, instead of waiting for the
+// slowest lane of its wave.  Rays there differ in cost by orders of magnitude (a sky ray ends after
+// one node, a ray into a 10M-triangle mesh visits dozens), so a statically assigned wave holds its
+// registers for its longest ray with most lanes idle; refilling keeps the wave's lanes, and with
+// them the memory requests in flight, busy.  Lanes advance kDynSteps node visits between refills.
+// The block still owns exactly the items of its static schedule (chunk c: sd.first + c * sd.step
+// + [0, kBlock)), so its hit-record segment and the consumer's mapping are unchanged.
+#ifndef SPTR_DYN_STEPS
+#define SPTR_DYN_STEPS 8
+#endif
+constexpr int kDynSteps = SPTR_DYN_STEPS;
+__device__ __forceinline__ uint32_t block_items(const Sched& sd, uint32_t n) {
+  if (sd.first >= n) return 0u;
+  const uint32_t rest = n - sd.first, full = rest / sd.step, tail = rest - full * sd.step;
+  return full * kBlock + (tail < kBlock ? tail : kBlock);
+}
+__device__ __forceinline__ uint32_t block_item(const Sched& sd, uint32_t k) {
+  return sd.first + (k / kBlock) * sd.step + (k % kBlock);
+}
+
+template <bool kCount, bool kPrimary, bool kCube>
+__global__ void __launch_bounds__(kBlock, kPrimary ? SPTR_TRACE_WAVES : SPTR_TRACE4_WAVES)
+    k_trace_dyn(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  const FrameView f = frame_dyn(fin);
+  __shared__ KernelStack<false> s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_cnt, s_next;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
+  if (threadIdx.x == 0) s_cnt = s_next = 0u;
+  uint32_t n, per_in = 0u, nlist = 0u;
+  if (kPrimary) {
+    nlist = f.plist ? f.plist[f.P] : 0u;
+    n = f.plist ? nlist * f.k : f.P * f.k;
+    __syncthreads();
+  } else {
+    n = seg_scan(w.segN, nseg_in, s_off, per_in);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+  const ImageDiv idiv = image_div(f);
+  const RayStream rs = w.rs[depth & 1];
+  Visits vc;
+  const Sched sd = block_sched(n);
+  const uint32_t nb = block_items(sd, n);
+  TravStack<kLdsStackG> stack;
+  stack.lds = &s_stack.e[0][threadIdx.x];
+  bool have = false, done = false;
+  uint32_t id = 0u, pid = 0u, ref = kNoHit;
+  float tfar = 0.0f;
+  Ray r;
+  WideWalk wk;
+  for (;;) {
+    const uint32_t k = block_take(&s_next, !have);
+    if (!have && k < nb) {
+      const uint32_t i = block_item(sd, k);
+      bool valid = true, culled = false;
+      vec3 o, d;
+      if (kPrimary) {
+        Primary pr;
+        uint32_t l, p = i;
+        if (f.plist) {
+          const uint32_t smp = i / nlist;
+          p = smp * f.P + f.plist[i - smp * nlist];
+        }
+        id = pid = p;
+        valid = primary_path(f, idiv, p, pr, l);
+        culled = !f.plist && pixel_culled(f, l);
+        o = f.cam_pos;
+        d = pr.d;
+      } else {
+        id = seg_slot(s_off, nseg_in, per_in, i);
+        const float4 o4 = rs.o[id], d4 = rs.d[id];
+        o = xyz(o4);
+        d = xyz(d4);
+        pid = __float_as_uint(d4.w);
+      }
+      if (valid) {
+        r = make_ray(o, d);
+        tfar = __builtin_huge_valf();
+        ref = kNoHit;
+        done = wide_start<false, kCount>(wk, culled ? kNoHit : sv.root4, sv.prim_ref, sv.tris, sv.sph, r, 0.0f, tfar,
+                                         ref, vc);
+        have = true;
+      }
+    }
+    if (__ballot(have) == 0ull) {
+      if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
+      continue;                                       // only invalid (outside-image) items taken
+    }
+    if (have && !done)
+      done = wide_walk<false, kCount>(wk, stack, sv.nodes4, sv.prim_ref, sv.tris, sv.sph, r, 0.0f, tfar, ref, vc,
+                                      kDynSteps);
+    const bool fin = have && done;
+    if (fin && !wk.hit) {
+      if (sh.debug_mode == 1) {
+        w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else {
+        const vec3 e = env_color<kCube>(sh, safe_renormalize_dir(r.d));
+        vec3 rv;
+        if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+        else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
+        w.rad[pid] = f4(rv, 0.0f);
+      }
+    }
+    const uint32_t j = block_append(&s_cnt, fin && wk.hit);
+    if (fin && wk.hit) {
+      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+      else w.tot[kTotOverflow] = 1ull;
+    }
+    if (fin) have = false;
+  }
+  seg_publish(w.segH, &s_cnt, sd.per);
+  report_stack(vc, w.tot);
+  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+}
+
 // --------------------------------------------------------------------------------- shading steps
 // The per-hit steps of WavefrontPathTracerCPU::traceRay (wf_pt_cpu.cpp:106-247), shared by the
 // wavefront k_shade and the path-per-thread k_tail so both evaluate every path identically.
@@ -1528,6 +1675,72 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
       }
     }
     if (any) w.rad[p] = f4(rv, 0.0f);
+  }
+  for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+  if (lane_id() == 0u) atomicAdd(&s_rays, rays);
+  __syncthreads();
+  if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
+  report_stack(vc, w.tot);
+  if (kCount) flush_visits(vc, w.tot, kTotShNodes);
+}
+
+// k_shadow for wide BVHs traversed from L2/HBM with one light (C3, C5): the any-hit queries of the
+// shadow records, with lanes refilled as in k_trace_dyn.  Per record: the same query, and the same
+// radiance update when it is unoccluded.
+template <bool kCount>
+__global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(SceneView sv, ShadeView sh, WaveView w, int depth,
+                                                                           uint32_t nseg_in) {
+  __shared__ KernelStack<false> s_stack;
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_rays, s_next;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
+  if (threadIdx.x == 0) s_rays = s_next = 0u;
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
+  const uint32_t ts = w.tstride;
+  Visits vc;
+  uint32_t rays = 0u;
+  const Sched sd = block_sched(n);
+  const uint32_t nb = block_items(sd, n);
+  TravStack<kLdsStackG> stack;
+  stack.lds = &s_stack.e[0][threadIdx.x];
+  bool have = false, done = false;
+  uint32_t p = 0u, ref = kNoHit;
+  float tfar = 0.0f;
+  vec3 contrib;
+  Ray r;
+  WideWalk wk;
+  for (;;) {
+    const uint32_t k = block_take(&s_next, !have);
+    if (!have && k < nb) {
+      const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, block_item(sd, k)) * ts;
+      const float4 c = task[1];
+      const uint32_t tag = __float_as_uint(c.w);
+      if (tag != 0u) {
+        p = tag - 1u;
+        contrib = xyz(c);
+        const float4 a = task[0];
+        const vec3 dir = (ts > 2u && sh.lights[0].type != 0) ? xyz(task[2])
+                                                            : v3(sh.lights[0].v[0], sh.lights[0].v[1], sh.lights[0].v[2]);
+        r = make_ray(xyz(a), dir);
+        tfar = a.w;
+        ref = kNoHit;
+        ++rays;
+        done = wide_start<true, kCount>(wk, sv.root4, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref, vc);
+        have = true;
+      }
+    }
+    if (__ballot(have) == 0ull) {
+      if (__ballot(!have && k < nb) == 0ull) break;
+      continue;
+    }
+    if (have && !done)
+      done = wide_walk<true, kCount>(wk, stack, sv.nodes4, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref, vc,
+                                     kDynSteps);
+    if (have && done) {
+      if (!wk.hit) w.rad[p] = f4(xyz(w.rad[p]) + contrib, 0.0f);
+      have = false;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
   if (lane_id() == 0u) atomicAdd(&s_rays, rays);
@@ -2412,6 +2625,16 @@ static unsigned dispatch(Fn&& fn, Flags<B...>, bool first, Rest... rest) {
   return first ? dispatch(fn, Flags<B..., true>{}, rest...) : dispatch(fn, Flags<B..., false>{}, rest...);
 }
 
+// experiment knob: SPTR_NO_DYN keeps the statically scheduled trace/shadow kernels for wide BVHs
+static bool no_dyn() {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static const bool v = getenv("SPTR_NO_DYN") != nullptr;
+  return v;
+#else
+  return false;
+#endif
+}
+
 unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                       bool count, uint32_t nseg, hipStream_t s) {
   const dim3 b(kBlock);
@@ -2442,6 +2665,17 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
           }(fl);
         },
         Flags<>{}, count, W, cube);
+  }
+  if (!L && W && !no_dyn()) {  // wide BVH from L2/HBM: refilling lanes
+    return dispatch(
+        [&](auto fl) -> unsigned {
+          return [&]<bool C, bool Pc, bool Cube>(Flags<C, Pc, Cube>) {
+            const unsigned g = resident_grid((const void*)&k_trace_dyn<C, Pc, Cube>, lb);
+            hipLaunchKernelGGL((k_trace_dyn<C, Pc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
+            return g;
+          }(fl);
+        },
+        Flags<>{}, count, P, cube);
   }
   return dispatch(
       [&](auto fl) -> unsigned {
@@ -2503,6 +2737,16 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   const bool W = sv.width == (uint32_t)kWide;
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
+  if (!L && W && w.L == 1u && !no_dyn()) {  // wide BVH from L2/HBM, one light: refilling lanes
+    if (count) {
+      g = resident_grid((const void*)&k_shadow_dyn<true>, lb);
+      hipLaunchKernelGGL(k_shadow_dyn<true>, dim3(g), b, lb, s, sv, sh, w, depth, nseg);
+    } else {
+      g = resident_grid((const void*)&k_shadow_dyn<false>, lb);
+      hipLaunchKernelGGL(k_shadow_dyn<false>, dim3(g), b, lb, s, sv, sh, w, depth, nseg);
+    }
+    return g;
+  }
 #define SPTR_SHADOW(Lc, C, Wc)                                                                      \
   do {                                                                                              \
     g = resident_grid((const void*)&k_shadow<Lc, C, Wc>, lb);                                       \
