@@ -384,18 +384,13 @@ using KernelStack = LdsStackN<kLds ? kLdsStack : kLdsStackG>;
 static_assert(sizeof(LdsStack) % 16 == 0 && sizeof(LdsStackN<kLdsStackG>) % 16 == 0, "keeps the dynamic-LDS base aligned");
 
 // BVH2 stack traversal: nearest child first; leaf children are tested as soon as their box is hit.
+// Resumable BVH2 walk (the WideWalk state): up to `steps` node visits; true when the traversal is
+// over.  traverse runs it to the end in one go.
 template <bool kAny, bool kCount, int N>
-__device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* prim_ref, const float4* tris,
-                                         const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
-                                         uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
-  if (root == kNoHit) return false;
-  if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-  TravStack<N> stack;
-  stack.lds = &ls.e[0][threadIdx.x];
-  int sp = 0;
-  uint32_t cur = root;
-  bool hit = false;
-  for (;;) {
+__device__ __forceinline__ bool bvh2_walk(uint32_t& cur, int& sp, bool& hit, TravStack<N>& stack, const BvhNode* nodes,
+                                          const uint32_t* prim_ref, const float4* tris, const float4* sph, const Ray& r,
+                                          float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  for (int it = 0; it < steps; ++it) {
     const BvhNode* nd = nodes + cur;
     const float4 lxy = nd->lxy, rxy = nd->rxy, z = nd->z;
     const uint4 ln = nd->link;
@@ -432,10 +427,24 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
     } else if (hr) {
       cur = R;
     } else {
-      if (sp == 0) break;
+      if (sp == 0) return true;
       cur = stack.get(--sp);
     }
   }
+  return false;
+}
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* prim_ref, const float4* tris,
+                                         const float4* sph, uint32_t root, const Ray& r, float tnear, float& tfar,
+                                         uint32_t& ref, Visits& vc, LdsStackN<N>& ls) {
+  if (root == kNoHit) return false;
+  if (root & kLeafBit) return leaf_test<kAny, kCount>(root, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
+  TravStack<N> stack;
+  stack.lds = &ls.e[0][threadIdx.x];
+  int sp = 0;
+  uint32_t cur = root;
+  bool hit = false;
+  (void)bvh2_walk<kAny, kCount>(cur, sp, hit, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc, 0x7FFFFFFF);
   return hit;
 }
 
@@ -1120,6 +1129,20 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (kCount) flush_visits(vc, w.tot, kTotNodes);
 }
 
+// BVH2 (LDS-staged) or wide walk over the staged / global scene pointers
+template <bool kAny, bool kCount, bool kW4>
+__device__ __forceinline__ bool walk_start(WideWalk& wk, const Staged& sc, uint32_t root, const Ray& r, float tnear,
+                                           float& tfar, uint32_t& ref, Visits& vc) {
+  return wide_start<kAny, kCount>(wk, root, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc);
+}
+template <bool kAny, bool kCount, bool kW4, int N>
+__device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const Ray& r, float tnear,
+                                           float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  if (kW4) return wide_walk<kAny, kCount>(wk, stack, sc.nodes4, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc, steps);
+  return bvh2_walk<kAny, kCount>(wk.cur, wk.sp, wk.hit, stack, sc.nodes, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref,
+                                 vc, steps);
+}
+
 // --------------------------------------------------------------------------------- refilling trace
 // k_trace for wide BVHs traversed from L2/HBM (C3, C5): the same per-ray work, but each lane takes
 // a new ray from the block's items as soon as its current one is done, instead of waiting for the
@@ -1133,6 +1156,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
 #define SPTR_DYN_STEPS 8
 #endif
 constexpr int kDynSteps = SPTR_DYN_STEPS;
+#ifndef SPTR_DYN_LDS
+#define SPTR_DYN_LDS 0  // LDS-staged BVH2 bounces: refilling measured 2-3 % slower on C2 (short, even traversals)
+#endif
+constexpr bool kDynLds = SPTR_DYN_LDS != 0;
 __device__ __forceinline__ uint32_t block_items(const Sched& sd, uint32_t n) {
   if (sd.first >= n) return 0u;
   const uint32_t rest = n - sd.first, full = rest / sd.step, tail = rest - full * sd.step;
@@ -1142,15 +1169,16 @@ __device__ __forceinline__ uint32_t block_item(const Sched& sd, uint32_t k) {
   return sd.first + (k / kBlock) * sd.step + (k % kBlock);
 }
 
-template <bool kCount, bool kPrimary, bool kCube>
-__global__ void __launch_bounds__(kBlock, kPrimary ? SPTR_TRACE_WAVES : SPTR_TRACE4_WAVES)
+template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace_dyn(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
   const FrameView f = frame_dyn(fin);
-  __shared__ KernelStack<false> s_stack;
+  __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt, s_next;
-  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = s_next = 0u;
+  const Staged sc = stage_scene<kLds>(sv, lds);
   uint32_t n, per_in = 0u, nlist = 0u;
   if (kPrimary) {
     nlist = f.plist ? f.plist[f.P] : 0u;
@@ -1165,7 +1193,7 @@ __global__ void __launch_bounds__(kBlock, kPrimary ? SPTR_TRACE_WAVES : SPTR_TRA
   Visits vc;
   const Sched sd = block_sched(n);
   const uint32_t nb = block_items(sd, n);
-  TravStack<kLdsStackG> stack;
+  TravStack<kLds ? kLdsStack : kLdsStackG> stack;
   stack.lds = &s_stack.e[0][threadIdx.x];
   bool have = false, done = false;
   uint32_t id = 0u, pid = 0u, ref = kNoHit;
@@ -1201,8 +1229,8 @@ __global__ void __launch_bounds__(kBlock, kPrimary ? SPTR_TRACE_WAVES : SPTR_TRA
         r = make_ray(o, d);
         tfar = __builtin_huge_valf();
         ref = kNoHit;
-        done = wide_start<false, kCount>(wk, culled ? kNoHit : sv.root4, sv.prim_ref, sv.tris, sv.sph, r, 0.0f, tfar,
-                                         ref, vc);
+        done = walk_start<false, kCount, kW4>(wk, sc, culled ? kNoHit : (kW4 ? sv.root4 : sv.root), r, 0.0f, tfar, ref,
+                                              vc);
         have = true;
       }
     }
@@ -1210,9 +1238,7 @@ __global__ void __launch_bounds__(kBlock, kPrimary ? SPTR_TRACE_WAVES : SPTR_TRA
       if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
       continue;                                       // only invalid (outside-image) items taken
     }
-    if (have && !done)
-      done = wide_walk<false, kCount>(wk, stack, sv.nodes4, sv.prim_ref, sv.tris, sv.sph, r, 0.0f, tfar, ref, vc,
-                                      kDynSteps);
+    if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, r, 0.0f, tfar, ref, vc, kDynSteps);
     const bool fin = have && done;
     if (fin && !wk.hit) {
       if (sh.debug_mode == 1) {
@@ -2625,7 +2651,16 @@ static unsigned dispatch(Fn&& fn, Flags<B...>, bool first, Rest... rest) {
   return first ? dispatch(fn, Flags<B..., true>{}, rest...) : dispatch(fn, Flags<B..., false>{}, rest...);
 }
 
-// experiment knob: SPTR_NO_DYN keeps the statically scheduled trace/shadow kernels for wide BVHs
+// experiment knobs: SPTR_NO_DYN keeps the statically scheduled trace/shadow kernels for wide BVHs;
+// SPTR_DYN_LDS=0/1 selects the refilling trace for the later bounces of LDS-staged scenes
+static bool dyn_lds() {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static const bool v = getenv("SPTR_DYN_LDS") ? atoi(getenv("SPTR_DYN_LDS")) != 0 : kDynLds;
+  return v;
+#else
+  return kDynLds;
+#endif
+}
 static bool no_dyn() {
 #ifdef SPTR_EXPERIMENT_KNOBS
   static const bool v = getenv("SPTR_NO_DYN") != nullptr;
@@ -2666,16 +2701,20 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         },
         Flags<>{}, count, W, cube);
   }
-  if (!L && W && !no_dyn()) {  // wide BVH from L2/HBM: refilling lanes
+  if (((!L && W) || (L && !W && !P && dyn_lds())) && !no_dyn()) {  // refilling lanes
     return dispatch(
         [&](auto fl) -> unsigned {
-          return [&]<bool C, bool Pc, bool Cube>(Flags<C, Pc, Cube>) {
-            const unsigned g = resident_grid((const void*)&k_trace_dyn<C, Pc, Cube>, lb);
-            hipLaunchKernelGGL((k_trace_dyn<C, Pc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
-            return g;
+          return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube>(Flags<Lc, C, Pc, Wc, Cube>) {
+            if constexpr (Lc == Wc) {
+              return 0u;  // not instantiated: LDS scenes traverse BVH2, L2/HBM scenes the wide BVH
+            } else {
+              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube>, lb);
+              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
+              return g;
+            }
           }(fl);
         },
-        Flags<>{}, count, P, cube);
+        Flags<>{}, L, count, P, W, cube);
   }
   return dispatch(
       [&](auto fl) -> unsigned {
