@@ -821,30 +821,32 @@ __device__ __forceinline__ vec3 env_color(const EnvView& sh, vec3 dir) {
   if (!kCube) return sky_color(dir);
   const vec3 d = renormalize_dir(dir);
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-  float ma, uc, vc;
-  int face;
-  if (ax >= ay && ax >= az) {
-    ma = ax;
-    if (d.x > 0) { face = 0; uc = -d.z; vc = -d.y; }
-    else         { face = 1; uc = d.z;  vc = -d.y; }
-  } else if (ay >= ax && ay >= az) {
-    ma = ay;
-    if (d.y > 0) { face = 2; uc = d.x; vc = d.z; }
-    else         { face = 3; uc = d.x; vc = -d.z; }
-  } else {
-    ma = az;
-    if (d.z > 0) { face = 4; uc = d.x;  vc = -d.y; }
-    else         { face = 5; uc = -d.x; vc = -d.y; }
-  }
-  const float u = clamp_g((uc / ma + 1.0f) * 0.5f, 0.0f, 1.0f);
-  const float v = clamp_g((vc / ma + 1.0f) * 0.5f, 0.0f, 1.0f);
+  // Cubemap::directionToUV's face cases as selects (no divergent branches): x-major, else y-major,
+  // else z-major, in the reference's order of tests
+  const bool xm = ax >= ay && ax >= az;
+  const bool ym = !xm && ay >= ax && ay >= az;
+  const float ma = xm ? ax : (ym ? ay : az);
+  const bool pos = xm ? d.x > 0.0f : (ym ? d.y > 0.0f : d.z > 0.0f);
+  const int face = (xm ? 0 : (ym ? 2 : 4)) + (pos ? 0 : 1);
+  const float uc = xm ? (pos ? -d.z : d.z) : (ym ? d.x : (pos ? d.x : -d.x));
+  const float vc = xm ? -d.y : (ym ? (pos ? d.z : -d.z) : -d.y);
+  // uc / ma and vc / ma share the divisor (ma in [1/sqrt(3), 1]): correctly rounded for |uc| >=
+  // 2^-100 (cr_math.h div_nrm, checked by tests/hip/crmath_check.hip); below that the quotient is
+  // under 2^-99 either way and q + 1 rounds to 1 exactly
+  const DivBy dm = div_by(ma);
+  const float u = clamp_g((div_nrm(uc, dm) + 1.0f) * 0.5f, 0.0f, 1.0f);
+  const float v = clamp_g((div_nrm(vc, dm) + 1.0f) * 0.5f, 0.0f, 1.0f);
   const int S = sh.env_size;
   const float fx_ = u * float(S - 1), fy_ = v * float(S - 1);
   const int x0 = (int)floorf(fx_), y0 = (int)floorf(fy_);
   const int x1 = min(x0 + 1, S - 1), y1 = min(y0 + 1, S - 1);
   const float fx = fx_ - float(x0), fy = fy_ - float(y0);
-  const vec3 c0 = mix(cube_texel(sh.env, S, face, x0, y0), cube_texel(sh.env, S, face, x1, y0), fx);
-  const vec3 c1 = mix(cube_texel(sh.env, S, face, x0, y1), cube_texel(sh.env, S, face, x1, y1), fx);
+  // texel (face, x, y) = env[(face * S + y) * S + x]; 24-bit multiplies (S <= 4096)
+  const uint32_t r0 = __umul24((uint32_t)(face * S + y0), (uint32_t)S), r1 = __umul24((uint32_t)(face * S + y1), (uint32_t)S);
+  const float4 t00 = sh.env[r0 + (uint32_t)x0], t10 = sh.env[r0 + (uint32_t)x1];
+  const float4 t01 = sh.env[r1 + (uint32_t)x0], t11 = sh.env[r1 + (uint32_t)x1];
+  const vec3 c0 = mix(xyz(t00), xyz(t10), fx);
+  const vec3 c1 = mix(xyz(t01), xyz(t11), fx);
   vec3 c = mix(c0, c1, fy);
   c = v3(fmin_g(c.x, sh.env_clamp), fmin_g(c.y, sh.env_clamp), fmin_g(c.z, sh.env_clamp));
   return c * sh.env_intensity;

@@ -6,7 +6,8 @@
 //              1024 ulps of 1.0, general sequence elsewhere) over the same floats
 //   inv_len  : every one of the 2^32 float bit patterns (NaN == NaN), against 1.0f / sqrtf(x)
 //   div_nrm  : divisors 1..8192 and the bench/test image sizes, 2^22 dividends each of the form
-//              float(x) + j (x integer pixel coordinate < b, j a 24-bit jitter), plus random floats
+//              float(x) + j (x integer pixel coordinate < b, j a 24-bit jitter), plus random floats;
+//              and 2^30 random pairs with divisors in [1/2, 1), dividends in [-1, 1] down to 2^-100
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -17,8 +18,8 @@
 
 using namespace sptr;
 
-__device__ unsigned long long g_bad[4];
-__device__ unsigned int g_first[4];
+__device__ unsigned long long g_bad[5];
+__device__ unsigned int g_first[5];
 
 __global__ void k_sqrt(uint32_t lo, uint32_t hi) {
   for (uint64_t u = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= hi; u += (uint64_t)gridDim.x * blockDim.x) {
@@ -83,9 +84,24 @@ __global__ void k_div(const float* divisors, int nd, uint32_t samples) {
   }
 }
 
+// divisors in [1/2, 1) (the cubemap's major axis, 1/sqrt(3)..1), dividends in [-1, 1] with exponents
+// down to 2^-100 (the face coordinates): 2^30 random pairs
+__global__ void k_div_unit(uint32_t samples) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < samples; s += gridDim.x * blockDim.x) {
+    const uint32_t h = hash(s * 2654435761u + 12345u), g = hash(h ^ 0x9E3779B9u);
+    const float b = __uint_as_float(0x3F000000u | (h & 0x007FFFFFu));                         // [0.5, 1)
+    const uint32_t e = 27u + g % 100u;                                                          // 2^-100 .. 2^-1
+    const float a = __uint_as_float(((g >> 8) & 1u) << 31 | e << 23 | (hash(g) & 0x007FFFFFu));
+    if (__float_as_uint(div_nrm(a, div_by(b))) != __float_as_uint(a / b)) {
+      atomicAdd(&g_bad[4], 1ull);
+      atomicMin(&g_first[4], __float_as_uint(a));
+    }
+  }
+}
+
 int main() {
-  const unsigned long long zero[4] = {0, 0, 0, 0};
-  const unsigned int big[4] = {~0u, ~0u, ~0u, ~0u};
+  const unsigned long long zero[5] = {0, 0, 0, 0, 0};
+  const unsigned int big[5] = {~0u, ~0u, ~0u, ~0u, ~0u};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_first), big, sizeof(big));
   const uint32_t s_lo = 0x0F800000u, s_hi = 0x71800000u;  // 2^-96 .. 2^100
@@ -100,17 +116,19 @@ int main() {
   (void)hipMalloc(&ddv, dv.size() * sizeof(float));
   (void)hipMemcpy(ddv, dv.data(), dv.size() * sizeof(float), hipMemcpyHostToDevice);
   hipLaunchKernelGGL(k_div, dim3(16, (unsigned)dv.size()), dim3(256), 0, 0, ddv, (int)dv.size(), 1u << 18);
+  hipLaunchKernelGGL(k_div_unit, dim3(8192), dim3(256), 0, 0, 1u << 30);
   if (hipDeviceSynchronize() != hipSuccess) {
     std::printf("hip error\n");
     return 2;
   }
-  unsigned long long bad[4];
-  unsigned int first[4];
+  unsigned long long bad[5];
+  unsigned int first[5];
   (void)hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad));
   (void)hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first));
-  const char* names[4] = {"sqrt_nrm", "rcp_nrm/inv_len_nrm/inv_len_unit", "div_nrm", "inv_len (all 2^32)"};
+  const char* names[5] = {"sqrt_nrm", "rcp_nrm/inv_len_nrm/inv_len_unit", "div_nrm", "inv_len (all 2^32)",
+                          "div_nrm unit divisors"};
   int rc = 0;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     std::printf("%s: %llu mismatches%s", names[i], bad[i], bad[i] ? "" : "\n");
     if (bad[i]) {
       std::printf(" (first input bits 0x%08x)\n", first[i]);

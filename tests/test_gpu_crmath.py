@@ -18,4 +18,4 @@ def test_cr_math_bit_exact(tmp_path):
                    check=True, capture_output=True, timeout=300)
     res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stdout + res.stderr
-    assert res.stdout.count(" 0 mismatches") == 4, res.stdout
+    assert res.stdout.count(" 0 mismatches") == 5, res.stdout
