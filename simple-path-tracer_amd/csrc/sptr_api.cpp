@@ -422,7 +422,10 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
   return launches;
 }
 
-constexpr uint64_t kFuseBouncePaths = 1ull << 26;
+#ifndef SPTR_FUSE_BOUNCE_LOG2
+#define SPTR_FUSE_BOUNCE_LOG2 26
+#endif
+constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 
 // Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
 uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
