@@ -930,10 +930,12 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
       if (valid) {
         Primary pr;
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
-        const Ray r = make_ray(f.cam_pos, pr.d);
         // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
         // 1 = constant environment, 4 = primary misses add no radiance
-        if (!(ablate(f) & 2u) && !culled) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!(ablate(f) & 2u) && !culled) {
+          const Ray r = make_ray(f.cam_pos, pr.d);
+          hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        }
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
           if (sh.debug_mode != 1) {
@@ -1013,8 +1015,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
       if (act) {
         Primary pr;
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
-        const Ray r = make_ray(f.cam_pos, pr.d);
-        if (!culled) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (!culled) {
+          const Ray r = make_ray(f.cam_pos, pr.d);
+          hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        }
         if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
       }
       // this pixel group's hits of the round -> number of leading misses still to fold
