@@ -38,7 +38,7 @@
 #define SPTR_SHADE_WAVES 5  // 111 -> 96 VGPRs, 4 -> 5 waves, no spills: C2 shade 0.971 -> 0.907 ms
 #endif                      // (6 waves spills 48-76 B/lane; profiles/r01f_variants.txt)
 #ifndef SPTR_BOUNCE_WAVES
-#define SPTR_BOUNCE_WAVES 5
+#define SPTR_BOUNCE_WAVES 6  // r02 ab23 (no packed FP32): 8-way shard 0.548 -> 0.525 ms, 2-way 1.662 -> 1.638; 7 spills
 #endif
 #ifndef SPTR_TAIL_WAVES
 #define SPTR_TAIL_WAVES 1
