@@ -31,7 +31,7 @@
 #define SPTR_TRACE_PM_WAVES SPTR_TRACE_WAVES
 #endif
 #ifndef SPTR_TRACE4_WAVES
-#define SPTR_TRACE4_WAVES 6  // BVH4, bounces >= 1: 7 waves (72 VGPRs) spills; measured C5 12.7 -> 7.1 ms
+#define SPTR_TRACE4_WAVES 7  // wide BVH, bounces >= 1 (refilling kernels, no packed FP32): C5 16.0 -> 15.2-15.6 ms/step (r02 ab24/25)
                              // (bounce 0 stays at 7: coherent rays gain more from occupancy, 8.4 -> 5.4)
 #endif
 #ifndef SPTR_SHADE_WAVES
