@@ -9,8 +9,9 @@
 //                   spheres into sorted slots; typed leaf links
 //   k_karras      : Karras 2012 binary radix tree over the sorted codes (ties broken by index)
 //   k_refit       : bottom-up box propagation; the second child to arrive at a node finishes it
-//                   (agent-scope release/acquire, write-through box stores — the hand-off recipe of
-//                   the gfx950 guide, Guideline 16)
+//                   (write-through 8-byte box pairs, drained before one agent-scope exchange that
+//                   also carries the subtree height — the fence-free hand-off of the gfx950 guide,
+//                   Guideline 16 R1)
 //   k_depth_wide + scan + k_collapse_wide : wide BVH (4 or 8 children) — every reachable BVH2 node
 //                   at a depth that is a multiple of kWideLevels becomes a wide node whose children
 //                   are its descendants kWideLevels levels down; leaves stay ranges
@@ -221,21 +222,29 @@ __global__ void k_karras(int N, const uint64_t* keys, uint32_t leaf_max, BvhNode
   }
 }
 
-__device__ __forceinline__ void st_agent(float* p, float v) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A child box travels to the parent as three 8-byte {lo, hi} pairs (x and y in the node's
+// interleaved xy words, z in its z words), each stored write-through (sc1) by one agent-scope
+// relaxed atomic store and read back by agent-scope loads: the hand-off form of the gfx950 guide
+// (Guideline 16, R1) with every payload store sc1 and drained and every payload load sc1, so neither
+// a release fence (an L2 write-back per level per thread) nor an acquire fence is needed.
+__device__ __forceinline__ void st_pair(float* p, float lo, float hi) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(lo) | ((unsigned long long)__float_as_uint(hi) << 32);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float ld_agent(const float* p) {
-  return __uint_as_float(
-      __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+__device__ __forceinline__ void ld_pair(const float* p, float& lo, float& hi) {
+  const unsigned long long v =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  lo = __uint_as_float((uint32_t)v);
+  hi = __uint_as_float((uint32_t)(v >> 32));
 }
 
 // Each leaf walks up; at each node the first arriving child stops, the second merges both child
-// boxes (read back through agent-scope loads) and continues.  Subtree heights travel up the same
-// way (the first arriver publishes its height in ht[node]), so the tree height — the deepest leaf,
-// which sizes the traversal stack — is the root's height, without a per-leaf walk to the root.
+// boxes and continues.  The arrival word doubles as the height hand-off: a child arriving swaps in
+// its subtree height + 1 (never 0), so the first arriver reads 0 and stops, and the second reads
+// its sibling's height.  The tree height — the deepest leaf, which sizes the traversal stack — is
+// the root's height, without a per-leaf walk to the root.
 __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const float4* bhi, const uint2* kids,
-                        const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* ht,
-                        uint32_t* max_depth) {
+                        const uint32_t* leaf_parent, BvhNode* nodes, uint32_t* flags, uint32_t* max_depth) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
     const uint32_t prim = vals[i];
     const float4 a = blo[prim], b = bhi[prim];
@@ -246,28 +255,29 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
     for (;;) {
       BvhNode* nd = nodes + par;
       const bool left = (kids[par].x == child);
+      // lxy = f[0..3], rxy = f[4..7], z = f[8..11]; own pairs at `m`, the sibling's at `o`
       float* f = reinterpret_cast<float*>(nd);
-      // lxy = f[0..3], rxy = f[4..7], z = f[8..11]
-      if (left) {
-        st_agent(f + 0, lo[0]); st_agent(f + 1, hi[0]); st_agent(f + 2, lo[1]); st_agent(f + 3, hi[1]);
-        st_agent(f + 8, lo[2]); st_agent(f + 9, hi[2]);
-      } else {
-        st_agent(f + 4, lo[0]); st_agent(f + 5, hi[0]); st_agent(f + 6, lo[1]); st_agent(f + 7, hi[1]);
-        st_agent(f + 10, lo[2]); st_agent(f + 11, hi[2]);
-      }
-      __hip_atomic_fetch_max(ht + par, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t old = __hip_atomic_fetch_add(flags + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float* m = f + (left ? 0 : 4);
+      float* o = f + (left ? 4 : 0);
+      float* mz = f + (left ? 8 : 10);
+      float* oz = f + (left ? 10 : 8);
+      st_pair(m, lo[0], hi[0]);
+      st_pair(m + 2, lo[1], hi[1]);
+      st_pair(mz, lo[2], hi[2]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // payload drained before the signal
+      const uint32_t old = __hip_atomic_exchange(flags + par, h + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == 0u) break;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      h = __hip_atomic_load(ht + par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-      const float l0 = ld_agent(f + 0), l1 = ld_agent(f + 1), l2 = ld_agent(f + 2), l3 = ld_agent(f + 3);
-      const float r0 = ld_agent(f + 4), r1 = ld_agent(f + 5), r2 = ld_agent(f + 6), r3 = ld_agent(f + 7);
-      const float z0 = ld_agent(f + 8), z1 = ld_agent(f + 9), z2 = ld_agent(f + 10), z3 = ld_agent(f + 11);
-      lo[0] = fminf(l0, r0); hi[0] = fmaxf(l1, r1);
-      lo[1] = fminf(l2, r2); hi[1] = fmaxf(l3, r3);
-      lo[2] = fminf(z0, z2); hi[2] = fmaxf(z1, z3);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below
+      h = max(h, old - 1u) + 1u;
+      float sl[3], sh[3];
+      ld_pair(o, sl[0], sh[0]);
+      ld_pair(o + 2, sl[1], sh[1]);
+      ld_pair(oz, sl[2], sh[2]);
+      for (int k = 0; k < 3; ++k) {
+        // fminf/fmaxf are symmetric, so the merged box does not depend on which child arrived last
+        lo[k] = fminf(lo[k], sl[k]);
+        hi[k] = fmaxf(hi[k], sh[k]);
+      }
       if (par == 0u) {
         *max_depth = h;  // only the second arriver at the root gets here
         break;
@@ -490,7 +500,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   uint32_t* cb = nullptr;
   uint64_t *keys = nullptr, *keys_s = nullptr;
   uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
-           *rflags = nullptr, *dmax = nullptr, *ht = nullptr;
+           *rflags = nullptr, *dmax = nullptr;
   uint2* kids = nullptr;
   LB_CHECK(tmp.alloc(&blo, N));
   LB_CHECK(tmp.alloc(&bhi, N));
@@ -504,7 +514,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(tmp.alloc(&kids, N));
   LB_CHECK(tmp.alloc(&leaf_parent, N));
   LB_CHECK(tmp.alloc(&rflags, N));
-  LB_CHECK(tmp.alloc(&ht, N));
   LB_CHECK(tmp.alloc(&dmax, 1));
   const uint32_t cb_init[8] = {~0u, ~0u, ~0u, 0u, 0u, 0u, 0u, 0u};
   LB_CHECK(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
@@ -545,11 +554,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
     LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
-    LB_CHECK(hipMemsetAsync(ht, 0, (size_t)N * 4, s));
     hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
                        leaf_parent);
     hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, kids, leaf_parent,
-                       nodes, rflags, ht, dmax);
+                       nodes, rflags, dmax);
     LB_CHECK(hipGetLastError());
     uint32_t dep = 0;
     LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
