@@ -289,10 +289,11 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
 }
 
 // Wide collapse, pass 1: keep[i] = 1 for BVH2 nodes that are reachable through internal links
-// (covering more than leaf_max primitives) and lie at a depth that is a multiple of kWideLevels.
-__global__ void k_depth_wide(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep) {
+// (covering more than leaf_max primitives) and lie at a depth that is a multiple of kWideLevels;
+// top[i] = 1 for the kept nodes of the top kTopLevels wide levels.
+__global__ void k_depth_wide(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep, uint32_t* top) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
-    uint32_t k = 0u;
+    uint32_t k = 0u, t = 0u;
     if (nodes[i].link.w > leaf_max) {
       uint32_t dep = 0u, q = (uint32_t)i;
       while (q != 0u) {
@@ -300,9 +301,20 @@ __global__ void k_depth_wide(int N, uint32_t leaf_max, const BvhNode* nodes, uin
         ++dep;
       }
       k = (dep % (uint32_t)kWideLevels) ? 0u : 1u;
+      t = k && dep / (uint32_t)kWideLevels < (uint32_t)kTopLevels ? 1u : 0u;
     }
     keep[i] = k;
+    top[i] = t;
   }
+}
+
+// Wide collapse, pass 1b: wide index of kept node i — the top-level nodes first (0..ntop-1, in
+// BVH2 index order, so the root stays 0), then the others in BVH2 index order.  slot / tslot: the
+// exclusive scans of keep / top; ntop comes from the last elements.
+__global__ void k_wide_index(int N, const uint32_t* keep, const uint32_t* top, uint32_t* slot, const uint32_t* tslot) {
+  const uint32_t ntop = tslot[N - 2] + top[N - 2];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x)
+    if (keep[i]) slot[i] = top[i] ? tslot[i] : ntop + (slot[i] - tslot[i]);
 }
 
 struct WideBoxes {
@@ -477,6 +489,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     c.root = kNoHit;
     c.root4 = kNoHit;
     c.num_nodes4 = 0;
+    c.num_top4 = 0;
     c.stack_need2 = c.stack_need4 = 0;
     return SPTR_OK;
   }
@@ -548,6 +561,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     c.root = kLeafBit | 0u;  // range [0, 1)
     c.root4 = c.root;
     c.num_nodes4 = 0;
+    c.num_top4 = 0;
     c.bvh_depth = 0;
     c.stack_need2 = c.stack_need4 = 0;
   } else {
@@ -575,21 +589,31 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     }
     if (c.root & kLeafBit) {
       c.num_nodes4 = 0;
+      c.num_top4 = 0;
       c.root4 = c.root;
     } else {
-      // BVH4: keep flags -> exclusive scan -> collapse (reusing flag/slot scratch arrays)
-      hipLaunchKernelGGL(k_depth_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag);
+      // BVH4: keep / top flags -> exclusive scans -> wide indices (top levels first) -> collapse
+      // (reusing the flag/slot scratch arrays; top flags and their scan in kids / leaf_parent)
+      uint32_t* topf = reinterpret_cast<uint32_t*>(kids);
+      uint32_t* tslot = leaf_parent;
+      hipLaunchKernelGGL(k_depth_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag, topf);
       LB_CHECK(hipGetLastError());
       size_t s4 = 0;
       LB_CHECK(rocprim::exclusive_scan(nullptr, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
       void* st4 = nullptr;
       LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&st4), s4));
       LB_CHECK(rocprim::exclusive_scan(st4, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
-      uint32_t last_keep = 0, last_slot = 0;
-      LB_CHECK(hipMemcpyAsync(&last_keep, flag + (N - 2), 4, hipMemcpyDeviceToHost, s));
-      LB_CHECK(hipMemcpyAsync(&last_slot, slot + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(rocprim::exclusive_scan(st4, s4, topf, tslot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
+      uint32_t last[4] = {0u, 0u, 0u, 0u};  // keep, slot, top, tslot of node N - 2
+      LB_CHECK(hipMemcpyAsync(&last[0], flag + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipMemcpyAsync(&last[1], slot + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipMemcpyAsync(&last[2], topf + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipMemcpyAsync(&last[3], tslot + (N - 2), 4, hipMemcpyDeviceToHost, s));
+      hipLaunchKernelGGL(k_wide_index, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, flag, topf, slot, tslot);
+      LB_CHECK(hipGetLastError());
       LB_CHECK(hipStreamSynchronize(s));
-      c.num_nodes4 = last_slot + last_keep;
+      c.num_nodes4 = last[1] + last[0];
+      c.num_top4 = last[3] + last[2];
       LB_CHECK(realloc_buf(c.nodes4, (size_t)c.num_nodes4 * sizeof(WideNode)));
       hipLaunchKernelGGL(k_collapse_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
                          static_cast<WideNode*>(c.nodes4.p));

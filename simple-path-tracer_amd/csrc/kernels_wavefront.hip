@@ -46,6 +46,9 @@
 #ifndef SPTR_SHADOW_WAVES
 #define SPTR_SHADOW_WAVES 6  // LDS-staged BVH2 scenes: 7 waves measured slower on C2 (0.409 -> 0.426 ms)
 #endif
+#ifndef SPTR_TOP_LDS
+#define SPTR_TOP_LDS 1  // wide-BVH top levels staged in LDS by the refilling kernels (0: A/B builds)
+#endif
 #ifndef SPTR_SHADOW4_WAVES
 #define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
@@ -497,24 +500,43 @@ struct WideWalk {
   bool hit;
 };
 // up to `steps` node visits; true when the traversal is over
+// top / ntop: an LDS copy of the wide nodes 0..ntop-1 (the top kTopLevels levels, stage_top), read
+// instead of L2/HBM for those indices (ntop = 0: every node from `nodes`).
 template <bool kAny, bool kCount, int N>
-__device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes,
-                                          const uint32_t* prim_ref, const float4* tris, const float4* sph, const Ray& r,
-                                          float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+__device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
+                                          uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                          const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
   for (int it = 0; it < steps; ++it) {
     const uint4* nq = reinterpret_cast<const uint4*>(nodes + wk.cur);
-    const uint4 h = nq[0];
+    uint4 h;
     uint32_t ln[kWide], qw[6 * kQWords];
-#pragma unroll
-    for (int j = 0; j < kWide / 4; ++j) {
-      const uint4 v = nq[1 + j];
-      ln[4 * j] = v.x; ln[4 * j + 1] = v.y; ln[4 * j + 2] = v.z; ln[4 * j + 3] = v.w;
-    }
     if (kWide == 4) {
-      const uint4 v = nq[2];
-      const uint2 u = *reinterpret_cast<const uint2*>(nq + 3);
-      qw[0] = v.x; qw[1] = v.y; qw[2] = v.z; qw[3] = v.w; qw[4] = u.x; qw[5] = u.y;
+      uint4 l4, q4;
+      uint2 q2;
+      if (wk.cur < ntop) {
+        const uint4* t = top + 4u * wk.cur;
+        h = t[0];
+        l4 = t[1];
+        q4 = t[2];
+        q2 = *reinterpret_cast<const uint2*>(t + 3);
+        // pins the LDS loads inside this branch: otherwise the compiler sinks both branches' loads
+        // past the join as flat loads of a selected address
+        asm volatile("" ::"v"(h.x), "v"(l4.x), "v"(q4.x), "v"(q2.x));
+      } else {
+        h = nq[0];
+        l4 = nq[1];
+        q4 = nq[2];
+        q2 = *reinterpret_cast<const uint2*>(nq + 3);
+      }
+      ln[0] = l4.x; ln[1] = l4.y; ln[2] = l4.z; ln[3] = l4.w;
+      qw[0] = q4.x; qw[1] = q4.y; qw[2] = q4.z; qw[3] = q4.w; qw[4] = q2.x; qw[5] = q2.y;
     } else {
+      h = nq[0];
+#pragma unroll
+      for (int j = 0; j < kWide / 4; ++j) {
+        const uint4 v = nq[1 + j];
+        ln[4 * j] = v.x; ln[4 * j + 1] = v.y; ln[4 * j + 2] = v.z; ln[4 * j + 3] = v.w;
+      }
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const uint4 v = nq[1 + kWide / 4 + j];
@@ -586,7 +608,7 @@ __device__ __forceinline__ bool traverse_wide(const WideNode* nodes, const uint3
   if (wide_start<kAny, kCount>(wk, root, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) return wk.hit;
   TravStack<N> stack;
   stack.lds = &ls.e[0][threadIdx.x];
-  (void)wide_walk<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc, 0x7FFFFFFF);
+  (void)wide_walk<kAny, kCount>(wk, stack, nodes, nullptr, 0u, prim_ref, tris, sph, r, tnear, tfar, ref, vc, 0x7FFFFFFF);
   return wk.hit;
 }
 
@@ -620,6 +642,22 @@ __device__ __forceinline__ Staged stage_scene(const SceneView& sv, float4* lds) 
     s.prim_ref = reinterpret_cast<const uint32_t*>(lds + nn + nt + ns);
   }
   return s;
+}
+
+// Copy the wide BVH's top levels (nodes 0..num_top4-1, SceneView::num_top4) to LDS at dst; the
+// caller's next block barrier (seg_scan's, or its own) publishes them.  Kernels traversing the wide
+// BVH from L2/HBM read these first node visits of every ray from LDS (wide_walk).
+__device__ __forceinline__ const uint4* stage_top(const SceneView& sv, float4* dst) {
+  const uint32_t n = sv.num_top4 * (uint32_t)(sizeof(WideNode) / 16);
+  const uint4* g = reinterpret_cast<const uint4*>(sv.nodes4);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) d[i] = g[i];
+  return d;
+}
+// float4 offset of the top-level copy in a kernel's dynamic LDS: after the staged scene (kLds) or
+// after the segment offsets s_off[0..nseg] of a consumer (!kPrimary)
+__device__ __forceinline__ uint32_t top_lds_offset(const SceneView& sv, bool lds, bool primary, uint32_t nseg) {
+  return (lds ? sv.lds_bytes / 16u : 0u) + (primary ? 0u : (4u * (nseg + 1u) + 15u) / 16u);
 }
 
 template <bool kW4, bool kAny, bool kCount, int N>
@@ -1142,9 +1180,12 @@ __device__ __forceinline__ bool walk_start(WideWalk& wk, const Staged& sc, uint3
   return wide_start<kAny, kCount>(wk, root, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc);
 }
 template <bool kAny, bool kCount, bool kW4, int N>
-__device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const Ray& r, float tnear,
-                                           float& tfar, uint32_t& ref, Visits& vc, int steps) {
-  if (kW4) return wide_walk<kAny, kCount>(wk, stack, sc.nodes4, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc, steps);
+__device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const uint4* top,
+                                           uint32_t ntop, const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
+                                           int steps) {
+  if (kW4)
+    return wide_walk<kAny, kCount>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
+                                   steps);
   return bvh2_walk<kAny, kCount>(wk.cur, wk.sp, wk.hit, stack, sc.nodes, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref,
                                  vc, steps);
 }
@@ -1185,6 +1226,8 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = s_next = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
+  const uint32_t ntop = (kW4 && !kLds) ? sv.num_top4 : 0u;
+  const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, kLds, kPrimary, nseg_in)) : nullptr;
   uint32_t n, per_in = 0u, nlist = 0u;
   if (kPrimary) {
     nlist = f.plist ? f.plist[f.P] : 0u;
@@ -1244,7 +1287,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
       continue;                                       // only invalid (outside-image) items taken
     }
-    if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, r, 0.0f, tfar, ref, vc, kDynSteps);
+    if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc, kDynSteps);
     const bool fin = have && done;
     if (fin && !wk.hit) {
       if (sh.debug_mode == 1) {
@@ -1727,6 +1770,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   __shared__ uint32_t s_rays, s_next;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
   if (threadIdx.x == 0) s_rays = s_next = 0u;
+  const uint32_t ntop = sv.num_top4;
+  const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, false, false, nseg_in)) : nullptr;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
   const uint32_t ts = w.tstride;
@@ -1767,8 +1812,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
       continue;
     }
     if (have && !done)
-      done = wide_walk<true, kCount>(wk, stack, sv.nodes4, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref, vc,
-                                     kDynSteps);
+      done = wide_walk<true, kCount>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref,
+                                     vc, kDynSteps);
     if (have && done) {
       if (!wk.hit) w.rad[p] = f4(xyz(w.rad[p]) + contrib, 0.0f);
       have = false;
@@ -2599,6 +2644,8 @@ SceneView scene_view(const Context& c) {
                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
   s.scene_bytes = bytes;
+  // the refilling wide-BVH kernels of L2/HBM scenes stage the top levels (4-wide nodes only)
+  s.num_top4 = (SPTR_TOP_LDS && s.width == (uint32_t)kWide && kWide == 4 && s.lds_bytes == 0u) ? c.num_top4 : 0u;
   return s;
 }
 
@@ -2708,14 +2755,15 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         Flags<>{}, count, W, cube);
   }
   if (((!L && W) || (L && !W && !P && dyn_lds())) && !no_dyn()) {  // refilling lanes
+    const unsigned lbd = lb + (!L && W ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
     return dispatch(
         [&](auto fl) -> unsigned {
           return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube>(Flags<Lc, C, Pc, Wc, Cube>) {
             if constexpr (Lc == Wc) {
               return 0u;  // not instantiated: LDS scenes traverse BVH2, L2/HBM scenes the wide BVH
             } else {
-              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube>, lb);
-              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
+              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube>, lbd);
+              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
               return g;
             }
           }(fl);
@@ -2783,12 +2831,13 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
   if (!L && W && w.L == 1u && !no_dyn()) {  // wide BVH from L2/HBM, one light: refilling lanes
+    const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
     if (count) {
-      g = resident_grid((const void*)&k_shadow_dyn<true>, lb);
-      hipLaunchKernelGGL(k_shadow_dyn<true>, dim3(g), b, lb, s, sv, sh, w, depth, nseg);
+      g = resident_grid((const void*)&k_shadow_dyn<true>, lbd);
+      hipLaunchKernelGGL(k_shadow_dyn<true>, dim3(g), b, lbd, s, sv, sh, w, depth, nseg);
     } else {
-      g = resident_grid((const void*)&k_shadow_dyn<false>, lb);
-      hipLaunchKernelGGL(k_shadow_dyn<false>, dim3(g), b, lb, s, sv, sh, w, depth, nseg);
+      g = resident_grid((const void*)&k_shadow_dyn<false>, lbd);
+      hipLaunchKernelGGL(k_shadow_dyn<false>, dim3(g), b, lbd, s, sv, sh, w, depth, nseg);
     }
     return g;
   }

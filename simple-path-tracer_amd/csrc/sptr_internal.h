@@ -44,7 +44,10 @@ constexpr int kMaxLights = 8;
 constexpr int kWide = SPTR_WIDE;
 static_assert(kWide == 4 || kWide == 8, "wide BVH: 4 or 8 children");
 constexpr int kWideLevels = kWide == 8 ? 3 : 2;  // BVH2 levels per wide level
-constexpr int kQWords = kWide / 4;               // u32 words per quantised plane, one byte per child
+constexpr int kQWords = kWide / 4;
+// The wide BVH's top kTopLevels levels (at most 1 + 4 + 16 = 21 nodes, 1.3 KB) take wide indices
+// 0..num_top4-1, so a kernel can stage them in LDS and tell an LDS node by its index alone.
+constexpr int kTopLevels = 3;               // u32 words per quantised plane, one byte per child
 constexpr int kMaxDepth = 32;
 // Traversal stack entries.  BVH2 pushes at most one entry per internal level, a wide BVH at most
 // kWide - 1, so a tree of height h needs h (BVH2) or (kWide - 1) * ((h - 1) / kWideLevels + 1)
@@ -112,6 +115,8 @@ struct SceneView {
   const uint32_t* sph_geom;  // geomID per sorted sphere
   uint32_t num_nodes, num_tris, num_sph, root;
   uint32_t num_nodes4, root4;
+  uint32_t num_top4;   // wide nodes 0..num_top4-1 are the top kTopLevels levels (staged in LDS by the
+                       // refilling kernels of scenes traversed from L2/HBM); 0 = none
   uint32_t width;      // 2: BVH2 traversal, 4: BVH4 traversal
   uint32_t lds_bytes;  // 0: traverse from global memory
   uint64_t scene_bytes;  // traversed nodes + triangles + spheres + refs
@@ -261,6 +266,7 @@ struct Context {
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_nodes4 = 0, root4 = 0;
+  uint32_t num_top4 = 0;  // wide nodes numbered first: the top kTopLevels levels
   uint32_t stack_need2 = 0, stack_need4 = 0;  // traversal stack entries the BVH2 / BVH4 can need
   DevBuf nodes4;
   uint32_t num_tri_geoms = 0;
