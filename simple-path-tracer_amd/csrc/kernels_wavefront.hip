@@ -46,6 +46,9 @@
 #ifndef SPTR_SHADOW_WAVES
 #define SPTR_SHADOW_WAVES 6  // LDS-staged BVH2 scenes: 7 waves measured slower on C2 (0.409 -> 0.426 ms)
 #endif
+#ifndef SPTR_SORT_OCTANT
+#define SPTR_SORT_OCTANT 0  // k_shade groups its continuation rays by direction octant (A/B builds)
+#endif
 #ifndef SPTR_TOP_LDS
 #define SPTR_TOP_LDS 1  // wide-BVH top levels staged in LDS by the refilling kernels (0: A/B builds)
 #endif
@@ -69,6 +72,43 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* s_cnt, bool pred) {
   if ((int)lane == leader) base = atomicAdd(s_cnt, (uint32_t)__popcll(m));
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+// Block-local append grouped by a 3-bit key (a continuation ray's direction octant): the chunk's
+// outputs land in the block's segment ordered by key, so that the consumer's waves trace rays of
+// one octant together (same near-child order, fewer divergent node visits).  Every thread of the
+// block must call it together (block barriers).  s_hist: 16 words of LDS.
+__device__ __forceinline__ uint32_t block_append_key(uint32_t* s_cnt, uint32_t* s_hist, bool pred, uint32_t key) {
+  if (threadIdx.x < 8u) s_hist[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t rank = 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < 8u; ++k) {
+    const bool mine = pred && key == k;
+    const unsigned long long m = __ballot(mine);
+    if (m) {
+      const int leader = __ffsll(m) - 1;
+      uint32_t b = 0u;
+      if ((int)lane == leader) b = atomicAdd(&s_hist[k], (uint32_t)__popcll(m));
+      b = __shfl(b, leader);
+      if (mine) rank = b + (uint32_t)__popcll(m & below);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    uint32_t run = *s_cnt;
+    for (uint32_t k = 0; k < 8u; ++k) {
+      s_hist[8u + k] = run;
+      run += s_hist[k];
+    }
+    *s_cnt = run;
+  }
+  __syncthreads();
+  return s_hist[8u + key] + rank;
+}
+__device__ __forceinline__ uint32_t octant(float x, float y, float z) {
+  return (x < 0.0f ? 1u : 0u) | (y < 0.0f ? 2u : 0u) | (z < 0.0f ? 4u : 0u);
 }
 // Block-local work counter: every lane with pred takes the next index (one LDS atomic per wave).
 __device__ __forceinline__ uint32_t block_take(uint32_t* s_next, bool pred) { return block_append(s_next, pred); }
@@ -1482,6 +1522,9 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   __shared__ DevMaterial smat[32];
   __shared__ uint32_t s_cnt_n, s_cnt_s, s_rays;
   __shared__ LdsStackN<kFuse ? kFuseStack : 1> s_stack;
+#if SPTR_SORT_OCTANT
+  __shared__ uint32_t s_hist[16];
+#endif
   const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x == 0) s_cnt_n = s_cnt_s = s_rays = 0u;
   const Staged sc = stage_scene<kFuse>(sv, lds);
@@ -1570,7 +1613,11 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     }
     if (active && sh.debug_mode != 1) cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
     if (!kFuse && active && dirty) w.rad[p] = f4(radv, 0.0f);
+#if SPTR_SORT_OCTANT
+    const uint32_t jn = block_append_key(&s_cnt_n, s_hist, cont, cont ? octant(nd.x, nd.y, nd.z) : 0u);
+#else
     const uint32_t jn = block_append(&s_cnt_n, cont);
+#endif
     if (cont && sd.seg0 + jn >= w.seg_cap) {
       cont = false;
       w.tot[kTotOverflow] = 1ull;
