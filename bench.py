@@ -66,11 +66,18 @@ class _DevArray:
 
 
 def _latest_profile(pattern):
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
-    if not found:
+    """The newest committed counter summary: by its "collected" UTC time (tools/prof_summary.py
+    --emit); files from before that field count as older, and among themselves go by name."""
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", pattern)):
+        with open(path) as f:
+            data = json.load(f)
+        key = (data.get("collected", ""), os.path.basename(path))
+        if best is None or key > best[0]:
+            best = (key, data, path)
+    if best is None:
         return None, None
-    with open(found[-1]) as f:
-        return json.load(f), os.path.relpath(found[-1], ROOT)
+    return best[1], os.path.relpath(best[2], ROOT)
 
 
 def roofline(cnt, stats, layout, wl_name, steps, samples):

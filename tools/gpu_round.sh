@@ -20,13 +20,10 @@ if [ $tests = 1 ]; then
     > "$out/pytest_gpu.log" 2>&1 || { tail -40 "$out/pytest_gpu.log"; exit 1; }
   tail -2 "$out/pytest_gpu.log"
 fi
+# Per workload the counter passes run first and their summaries are emitted into profiles/ (on the
+# box), so that the bench line that follows cites this session's counters (bench.py picks the
+# newest summary by its collection time); tools/save_profiles.sh copies them into the tracked tree.
 for wl in "$@"; do
-  echo "[$(date +%T)] bench $wl"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
-  tail -1 "$out/bench_$wl.json"
-  echo "[$(date +%T)] bench $wl --stage-timing"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 --stage-timing --no-cpu-baseline --no-interactive \
-    > "$out/bench_${wl}_stages.json" 2> "$out/bench_${wl}_stages.err"
   echo "[$(date +%T)] rocprof kernel trace + stats $wl"
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_$wl" -o run -- \
     python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive > "$out/stats_$wl.log" 2>&1
@@ -38,6 +35,7 @@ for wl in "$@"; do
   python3 tools/prof_summary.py "$out/stats_$wl" "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" > "$out/summary_$wl.txt"
   python3 tools/prof_summary.py "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" --emit "$out/pmc_${wl}_trace.json" \
     --kernel k_trace --workload "$wl" > /dev/null
+  cp "$out/pmc_${wl}_trace.json" "profiles/${tag}_pmc_${wl}_trace.json"
   if [ $sq = 1 ]; then
     echo "[$(date +%T)] pmc SQ $wl"
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
@@ -45,6 +43,13 @@ for wl in "$@"; do
       python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_SQ_$wl.log" 2>&1
     python3 tools/prof_summary.py "$out/pmc_SQ_$wl" > "$out/sq_$wl.txt"
     python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_trace.json" --kernel k_trace --workload "$wl" > /dev/null
+    cp "$out/sq_${wl}_trace.json" "profiles/${tag}_sq_${wl}_trace.json"
   fi
+  echo "[$(date +%T)] bench $wl"
+  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
+  tail -1 "$out/bench_$wl.json"
+  echo "[$(date +%T)] bench $wl --stage-timing"
+  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 --stage-timing --no-cpu-baseline --no-interactive \
+    > "$out/bench_${wl}_stages.json" 2> "$out/bench_${wl}_stages.err"
 done
 echo "[$(date +%T)] done"

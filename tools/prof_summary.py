@@ -10,10 +10,16 @@ MI355X_MICROARCH.md §HBM); WRITE_SIZE as read.
 """
 import collections
 import csv
+import datetime
 import glob
 import json
 import os
 import sys
+
+
+def _now():
+    """UTC collection time; bench.py cites the newest emitted file by this field."""
+    return datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
 def short(n):
@@ -47,7 +53,7 @@ def emit(dirs, kernel, out_path, workload):
     if "SQ_INSTS_VALU" in mean:  # SQ pass: VALU wave-instructions per launch (bench.py valu_issue_frac)
         d = dict(dur)
         t = sum(d.values()) / max(1, len(d))
-        res = {"workload": workload, "kernel": kernel, "dispatches": len(per["SQ_INSTS_VALU"]),
+        res = {"workload": workload, "collected": _now(), "kernel": kernel, "dispatches": len(per["SQ_INSTS_VALU"]),
                "valu_per_launch": mean["SQ_INSTS_VALU"], "counters_per_launch": mean,
                "profiled_launch_us": t * 1e6,
                "valu_issue_frac_profiled": mean["SQ_INSTS_VALU"] / t / (256 * 4 * 0.5 * 2.4e9) if t else None,
@@ -60,7 +66,7 @@ def emit(dirs, kernel, out_path, workload):
         return
     fetch = 2.0 * mean.get("FETCH_SIZE", 0.0) * 1024.0
     write = mean.get("WRITE_SIZE", 0.0) * 1024.0
-    res = {"workload": workload, "kernel": kernel, "dispatches": {c: len(v) for c, v in per.items()},
+    res = {"workload": workload, "collected": _now(), "kernel": kernel, "dispatches": {c: len(v) for c, v in per.items()},
            "fetch_bytes_per_launch_x2": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (calibrated for 16-B/lane streams only); "
