@@ -46,6 +46,9 @@
 #ifndef SPTR_SHADOW_WAVES
 #define SPTR_SHADOW_WAVES 6  // LDS-staged BVH2 scenes: 7 waves measured slower on C2 (0.409 -> 0.426 ms)
 #endif
+#ifndef SPTR_SKY_ILP
+#define SPTR_SKY_ILP 4  // independent samples per step of k_sky's per-pixel loop
+#endif
 #ifndef SPTR_SORT_OCTANT
 #define SPTR_SORT_OCTANT 0  // k_shade groups its continuation rays by direction octant (A/B builds)
 #endif
@@ -1987,15 +1990,16 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
         if (sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
         return rv;
       };
-      // four independent samples (their environment fetches in flight together), then their adds in
-      // sample order
+      // kSkyIlp independent samples (their environment fetches in flight together), then their adds
+      // in sample order
+      constexpr uint32_t kSkyIlp = SPTR_SKY_ILP;
       uint32_t smp = 0;
-      for (; smp + 4u <= f.k; smp += 4u) {
-        vec3 rv[4];
+      for (; smp + kSkyIlp <= f.k; smp += kSkyIlp) {
+        vec3 rv[kSkyIlp];
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) rv[j] = sample(smp + j);
+        for (uint32_t j = 0; j < kSkyIlp; ++j) rv[j] = sample(smp + j);
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) a = a + rv[j];
+        for (uint32_t j = 0; j < kSkyIlp; ++j) a = a + rv[j];
       }
       for (; smp < f.k; ++smp) a = a + sample(smp);
       resume = f.k;
