@@ -51,7 +51,7 @@ VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 0.5 * 2.4e9
 STREAM_READ_BYTES, STREAM_WRITE_BYTES = 28.0, 8.0
 L2_BYTES_PER_XCD = 4 << 20  # MI355X: 4 MB L2 per XCD (MI355X_MICROARCH.md)
 XCDS = 8
-CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 8, "c4": 4, "c5": 1}
+CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 128, "c4": 64, "c5": 64}  # ~1-4 s per run on 16 host threads
 # experiment knobs of the library and the build (timing studies only); a bench line records any that
 # is set, so a stray variable cannot silently change a measured number
 KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU")
