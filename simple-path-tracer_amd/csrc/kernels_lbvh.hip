@@ -12,9 +12,13 @@
 //                   (write-through 8-byte box pairs, drained before one agent-scope exchange that
 //                   also carries the subtree height — the fence-free hand-off of the gfx950 guide,
 //                   Guideline 16 R1)
-//   k_depth_wide + scan + k_collapse_wide : wide BVH (4 or 8 children) — every reachable BVH2 node
-//                   at a depth that is a multiple of kWideLevels becomes a wide node whose children
-//                   are its descendants kWideLevels levels down; leaves stay ranges
+//   k_wide_count + scan + k_wide_emit, one wide level at a time (SPTR_WIDE_GREEDY, the default):
+//                   wide BVH (4 or 8 children) by the greedy surface-area collapse — a wide node
+//                   opens its largest-area internal child until it has kWide children; leaves stay
+//                   ranges; wide nodes are numbered level by level (top levels first)
+//   k_depth_wide + scans + k_wide_index + k_collapse_wide (SPTR_WIDE_GREEDY=0): fixed collapse —
+//                   every reachable BVH2 node at a depth that is a multiple of kWideLevels becomes a
+//                   wide node whose children are its descendants kWideLevels levels down
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,6 +27,10 @@
 #include <rocprim/rocprim.hpp>
 
 #include "sptr_internal.h"
+
+#ifndef SPTR_WIDE_GREEDY
+#define SPTR_WIDE_GREEDY 1  // 0: every kWideLevels-th LBVH level becomes a wide level (A/B builds)
+#endif
 
 namespace sptr {
 
@@ -434,6 +442,91 @@ __global__ void k_collapse_wide(int N, const BvhNode* nodes, const uint32_t* kee
   }
 }
 
+// Greedy surface-area collapse (SPTR_WIDE_GREEDY), top-down one wide level per launch pair: a wide
+// node's child list starts as its BVH2 node's two children and grows, up to kWide entries, by
+// opening the internal entry whose box has the largest surface area (lowest slot on ties) — it is
+// replaced in place by its left and right children, so the list stays in left-to-right order.
+// Unlike the fixed two-level collapse this fills nodes whose grandchildren include leaves and
+// spends the wide levels where the big boxes are, so deep LBVH chains give shallower wide trees.
+// Its internal entries become the next level's wide nodes.
+__device__ __forceinline__ float box_area(const WideBoxes& b, int e) {
+  const float dx = b.hi[0][e] - b.lo[0][e], dy = b.hi[1][e] - b.lo[1][e], dz = b.hi[2][e] - b.lo[2][e];
+  return dx * dy + dy * dz + dz * dx;
+}
+__device__ __forceinline__ void put_child(WideBoxes& b, int e, const BvhNode& nd, bool right) {
+  if (!right) {
+    b.link[e] = nd.link.x;
+    b.lo[0][e] = nd.lxy.x; b.hi[0][e] = nd.lxy.y; b.lo[1][e] = nd.lxy.z; b.hi[1][e] = nd.lxy.w;
+    b.lo[2][e] = nd.z.x;   b.hi[2][e] = nd.z.y;
+  } else {
+    b.link[e] = nd.link.y;
+    b.lo[0][e] = nd.rxy.x; b.hi[0][e] = nd.rxy.y; b.lo[1][e] = nd.rxy.z; b.hi[1][e] = nd.rxy.w;
+    b.lo[2][e] = nd.z.z;   b.hi[2][e] = nd.z.w;
+  }
+}
+__device__ int expand_greedy(const BvhNode* nodes, uint32_t node, WideBoxes& b) {
+  for (int k = 0; k < kWide; ++k) {
+    b.link[k] = kNoHit;
+    for (int a = 0; a < 3; ++a) b.lo[a][k] = b.hi[a][k] = 0.0f;
+  }
+  const BvhNode nd = nodes[node];
+  put_child(b, 0, nd, false);
+  put_child(b, 1, nd, true);
+  int n = 2;
+  while (n < kWide) {
+    int best = -1;
+    float ba = -1.0f;
+    for (int e = 0; e < n; ++e)
+      if (!(b.link[e] & kLeafBit)) {
+        const float a = box_area(b, e);
+        if (a > ba) {
+          ba = a;
+          best = e;
+        }
+      }
+    if (best < 0) break;
+    const BvhNode cn = nodes[b.link[best]];
+    for (int e = n; e > best + 1; --e) {
+      b.link[e] = b.link[e - 1];
+      for (int a = 0; a < 3; ++a) {
+        b.lo[a][e] = b.lo[a][e - 1];
+        b.hi[a][e] = b.hi[a][e - 1];
+      }
+    }
+    put_child(b, best, cn, false);
+    put_child(b, best + 1, cn, true);
+    ++n;
+  }
+  return n;
+}
+// pass 1: internal children per wide node of this level (cur[j] = {BVH2 node, parent wide index})
+__global__ void k_wide_count(uint32_t ncur, const uint2* cur, const BvhNode* nodes, uint32_t* cnt) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ncur; j += gridDim.x * blockDim.x) {
+    WideBoxes b;
+    const int n = expand_greedy(nodes, cur[j].x, b);
+    uint32_t m = 0u;
+    for (int e = 0; e < n; ++e) m += (b.link[e] & kLeafBit) ? 0u : 1u;
+    cnt[j] = m;
+  }
+}
+// pass 2: wide node base + j; its m-th internal child becomes next[off[j] + m] = wide node
+// base + ncur + off[j] + m of the next level
+__global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, const BvhNode* nodes, const uint32_t* off,
+                            uint2* next, WideNode* out) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ncur; j += gridDim.x * blockDim.x) {
+    WideBoxes b;
+    const int n = expand_greedy(nodes, cur[j].x, b);
+    uint32_t m = off[j];
+    for (int e = 0; e < n; ++e)
+      if (!(b.link[e] & kLeafBit)) {
+        next[m] = make_uint2(b.link[e], base + j);
+        b.link[e] = base + ncur + m;
+        ++m;
+      }
+    out[base + j] = quantize_wide(b, n, cur[j].y);
+  }
+}
+
 struct Tmp {
   std::vector<void*> ptrs;
   ~Tmp() {
@@ -592,7 +685,46 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       c.num_top4 = 0;
       c.root4 = c.root;
     } else {
-      // BVH4: keep / top flags -> exclusive scans -> wide indices (top levels first) -> collapse
+#if SPTR_WIDE_GREEDY
+      // wide BVH, greedy surface-area collapse, top-down: level L's wide nodes are numbered after
+      // levels 0..L-1 (so the top kTopLevels levels come first); cnt -> exclusive scan -> emit
+      uint2 *cur = nullptr, *nxt = nullptr;
+      uint32_t* off = nullptr;
+      LB_CHECK(tmp.alloc(&cur, N));
+      LB_CHECK(tmp.alloc(&nxt, N));
+      LB_CHECK(tmp.alloc(&off, N));
+      size_t sw = 0;
+      LB_CHECK(rocprim::exclusive_scan(nullptr, sw, flag, off, 0u, N, rocprim::plus<uint32_t>(), s));
+      void* stw = nullptr;
+      LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&stw), sw));
+      LB_CHECK(realloc_buf(c.nodes4, (size_t)(N - 1) * sizeof(WideNode)));  // <= one wide node per BVH2 node
+      const uint2 root2 = make_uint2(0u, kNoHit);
+      LB_CHECK(hipMemcpyAsync(cur, &root2, sizeof(root2), hipMemcpyHostToDevice, s));
+      uint32_t ncur = 1u, base = 0u, levels = 0u;
+      c.num_top4 = 0u;
+      while (ncur > 0u) {
+        hipLaunchKernelGGL(k_wide_count, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, nodes, flag);
+        LB_CHECK(hipGetLastError());
+        LB_CHECK(rocprim::exclusive_scan(stw, sw, flag, off, 0u, ncur, rocprim::plus<uint32_t>(), s));
+        hipLaunchKernelGGL(k_wide_emit, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, base, nodes, off, nxt,
+                           static_cast<WideNode*>(c.nodes4.p));
+        LB_CHECK(hipGetLastError());
+        uint32_t last[2] = {0u, 0u};  // cnt, off of the level's last node
+        LB_CHECK(hipMemcpyAsync(&last[0], flag + (ncur - 1u), 4, hipMemcpyDeviceToHost, s));
+        LB_CHECK(hipMemcpyAsync(&last[1], off + (ncur - 1u), 4, hipMemcpyDeviceToHost, s));
+        LB_CHECK(hipStreamSynchronize(s));
+        base += ncur;
+        ++levels;
+        if (levels == (uint32_t)kTopLevels) c.num_top4 = base;
+        ncur = last[0] + last[1];
+        std::swap(cur, nxt);
+      }
+      if (levels < (uint32_t)kTopLevels) c.num_top4 = base;
+      c.num_nodes4 = base;
+      // a wide node at wide depth d holds at most (kWide-1)*d stack entries and pushes up to kWide-1
+      c.stack_need4 = (uint32_t)(kWide - 1) * levels;
+#else
+      // fixed collapse: keep / top flags -> exclusive scans -> wide indices (top levels first) -> collapse
       // (reusing the flag/slot scratch arrays; top flags and their scan in kids / leaf_parent)
       uint32_t* topf = reinterpret_cast<uint32_t*>(kids);
       uint32_t* tslot = leaf_parent;
@@ -618,6 +750,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       hipLaunchKernelGGL(k_collapse_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
                          static_cast<WideNode*>(c.nodes4.p));
       LB_CHECK(hipGetLastError());
+#endif
       c.root4 = 0u;  // node 0 (depth 0) is kept and scans to index 0
     }
   }

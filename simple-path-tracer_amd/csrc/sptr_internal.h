@@ -44,10 +44,10 @@ constexpr int kMaxLights = 8;
 constexpr int kWide = SPTR_WIDE;
 static_assert(kWide == 4 || kWide == 8, "wide BVH: 4 or 8 children");
 constexpr int kWideLevels = kWide == 8 ? 3 : 2;  // BVH2 levels per wide level
-constexpr int kQWords = kWide / 4;
+constexpr int kQWords = kWide / 4;         // u32 words per quantised plane, one byte per child
 // The wide BVH's top kTopLevels levels (at most 1 + 4 + 16 = 21 nodes, 1.3 KB) take wide indices
 // 0..num_top4-1, so a kernel can stage them in LDS and tell an LDS node by its index alone.
-constexpr int kTopLevels = 3;               // u32 words per quantised plane, one byte per child
+constexpr int kTopLevels = 3;
 constexpr int kMaxDepth = 32;
 // Traversal stack entries.  BVH2 pushes at most one entry per internal level, a wide BVH at most
 // kWide - 1, so a tree of height h needs h (BVH2) or (kWide - 1) * ((h - 1) / kWideLevels + 1)
@@ -66,11 +66,6 @@ struct BvhNode {
   uint4 link;  // left, right, parent, pad
 };
 static_assert(sizeof(BvhNode) == 64, "node size");
-
-// BVH4 node, 128 B (one cache line): four child boxes stored SoA so the four slab tests vectorise,
-// four child links (BVH4 node index, leaf range, or kNoHit for an empty slot).  Built by collapsing
-// the LBVH: the BVH2 nodes at even depth become BVH4 nodes whose children are their grandchildren.
-
 
 // Wide BVH node (64 B for 4 children = half a 128-B cache line; 128 B for 8): the child boxes
 // quantised to 8 bits per plane on a per-node, per-axis power-of-two grid anchored at the node's
