@@ -185,7 +185,7 @@ int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
  * >= max_depth = none.  The image and the query counts do not depend on it. */
 int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
- * LDS, 2 otherwise); applies to the next sptr_upload_scene. */
+ * LDS, 1 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call

@@ -644,10 +644,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
                      static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p),
                      static_cast<uint32_t*>(c.prim_ref.p));
   LB_CHECK(hipGetLastError());
-  // automatic leaf size (measured, profiles/r01*): ranges of 8 for scenes small enough to be staged
-  // in LDS (fewer, divergence-free node steps), 2 for meshes traversed from L2/HBM
+  // automatic leaf size (measured, profiles/r01*, r02g_leaf.txt): ranges of 8 for scenes small enough
+  // to be staged in LDS (fewer, divergence-free node steps), single primitives for meshes traversed
+  // from L2/HBM (with the greedy wide collapse: C5 14.9 -> 13.9, C3 5.04 -> 4.87 ms/step vs 2)
   const uint32_t auto_leaf = ((uint64_t)(N > 1 ? N - 1 : 0) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 +
-                              ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : 2u;
+                              ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : (SPTR_WIDE_GREEDY ? 1u : 2u);
   const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size ? c.leaf_size : auto_leaf, kMaxLeafSize));
   c.leaf_used = leaf_max;
   if (N == 1) {
