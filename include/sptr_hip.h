@@ -161,7 +161,9 @@ typedef struct sptr_stats {
   uint64_t waves;        /* wavefront batches launched */
   double ms_total;       /* wall time of the call on the device stream */
   double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_accum; /* SPTR_FRAME_TIMING only; raygen is fused
-                                                                into the bounce-0 trace (ms_raygen = 0) */
+                                                                into the bounce-0 trace (ms_raygen = 0);
+                                                                ms_accum includes the culled pixels'
+                                                                environment sums (k_sky) */
   uint64_t trace_launches;
   uint64_t node_visits, tri_tests, sphere_tests; /* SPTR_FRAME_COUNT_VISITS only */
   uint64_t shadow_node_visits, shadow_prim_tests;

@@ -491,8 +491,12 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         std::swap(rays_tab, spare_tab);
         continue;
       }
+      if (d == 0 && fv.sky_fold) {  // the culled pixels' environment sums: accumulation, not k_trace
+        tm.begin(4);
+        launch_sky(sh, fv, s);
+        tm.end();
+      }
       tm.begin(d == 0 ? 5 : 1);
-      if (d == 0 && fv.sky_fold) launch_sky(sh, fv, s);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
       tm.begin(d == 0 ? 6 : 2);
