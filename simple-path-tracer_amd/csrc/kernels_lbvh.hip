@@ -28,6 +28,9 @@
 
 #include "sptr_internal.h"
 
+#ifndef SPTR_GREEDY_WEIGHT
+#define SPTR_GREEDY_WEIGHT 0  // 1: the greedy collapse opens the child of largest area x primitives
+#endif
 #ifndef SPTR_WIDE_GREEDY
 #define SPTR_WIDE_GREEDY 1  // 0: every kWideLevels-th LBVH level becomes a wide level (A/B builds)
 #endif
@@ -478,7 +481,10 @@ __device__ int expand_greedy(const BvhNode* nodes, uint32_t node, WideBoxes& b) 
     float ba = -1.0f;
     for (int e = 0; e < n; ++e)
       if (!(b.link[e] & kLeafBit)) {
-        const float a = box_area(b, e);
+        float a = box_area(b, e);
+#if SPTR_GREEDY_WEIGHT
+        a *= (float)nodes[b.link[e]].link.w;  // area x primitives: the child's SAH cost term
+#endif
         if (a > ba) {
           ba = a;
           best = e;
