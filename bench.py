@@ -8,7 +8,7 @@ selects the other configurations (simple-path-tracer_amd/workloads.py); c5 is th
 
 One "step" = one complete render of the frame at the workload's spp: every rank renders its
 interleaved 32x32 tiles (the reference's tile schedule, src/GLRenderer.cpp:335-350) and resolves
-them; the resolved RGBA8 tiles are all-gathered over RCCL and rank 0 unpacks them into the W x H
+them; the resolved RGBA8 tiles are gathered to rank 0 over RCCL and rank 0 unpacks them into the W x H
 RGB8 image.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2]
@@ -17,7 +17,7 @@ RGB8 image.
 `--gpus N` without a torch.distributed environment launches the N ranks itself: a child
 `torch.distributed.run` of a fresh interpreter, started before this process touches the GPU (this
 process only waits for it and exits with its code).  `--dry-run` runs the same rank launch, tile
-schedule, all-gather and unpack on the CPU over gloo with a synthetic per-pixel pattern instead of
+schedule, gather and unpack on the CPU over gloo with a synthetic per-pixel pattern instead of
 the renderer (a check of the multi-rank plumbing that needs no GPU).
 
 value = all ranks' rays (closest-hit + any-hit queries, = the reference's rtcIntersect1 +
@@ -229,10 +229,18 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
 
 
+def gather_tiles(send, gathered, world, rank):
+    """Rank 0 collects every rank's resolved tiles (dist.gather: one point-to-point transfer per
+    rank to rank 0).  On the fully connected xGMI mesh of an 8-GPU node the 7 transfers use 7
+    different links at once; a ring all-gather would move the frame over one link per step, N-1
+    steps in a row, and hand every rank a whole frame that only rank 0 uses."""
+    dist.gather(send, list(gathered.chunk(world)) if rank == 0 else None, dst=0)
+
+
 def dry_run(args, wl, world, rank):
     """CPU plumbing check of the multi-rank step (gloo): each rank packs its interleaved tiles of a
     synthetic per-pixel pattern with the product's host tile packing (the twin of the device
-    resolve's tile layout), one all-gather, rank 0 unpacks and compares with the whole pattern."""
+    resolve's tile layout), one gather to rank 0, which unpacks and compares with the whole pattern."""
     import numpy as np
 
     W, H = wl.width, wl.height
@@ -240,7 +248,7 @@ def dry_run(args, wl, world, rank):
     pattern = np.stack([(xx * 7 + yy) & 255, (xx ^ yy) & 255, (xx * 13 + yy * 5) & 255], -1).astype(np.uint8)
     tiles = sptr.pack_tiles(pattern, world, rank)
     gathered = torch.zeros(world * tiles.size, dtype=torch.int32)
-    dist.all_gather_into_tensor(gathered, torch.from_numpy(tiles.view(np.int32)))
+    gather_tiles(torch.from_numpy(tiles.view(np.int32)), gathered, world, rank)
     mine = torch.tensor([float(((tiles >> 24) == 255).sum())], dtype=torch.float64)  # pixels inside the image
     dist.all_reduce(mine)
     if rank == 0:
@@ -340,14 +348,14 @@ def main():
 
     def step(flags=0):
         # every stage of a step is enqueued on torch's current stream, with no host synchronisation:
-        # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL all-gather -> rank-0 unpack
+        # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL gather to rank 0 -> rank-0 unpack
         r.render(cam, W, H, spp=frames, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
                  flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream, integrator=integ, samples_per_frame=4)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
         send[: local_tiles.numel()].copy_(local_tiles)
         if distributed:
-            dist.all_gather_into_tensor(gathered, send)
+            gather_tiles(send, gathered, world, rank)
         else:
             gathered[: send.numel()].copy_(send)
         if rank == 0:
@@ -407,10 +415,10 @@ def main():
             "data": "synthetic (the reference's procedural scenes; no datasets)",
             "config": {"workload": wl.description, "scene": os.path.basename(wl.scene), "width": W, "height": H,
                        "spp": wl.spp, "max_depth": wl.max_depth,
-                       "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL all-gather"},
+                       "parallelism": f"tile-sharded x{world} (interleaved 32x32 tiles) + RCCL gather to rank 0"},
             "integrator": args.integrator,
             "world_size": world,
-            "collective": ("RCCL all_gather_into_tensor of the RGBA8 tiles, once per step" if distributed
+            "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
             "roofline": roofline(cnt, stats, layout, wl.name, args.steps, samples),
             "stage_ms_per_step": stage_ms,

@@ -295,7 +295,7 @@ def tiles_per_rank(width: int, height: int, shard_count: int) -> int:
 
 def pack_tiles(rgb: np.ndarray, shard_count: int, shard_rank: int) -> np.ndarray:
     """Host twin of the device tile packing: this shard's pixels as RGBA8 words, tile-packed and
-    padded to tiles_per_rank tiles (the all-gather send buffer)."""
+    padded to tiles_per_rank tiles (the send buffer of the gather to rank 0)."""
     rgb = np.ascontiguousarray(rgb, np.uint8)
     h, w = rgb.shape[:2]
     out = np.zeros(tiles_per_rank(w, h, shard_count) * 1024, np.uint32)

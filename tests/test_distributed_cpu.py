@@ -1,9 +1,10 @@
 """CPU, world_size 2 over gloo: the multi-GPU data path of bench.py / DESIGN.md §Multi-GPU.
 
 Each rank renders its interleaved 32x32 tiles (oracle stands in for the GPU render here — this is a
-test of sharding + packing + the one all-gather + unpack, not of the renderer), packs them with the
-product's sptr_host_pack_tiles, all-gathers, and unpacks with sptr_host_unpack_tiles.  The gathered
+test of sharding + packing + the one gather to rank 0 + unpack, not of the renderer), packs them with the
+product's sptr_host_pack_tiles, gathers them to rank 0 with bench.gather_tiles, and unpacks with sptr_host_unpack_tiles.  The gathered
 image must equal a single-rank render bit for bit."""
+import importlib.util
 import os
 import socket
 import sys
@@ -39,7 +40,11 @@ def _worker(rank, world, port, out_dir):
     tpr = sptr.tiles_per_rank(W, H, world)
     assert tiles.size == tpr * 1024
     gathered = torch.zeros(world * tiles.size, dtype=torch.int32)
-    dist.all_gather_into_tensor(gathered, torch.from_numpy(tiles.view(np.int32)))
+    # the bench's own data-path collective: every rank's tiles gathered to rank 0
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    bench.gather_tiles(torch.from_numpy(tiles.view(np.int32)), gathered, world, rank)
     rays = torch.tensor([cnt["rays_closest"] + cnt["rays_shadow"]], dtype=torch.float64)
     dist.all_reduce(rays)
     if rank == 0:
@@ -79,7 +84,7 @@ def _bench(args, env=None, timeout=240):
 
 def test_bench_gpus_2_launches_two_ranks():
     """`bench.py --gpus 2` with no torch.distributed environment launches 2 ranks itself (a child
-    torch.distributed.run); --dry-run runs the tile schedule + all-gather + unpack over gloo."""
+    torch.distributed.run); --dry-run runs the tile schedule + gather + unpack over gloo."""
     rc, line, err = _bench(["--gpus", "2", "--dry-run", "--workload", "c1"])
     assert rc == 0, err[-3000:]
     assert line["dry_run"] and line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"

@@ -156,7 +156,7 @@ def test_c4_4k_pixel_indexing(renderer, c4_frame):
 
 def test_c4_8way_shard_union(renderer, c4_frame):
     """The C4 multi-GPU schedule at full size: 8 interleaved tile shards, each rank's resolved tiles
-    packed as the all-gather sends them, unpacked on rank 0 == the one-GPU frame, byte for byte."""
+    packed as the gather to rank 0 sends them, unpacked on rank 0 == the one-GPU frame, byte for byte."""
     cam, st0, rgb0, _ = c4_frame
     G, W, H = 8, 3840, 2160
     tpr = sptr.tiles_per_rank(W, H, G)
