@@ -120,6 +120,7 @@ __device__ __forceinline__ uint32_t block_take(uint32_t* s_next, bool pred) { re
 // different XCDs and every XCD's private 4 MB L2 has to hold the BVH working set of the whole
 // frame.  Remapping gives XCD x the contiguous logical range [x*G/8, (x+1)*G/8).
 constexpr uint32_t kXcds = 8;
+constexpr uint64_t kL2BytesPerXcd = 4ull << 20;
 __device__ __forceinline__ uint32_t logical_block() {
   const uint32_t g = gridDim.x, b = blockIdx.x;
   return (g % kXcds) ? b : (b % kXcds) * (g / kXcds) + b / kXcds;
@@ -1530,6 +1531,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 #endif
   const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x == 0) s_cnt_n = s_cnt_s = s_rays = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < kXcds)  // k_shadow_dyn's per-XCD queues of this bounce
+    w.work[((uint32_t)depth % (kWorkWords / 256u)) * 256u + threadIdx.x * 32u] = 0u;
   const Staged sc = stage_scene<kFuse>(sv, lds);
   Visits vc;
   uint32_t rays = 0u;
@@ -1812,7 +1815,11 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
 // k_shadow for wide BVHs traversed from L2/HBM with one light (C3, C5): the any-hit queries of the
 // shadow records, with lanes refilled as in k_trace_dyn.  Per record: the same query, and the same
 // radiance update when it is unoccluded.
-template <bool kCount>
+// kQueue (scenes traversed from HBM): the block's tasks are handed out by per-XCD work queues
+// (below) instead of the block's static share.  Measured (r02i, profiles/r02i_ab_shadow_queue.txt):
+// C5 shadow 4.97 -> 4.78 ms/step; C3 (L2 scene, 0.14-ms launches) 0.82 -> 0.87, so L2 scenes keep
+// the static share.
+template <bool kCount, bool kQueue>
 __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(SceneView sv, ShadeView sh, WaveView w, int depth,
                                                                            uint32_t nseg_in) {
   __shared__ KernelStack<false> s_stack;
@@ -1837,10 +1844,57 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   vec3 contrib;
   Ray r;
   WideWalk wk;
+  // kQueue: one queue per XCD (counter at a 128-B stride, zeroed by k_shade) hands out that XCD's
+  // 256-task chunks of the static round-robin schedule in order, 64 tasks at a time to a wave whose
+  // chunk is used up, so the schedule's L2 locality stays, each counter sees an eighth of the grabs,
+  // and no wave idles while its XCD still holds unstarted tasks.  Any block may trace any of its
+  // XCD's tasks: they only add to rad[p], there is no output stream.
+  constexpr uint32_t kQueueChunk = 64u;
+  const bool xm = (gridDim.x % kXcds) == 0u;
+  const uint32_t xcd = xm ? blockIdx.x % kXcds : 0u;
+  const uint32_t per_xcd = xm ? gridDim.x / kXcds : gridDim.x;  // logical blocks per XCD
+  uint32_t* queue = w.work + ((uint32_t)depth % (kWorkWords / 256u)) * 256u + xcd * 32u;
+  const uint32_t lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t cbase = 0u, cend = 0u;  // the wave's current chunk [cbase, cend) (wave-uniform)
+  bool drained = false;            // the queue has no unstarted task left for this wave
   for (;;) {
-    const uint32_t k = block_take(&s_next, !have);
-    if (!have && k < nb) {
-      const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, block_item(sd, k)) * ts;
+    uint32_t item = kNoHit;
+    bool more;  // unstarted tasks may remain for this wave
+    if constexpr (kQueue) {
+      const unsigned long long need = __ballot(!have);
+      if (need != 0ull && !drained) {
+        const uint32_t cnt = (uint32_t)__popcll(need), rank = (uint32_t)__popcll(need & below);
+        const uint32_t t1 = min(cnt, cend - cbase);
+        if (!have && rank < t1) item = cbase + rank;
+        cbase += t1;
+        if (cnt > t1) {  // the chunk ran out: the next one from the queue
+          uint32_t u = 0u;
+          if (lane == 0u) u = atomicAdd(queue, 1u);
+          u = __shfl(u, 0);
+          // unit u: 64-task quarter u % 4 of this XCD's (u / 4)-th chunk c = j * G + xcd * per + rr
+          const uint32_t kq = u >> 2, j = kq / per_xcd, rr = kq - j * per_xcd;
+          const uint64_t c = (uint64_t)j * gridDim.x + (uint64_t)xcd * per_xcd + rr;
+          const uint64_t b0 = c * kBlock + (u & 3u) * kQueueChunk;
+          if (b0 >= n) {
+            drained = true;
+          } else {
+            cbase = (uint32_t)b0;
+            cend = min((uint32_t)b0 + kQueueChunk, n);
+            const uint32_t t2 = min(cnt - t1, cend - cbase);
+            if (!have && rank >= t1 && rank - t1 < t2) item = cbase + (rank - t1);
+            cbase += t2;
+          }
+        }
+      }
+      more = !drained;
+    } else {
+      const uint32_t k = block_take(&s_next, !have);
+      if (!have && k < nb) item = block_item(sd, k);
+      more = __ballot(!have && k < nb) != 0ull;
+    }
+    if (item != kNoHit) {
+      const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, item) * ts;
       const float4 c = task[1];
       const uint32_t tag = __float_as_uint(c.w);
       if (tag != 0u) {
@@ -1858,8 +1912,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
       }
     }
     if (__ballot(have) == 0ull) {
-      if (__ballot(!have && k < nb) == 0ull) break;
-      continue;
+      if (!more) break;  // every lane idle and nothing left to take
+      continue;          // only unlit tasks taken
     }
     if (have && !done)
       done = wide_walk<true, kCount>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref,
@@ -2883,14 +2937,17 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   unsigned g = 0;
   if (!L && W && w.L == 1u && !no_dyn()) {  // wide BVH from L2/HBM, one light: refilling lanes
     const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
-    if (count) {
-      g = resident_grid((const void*)&k_shadow_dyn<true>, lbd);
-      hipLaunchKernelGGL(k_shadow_dyn<true>, dim3(g), b, lbd, s, sv, sh, w, depth, nseg);
-    } else {
-      g = resident_grid((const void*)&k_shadow_dyn<false>, lbd);
-      hipLaunchKernelGGL(k_shadow_dyn<false>, dim3(g), b, lbd, s, sv, sh, w, depth, nseg);
-    }
-    return g;
+    // per-XCD work queues for scenes larger than an XCD's L2 (k_shadow_dyn kQueue)
+    const bool queue = sv.scene_bytes > kL2BytesPerXcd;
+    return dispatch(
+        [&](auto fl) -> unsigned {
+          return [&]<bool C, bool Q>(Flags<C, Q>) {
+            const unsigned gq = resident_grid((const void*)&k_shadow_dyn<C, Q>, lbd);
+            hipLaunchKernelGGL((k_shadow_dyn<C, Q>), dim3(gq), b, lbd, s, sv, sh, w, depth, nseg);
+            return gq;
+          }(fl);
+        },
+        Flags<>{}, count, queue);
   }
 #define SPTR_SHADOW(Lc, C, Wc)                                                                      \
   do {                                                                                              \

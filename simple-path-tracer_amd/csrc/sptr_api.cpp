@@ -149,6 +149,7 @@ WaveView wave_view(Context& c) {
   w.segS = SegTable{seg + 2 * (kMaxSegs + 4), seg + 2 * (kMaxSegs + 4) + kMaxSegs};
   w.bstat = reinterpret_cast<unsigned long long*>(seg + 3 * (kMaxSegs + 4));
   w.bstat_closest = w.bstat + kMaxSegs;
+  w.work = reinterpret_cast<uint32_t*>(w.bstat_closest + kMaxSegs);
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
@@ -685,7 +686,7 @@ int sptr_create(int device, sptr_ctx** out) {
     delete x;
     return SPTR_ERR_HIP;
   }
-  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8;
+  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kWorkWords * 4;
   if (ensure_buf(c.w_seg, seg_bytes) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
       ensure_buf(c.dyn, 64) != hipSuccess ||
       hipMemset(c.w_seg.p, 0, seg_bytes) != hipSuccess) {

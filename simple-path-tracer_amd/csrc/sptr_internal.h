@@ -164,6 +164,7 @@ struct FrameView {
 // pixel's leading misses into accum and record the resume slot for k_accum.
 enum : uint32_t { kFoldNone = 0, kFoldThread = 1, kFoldWave = 2 };
 
+constexpr uint32_t kWorkWords = 512;  // work-queue counters (WaveView::work): 2 bounce slots x 8 XCDs, 128-B apart
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 
 // 64-bit totals block
@@ -200,6 +201,7 @@ struct WaveView {
   unsigned long long* tot;
   unsigned long long* bstat;          // [kMaxSegs] per-block any-hit tallies (k_shadow, k_tail), folded by k_accum
   unsigned long long* bstat_closest;  // [kMaxSegs] per-block closest-hit tallies of k_tail
+  uint32_t* work;    // [kWorkWords] work-queue counters of k_shadow_dyn, one per bounce (zeroed by k_shade)
   uint32_t seg_cap;  // records allocated per segmented stream (bounds guard)
   uint32_t hrec_cap;  // hit records allocated (bounce 0 segments span k samples per pixel slot)
   uint32_t L;        // lights (tasks per shaded path)
