@@ -780,7 +780,8 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv&
 constexpr float kCullMarginPx = 1.0f / 64.0f;
 constexpr float kCullSlack = 1e-4f;
 #ifndef SPTR_CULL_DEPTH
-#define SPTR_CULL_DEPTH 4  // r02 A/B: 2 -> 4 levels, C2 primary trace 1.12 -> 1.09 ms; deeper gains nothing
+#define SPTR_CULL_DEPTH 8  // r02 A/B: 2 -> 4 levels, C2 primary trace 1.12 -> 1.09 ms; 4 -> 8 (r02i): C5 primary
+                           // trace 3.11 -> 2.87 ms, C2/C3 unchanged (profiles/r02i_ab_cull_depth.txt)
 #endif
 constexpr int kCullDepth = SPTR_CULL_DEPTH;  // BVH2 levels below the root whose boxes the test visits
 struct Box {
