@@ -779,11 +779,12 @@ __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv&
 // this test itself, so a pixel is culled only when its rays certainly miss.
 constexpr float kCullMarginPx = 1.0f / 64.0f;
 constexpr float kCullSlack = 1e-4f;
-#ifndef SPTR_CULL_DEPTH
-#define SPTR_CULL_DEPTH 8  // r02 A/B: 2 -> 4 levels, C2 primary trace 1.12 -> 1.09 ms; 4 -> 8 (r02i): C5 primary
-                           // trace 3.11 -> 2.87 ms, C2/C3 unchanged (profiles/r02i_ab_cull_depth.txt)
-#endif
-constexpr int kCullDepth = SPTR_CULL_DEPTH;  // BVH2 levels below the root whose boxes the test visits
+// BVH2 levels below the root whose boxes the test visits (FrameView::cull_depth, chosen per call by
+// cull_depth_for): r02 A/B, 2 -> 4 levels: C2 primary trace 1.12 -> 1.09 ms; 4 -> 8 (r02i): C5
+// primary trace 3.11 -> 2.87 ms, C2/C3 unchanged (profiles/r02i_ab_cull_depth.txt).  The mask is
+// recomputed whenever the camera moves, so calls of few samples per pixel (the interactive 1 spp
+// per frame) keep the cheaper 4-level test.
+constexpr int kCullDepthMax = 8;
 struct Box {
   vec3 lo, hi;
 };
@@ -819,7 +820,7 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
     uint32_t link, depth;
     Box b;
   };
-  Entry st[2 * kCullDepth + 2];
+  Entry st[2 * kCullDepthMax + 2];
   int sp = 0;
   {
     const BvhNode r = sv.nodes[0];
@@ -829,7 +830,7 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   while (sp > 0) {
     const Entry e = st[--sp];
     if (box_outside(e.b, n, f.cam_pos)) continue;
-    if ((e.link & kLeafBit) || e.depth >= (uint32_t)kCullDepth) return false;
+    if ((e.link & kLeafBit) || e.depth >= f.cull_depth) return false;
     const BvhNode g = sv.nodes[e.link];
     st[sp++] = Entry{g.link.y, e.depth + 1u, Box{v3(g.rxy.x, g.rxy.z, g.z.z), v3(g.rxy.y, g.rxy.w, g.z.w)}};
     st[sp++] = Entry{g.link.x, e.depth + 1u, Box{v3(g.lxy.x, g.lxy.z, g.z.x), v3(g.lxy.y, g.lxy.w, g.z.y)}};
@@ -2909,6 +2910,8 @@ unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView&
       },
       Flags<>{}, depth == 0, fuse);
 }
+
+uint32_t cull_depth_for(uint32_t spp) { return spp >= 16u ? (uint32_t)kCullDepthMax : 4u; }
 
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s) {
   if (f.P == 0u) return;

@@ -199,6 +199,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.pixel_major = 0;
   v.dyn = nullptr;
   v.cull = nullptr;
+  v.cull_depth = 4u;
   v.sky_fold = 0u;
   v.plist = nullptr;
   v.integrator = f.integrator;
@@ -445,11 +446,14 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it)
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
     // the mask depends on the scene, the pixel layout (both covered by the epoch) and the camera
-    if (c.cull_epoch != c.epoch || std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) != 0) {
+    fv.cull_depth = cull_depth_for(f.spp);
+    if (c.cull_epoch != c.epoch || c.cull_depth != fv.cull_depth ||
+        std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) != 0) {
       API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 4, s));
       launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
       c.cull_epoch = c.epoch;
       c.cull_cam = f.camera;
+      c.cull_depth = fv.cull_depth;
     }
     fv.cull = static_cast<const uint32_t*>(c.cull.p);
   }

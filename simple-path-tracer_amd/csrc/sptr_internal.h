@@ -156,6 +156,7 @@ struct FrameView {
   uint32_t ox_has_light;
   const uint32_t* cull;  // bit l: camera rays through local pixel l cannot hit the scene (k_cull); may be null
   uint32_t sky_fold;     // path-major bounce 0 with a cull mask: k_sky sums culled pixels into accum
+  uint32_t cull_depth;   // BVH2 levels k_cull tests (<= kCullDepthMax)
   const uint32_t* plist; // with sky_fold: the unculled local pixels (count at plist[P]), bounce 0's paths
 };
 
@@ -291,6 +292,7 @@ struct Context {
   // what the mask was computed for (state epoch, camera): k_cull reruns only when these change
   uint64_t cull_epoch = 0;
   sptr_camera cull_cam{};
+  uint32_t cull_depth = 0;  // depth the cached mask was computed with
   uint32_t last_samples = 0;  // accumulation count after the last render
   // query scratch
   DevBuf qbuf;
@@ -326,6 +328,8 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
                    hipStream_t s);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
+// BVH2 levels the bounce-0 pixel cull tests for a call of spp samples per pixel
+uint32_t cull_depth_for(uint32_t spp);
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s);
 void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
