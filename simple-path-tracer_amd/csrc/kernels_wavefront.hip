@@ -30,6 +30,9 @@
 #ifndef SPTR_TRACE_PM_WAVES
 #define SPTR_TRACE_PM_WAVES SPTR_TRACE_WAVES
 #endif
+#ifndef SPTR_TRACE_WP_WAVES
+#define SPTR_TRACE_WP_WAVES SPTR_TRACE_WAVES  // lane-group bounce 0 (sharded LDS-scene batches)
+#endif
 #ifndef SPTR_TRACE4_WAVES
 #define SPTR_TRACE4_WAVES 7  // wide BVH, bounces >= 1 (refilling kernels, no packed FP32): C5 16.0 -> 15.2-15.6 ms/step (r02 ab24/25)
                              // (bounce 0 stays at 7: coherent rays gain more from occupancy, 8.4 -> 5.4)
@@ -1058,7 +1061,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 template <bool kLds, bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WP_WAVES)
     k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
