@@ -2067,59 +2067,6 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
   }
 }
 
-// --------------------------------------------------------------------------------- k_accum / resolve
-// Per-pixel sample sums in sample order.  A folding bounce 0 (f.pixel_major: thread or lane group
-// per pixel; f.sky_fold: k_sky for the culled pixels of a path-major bounce 0) began them:
-// accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
-// batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
-// slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
-__global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, float4* accum) {
-  const FrameView f = frame_dyn(fin);
-  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
-    uint32_t s0 = 0u;
-    vec3 a = v3(0.0f, 0.0f, 0.0f);
-    if (f.pixel_major || f.sky_fold) {
-      const float4 a4 = accum[l];
-      s0 = __float_as_uint(a4.w);
-      if (s0 >= f.k) continue;
-      a = xyz(a4);
-    } else if (!f.reset) {
-      a = xyz(accum[l]);
-    }
-    // sample order is the reference's accumulation order (one add per frame); the unroll only
-    // lets eight sample loads be in flight per thread before the first add
-    const float4* src = w.rad + l;
-    uint32_t s = s0;
-    for (; s + 8u <= f.k; s += 8u) {
-      float4 v[8];
-#pragma unroll
-      for (uint32_t j = 0; j < 8u; ++j) v[j] = src[(size_t)(s + j) * f.P];
-#pragma unroll
-      for (uint32_t j = 0; j < 8u; ++j) a = a + xyz(v[j]);
-    }
-    for (; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
-    accum[l] = f4(a, __uint_as_float(f.k));
-  }
-  if (blockIdx.x == 0) {  // fold the per-block query tallies of this batch into the totals
-    unsigned long long s = 0ull, c = 0ull;
-    for (uint32_t b = threadIdx.x; b < kMaxSegs; b += kBlock) {
-      s += w.bstat[b];
-      c += w.bstat_closest[b];
-      w.bstat[b] = 0ull;
-      w.bstat_closest[b] = 0ull;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      s += __shfl_xor(s, off);
-      c += __shfl_xor(c, off);
-    }
-    if (lane_id() == 0u) {
-      atomicAdd(&w.tot[kTotShadow], s);
-      atomicAdd(&w.tot[kTotClosest], c);
-      atomicAdd(&w.tot[kTotTail], c);
-    }
-  }
-}
-
 // EnvironmentManager::acesToneMapping (src/EnvironmentManager.cpp:63-74)
 __device__ __forceinline__ vec3 aces(vec3 c) {
   return clamp_g((c * (2.51f * c + 0.03f)) / (c * (2.43f * c + 0.59f) + 0.14f), 0.0f, 1.0f);
@@ -2153,6 +2100,80 @@ __device__ __forceinline__ uint32_t resolve_rgba_optix(float4 a) {
   const float g = 1.0f / 2.2f;
   c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
   return pack_rgba(v3(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f)));
+}
+
+// --------------------------------------------------------------------------------- k_accum / resolve
+// Per-pixel sample sums in sample order.  A folding bounce 0 (f.pixel_major: thread or lane group
+// per pixel; f.sky_fold: k_sky for the culled pixels of a path-major bounce 0) began them:
+// accum[l] holds the sum up to (excluding) slot accum[l].w, the pixel's first primary hit in this
+// batch, and all-sky pixels are already complete (slot = k) and are not touched.  Otherwise every
+// slot's radiance is summed here, onto the previous batches' sum unless the batch resets it.
+// kResolve (the last batch of a wavefront call that resolves): each thread also resolves its pixel
+// from the sum it holds, as k_resolve would next (one launch and one accum re-read less).
+template <bool kResolve>
+__global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, float4* accum, uint32_t* tiles,
+                                                  uint8_t* image) {
+  const FrameView f = frame_dyn(fin);
+  const uint32_t n_total = f.dyn ? f.dyn[2] : 0u;  // total frames of the accumulation (kResolve)
+  for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
+    uint32_t s0 = 0u;
+    vec3 a = v3(0.0f, 0.0f, 0.0f);
+    bool sum = true;
+    if (f.pixel_major || f.sky_fold) {
+      const float4 a4 = accum[l];
+      s0 = __float_as_uint(a4.w);
+      a = xyz(a4);
+      sum = s0 < f.k;
+      if (!kResolve && !sum) continue;
+    } else if (!f.reset) {
+      a = xyz(accum[l]);
+    }
+    if (sum) {
+    // sample order is the reference's accumulation order (one add per frame); the unroll only
+    // lets eight sample loads be in flight per thread before the first add
+    const float4* src = w.rad + l;
+    uint32_t s = s0;
+    for (; s + 8u <= f.k; s += 8u) {
+      float4 v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8u; ++j) v[j] = src[(size_t)(s + j) * f.P];
+#pragma unroll
+      for (uint32_t j = 0; j < 8u; ++j) a = a + xyz(v[j]);
+    }
+    for (; s < f.k; ++s) a = a + xyz(w.rad[(size_t)s * f.P + l]);
+    accum[l] = f4(a, __uint_as_float(f.k));
+    }
+    if (kResolve) {
+      int x, y;
+      const bool valid = local_pixel(f, l, x, y);
+      const uint32_t px = valid ? resolve_rgba(a, n_total) : 0u;
+      tiles[l] = px;
+      if (valid && image) {
+        uint8_t* o = image + ((size_t)y * f.W + x) * 3;
+        o[0] = (uint8_t)(px & 0xFF);
+        o[1] = (uint8_t)((px >> 8) & 0xFF);
+        o[2] = (uint8_t)((px >> 16) & 0xFF);
+      }
+    }
+  }
+  if (blockIdx.x == 0) {  // fold the per-block query tallies of this batch into the totals
+    unsigned long long s = 0ull, c = 0ull;
+    for (uint32_t b = threadIdx.x; b < kMaxSegs; b += kBlock) {
+      s += w.bstat[b];
+      c += w.bstat_closest[b];
+      w.bstat[b] = 0ull;
+      w.bstat_closest[b] = 0ull;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off);
+      c += __shfl_xor(c, off);
+    }
+    if (lane_id() == 0u) {
+      atomicAdd(&w.tot[kTotShadow], s);
+      atomicAdd(&w.tot[kTotClosest], c);
+      atomicAdd(&w.tot[kTotTail], c);
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n_arg, uint32_t* tiles,
@@ -3028,8 +3049,10 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
   else hipLaunchKernelGGL(k_sky<false>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
 }
 
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s) {
-  hipLaunchKernelGGL(k_accum, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum);
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,
+                       bool resolve, hipStream_t s) {
+  if (resolve) hipLaunchKernelGGL(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
+  else hipLaunchKernelGGL(k_accum<false>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
 }
 
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,

@@ -513,17 +513,15 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         tm.end();
       }
     }
+    // the call's last batch resolves in the same launch (k_accum<true>: each thread resolves the
+    // sum it holds, as k_resolve would next)
+    const bool resolve = done + kk >= f.spp && !(f.flags & SPTR_FRAME_NO_RESOLVE);
     tm.begin(4);
-    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), s);
+    launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
+                      static_cast<uint8_t*>(c.image.p), resolve, s);
     tm.end();
     done += kk;
     ++waves;
-  }
-  if (!(f.flags & SPTR_FRAME_NO_RESOLVE)) {
-    tm.begin(4);
-    launch_resolve(fv, static_cast<const float4*>(c.accum.p), 0u, static_cast<uint32_t*>(c.tiles.p),
-                   static_cast<uint8_t*>(c.image.p), s);
-    tm.end();
   }
   tm.end_call();
   return waves;

@@ -327,7 +327,9 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
                    hipStream_t s);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, hipStream_t s);
+// resolve: also tone-map the sums into tiles (+ image) in the same launch (the call's last batch)
+void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,
+                       bool resolve, hipStream_t s);
 // BVH2 levels the bounce-0 pixel cull tests for a call of spp samples per pixel
 uint32_t cull_depth_for(uint32_t spp);
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s);
