@@ -367,12 +367,18 @@ def main():
     # untimed instrumented pass: BVH node / primitive fetch counts for the algorithmic-bytes model
     step(sptr.SPTR_FRAME_COUNT_VISITS)
     cnt = r.collect_stats()
+    # the timed call shape (its event flag differs from the warmup's) seen twice before timing: the
+    # library captures a repeated shape into a launch graph on its second call, so the capture
+    # happens here and every timed step replays it, as repeated renders of one frame do
+    timing = sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE
+    for _ in range(2):
+        step(timing)
+    r.collect_stats()
 
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    timing = sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE
     for _ in range(args.steps):
         step(timing)
     torch.cuda.synchronize()
