@@ -80,53 +80,113 @@ def _latest_profile(pattern):
     return best[1], os.path.relpath(best[2], ROOT)
 
 
-def roofline(cnt, stats, layout, wl_name, steps, samples):
+def _residency(layout):
+    footprint = sum(layout[k] for k in ("node_bytes", "tri_bytes", "sphere_bytes", "prim_ref_bytes"))
+    res = "lds" if layout["lds_bytes"] > 0 else ("l2" if footprint <= L2_BYTES_PER_XCD else "hbm")
+    return res, footprint
+
+
+def _counter_fracs(wl_name, kernel, avg_launch_s):
+    """counter_frac = FETCH_SIZE x2 + WRITE_SIZE per launch (the newest profiles/r*_pmc_<wl>_<kernel>.json)
+    over the live launch time; valu_issue_frac = SQ_INSTS_VALU per launch (profiles/r*_sq_<wl>_<kernel>.json)
+    over the live launch time and the 1.23e12/s issue peak; salu_per_valu from the same SQ pass."""
+    pmc, pmc_src = _latest_profile(f"r*_pmc_{wl_name}_{kernel}.json")
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    sq, sq_src = _latest_profile(f"r*_sq_{wl_name}_{kernel}.json")
+    valu = sq.get("valu_per_launch") if sq else None
+    salu = sq.get("counters_per_launch", {}).get("SQ_INSTS_SALU") if sq else None
+    return {"traffic": traffic, "traffic_source": pmc_src,
+            "counter_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s else None,
+            "valu_issue_frac": round(valu / avg_launch_s / VALU_PEAK_WAVE_INSTR_PER_S, 4) if valu and avg_launch_s else None,
+            "salu_per_valu": round(salu / valu, 3) if salu and valu else None, "valu_source": sq_src}
+
+
+def roofline(cnt, stats, layout, wl_name, steps):
     """Roofline of the dominant kernel, k_trace (all bounces; one template).
 
-    Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 + 64 n_node + 48 n_tri + 16 n_sph with the
-    visit counts taken from an instrumented pass over the same rays; primary rays (raygen fused, no
-    input stream) are charged their 8 written bytes only.  Which of the node/primitive bytes are HBM
-    bytes depends on where the scene lives:
+    cnt: the stats of one instrumented (SPTR_FRAME_COUNT_VISITS) step, used only for BVH visits per
+    traversed ray; stats: the K timed steps (launch times, launch counts and the rays the trace
+    launches traversed, all summed over the K steps), so every per-launch figure below is a ratio of
+    two sums over the same launches and does not depend on K.
+
+    Rays are those the trace launches actually traverse (the library's traced_primary /
+    traced_bounce): camera rays of frustum-culled pixels are answered without a traversal and are not
+    charged.  Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 (28 read: path id, o, d; 8 written:
+    t, prim) + 64 n_node + 48 n_tri + 16 n_sph, with the visit counts per traversed ray of the
+    instrumented pass (bounce 0 and later bounces separately); a camera ray reads no input stream
+    (raygen is fused into the bounce-0 trace) and is charged its 8 written bytes.  Which node/primitive
+    bytes are HBM bytes depends on where the scene lives:
       lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU;
-      l2   scene fits one XCD's 4 MB L2: one scene copy per XCD per launch (counting every visit as
-           HBM bytes would report more than the peak on C3);
+      l2   scene fits one XCD's 4 MB L2: one scene copy per XCD per launch;
       hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in §8(d).
-    Beside the modelled fraction: counter_frac = FETCH_SIZE x2 + WRITE_SIZE per launch (the latest
-    profiles/r*_pmc_<wl>_trace.json) over the live launch time, and valu_issue_frac = SQ_INSTS_VALU per
-    launch (profiles/r*_sq_<wl>_trace.json) over the live launch time and the 1.23e12/s issue peak."""
+    frac_s8d: §8(d) taken literally (36 B per traversed ray and every visit charged, whatever the residency).
+    Beside them: counter_frac / valu_issue_frac / salu_per_valu from the session's rocprofv3 passes."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
-    launches_per_step = max(1, launches // max(1, steps))
-    traced = cnt.rays_closest - cnt.rays_tail  # closest-hit queries of k_trace (the rest run in k_tail)
-    primary = min(traced, samples)  # one primary ray per pixel sample, all traced by k_trace
-    stream = (STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (traced - primary) + STREAM_WRITE_BYTES * primary
+    tp = sum(s.traced_primary for s in stats)
+    tb = sum(s.traced_bounce for s in stats)
+    # visits per traversed ray, bounce 0 and later bounces (instrumented step)
+    vp = [cnt.node_visits_primary, cnt.tri_tests_primary, cnt.sphere_tests_primary]
+    vb = [cnt.node_visits - vp[0], cnt.tri_tests - vp[1], cnt.sphere_tests - vp[2]]
+    pp = [v / max(1, cnt.traced_primary) for v in vp]
+    pb = [v / max(1, cnt.traced_bounce) for v in vb]
     node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0
-    scene = node_b * cnt.node_visits + 48.0 * cnt.tri_tests + 16.0 * cnt.sphere_tests
-    lds = layout["lds_bytes"] > 0
-    footprint = sum(layout[k] for k in ("node_bytes", "tri_bytes", "sphere_bytes", "prim_ref_bytes"))
-    residency = "lds" if lds else ("l2" if footprint <= L2_BYTES_PER_XCD else "hbm")
-    hbm_alg = stream + {"lds": 0.0, "l2": XCDS * footprint * launches_per_step, "hbm": scene}[residency]
-    per_launch = hbm_alg / launches_per_step
+    scene_p = node_b * pp[0] + 48.0 * pp[1] + 16.0 * pp[2]
+    scene_b = node_b * pb[0] + 48.0 * pb[1] + 16.0 * pb[2]
+    stream = STREAM_WRITE_BYTES * tp + (STREAM_READ_BYTES + STREAM_WRITE_BYTES) * tb
+    residency, footprint = _residency(layout)
+    scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * tb}[residency]
+    per_launch = (stream + scene) / max(1, launches)
     achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    pmc, pmc_src = _latest_profile(f"r*_pmc_{wl_name}_trace.json")
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    sq, sq_src = _latest_profile(f"r*_sq_{wl_name}_trace.json")
-    valu = sq.get("valu_per_launch") if sq else None
+    s8d = ((STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (tp + tb) + 64.0 * (pp[0] * tp + pb[0] * tb)
+           + 48.0 * (pp[1] * tp + pb[1] * tb) + 16.0 * (pp[2] * tp + pb[2] * tb)) / max(1, launches)
     out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": pmc_src,
-           "counter_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s else None,
-           "valu_issue_frac": round(valu / avg_launch_s / VALU_PEAK_WAVE_INSTR_PER_S, 4) if valu and avg_launch_s else None,
-           "valu_source": sq_src,
-           "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
-           "launches_per_step": launches_per_step,
-           "scene_in_lds": lds, "scene_residency": residency, "scene_bytes": int(footprint),
-           "b_ray_full_gbs": round((stream + scene) / launches_per_step / avg_launch_s / 1e9, 1) if avg_launch_s else 0,
-           "per_ray": {"nodes": round(cnt.node_visits / max(1, traced), 3),
-                       "tris": round(cnt.tri_tests / max(1, traced), 3),
-                       "spheres": round(cnt.sphere_tests / max(1, traced), 3)}}
+           "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    out.update(_counter_fracs(wl_name, "trace", avg_launch_s))
+    out.update({
+        "frac_s8d": round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None,
+        "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+        "launches_per_step": round(launches / max(1, steps), 3),
+        "traversed_rays_per_launch": round((tp + tb) / max(1, launches)),
+        "scene_in_lds": residency == "lds", "scene_residency": residency, "scene_bytes": int(footprint),
+        "per_ray": {"primary": {"nodes": round(pp[0], 3), "tris": round(pp[1], 3), "spheres": round(pp[2], 3)},
+                    "bounce": {"nodes": round(pb[0], 3), "tris": round(pb[1], 3), "spheres": round(pb[2], 3)}}})
     fr = {"hbm_model": out["frac"], "hbm_counters": out["counter_frac"], "valu_issue": out["valu_issue_frac"]}
     known = {k: v for k, v in fr.items() if v is not None}
     out["binding"] = max(known, key=known.get) if known else None
+    return out
+
+
+# shadow task bytes: {origin, tfar} + {contrib, path id} read (32 B) and the radiance read-modify-write
+# of an unoccluded task (32 B; charged to every task, an upper bound)
+SHADOW_TASK_BYTES = 64.0
+
+
+def shadow_roofline(cnt, stats, layout, wl_name, steps):
+    """Roofline of the any-hit stage (k_shadow / k_shadow_dyn) where it runs as launches of its own (L2/HBM
+    scenes; LDS scenes trace the shadow ray inside k_shade, and their line carries no shadow entry).  Per
+    task: SHADOW_TASK_BYTES + 64 n_node + 48 n_tri with the instrumented pass's visits per any-hit query,
+    HBM bytes per the scene residency as in roofline(); counters / VALU / SALU from the session's
+    r*_pmc_<wl>_shadow.json / r*_sq_<wl>_shadow.json."""
+    launches = sum(s.shadow_launches for s in stats)
+    if not launches:
+        return None
+    avg_launch_s = sum(s.ms_shadow for s in stats) / launches * 1e-3
+    tasks = sum(s.rays_shadow for s in stats)
+    n_node = cnt.shadow_node_visits / max(1, cnt.rays_shadow)
+    n_tri = cnt.shadow_prim_tests / max(1, cnt.rays_shadow)
+    node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0
+    residency, footprint = _residency(layout)
+    scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": (node_b * n_node + 48.0 * n_tri) * tasks}[residency]
+    per_launch = (SHADOW_TASK_BYTES * tasks + scene) / launches
+    achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    out = {"bound": "hbm", "kernel": "k_shadow", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    out.update(_counter_fracs(wl_name, "shadow", avg_launch_s))
+    out.update({"bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                "launches_per_step": round(launches / max(1, steps), 3), "tasks_per_launch": round(tasks / launches),
+                "per_task": {"nodes": round(n_node, 3), "tris": round(n_tri, 3)}, "scene_residency": residency,
+                "ms_per_step": round(sum(s.ms_shadow for s in stats) / max(1, steps), 3)})
     return out
 
 
@@ -246,17 +306,26 @@ def dry_run(args, wl, world, rank):
     W, H = wl.width, wl.height
     yy, xx = np.mgrid[0:H, 0:W].astype(np.uint32)
     pattern = np.stack([(xx * 7 + yy) & 255, (xx ^ yy) & 255, (xx * 13 + yy * 5) & 255], -1).astype(np.uint8)
-    tiles = sptr.pack_tiles(pattern, world, rank)
+    dist.barrier()
+    t0 = time.perf_counter()
+    tiles = sptr.pack_tiles(pattern, world, rank)  # stands in for the render + resolve of this rank's tiles
+    t1 = time.perf_counter()
     gathered = torch.zeros(world * tiles.size, dtype=torch.int32)
     gather_tiles(torch.from_numpy(tiles.view(np.int32)), gathered, world, rank)
+    img = sptr.unpack_tiles(gathered.numpy().view(np.uint32), world, W, H) if rank == 0 else None
+    t2 = time.perf_counter()
     mine = torch.tensor([float(((tiles >> 24) == 255).sum())], dtype=torch.float64)  # pixels inside the image
     dist.all_reduce(mine)
+    # the same per-step split the GPU line reports: max over ranks of render and of gather (+ unpack)
+    tm = torch.tensor([(t1 - t0) * 1e3, (t2 - t1) * 1e3], dtype=torch.float64)
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
     if rank == 0:
-        img = sptr.unpack_tiles(gathered.numpy().view(np.uint32), world, W, H)
         ok = bool(np.array_equal(img, pattern)) and int(mine.item()) == W * H
         print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": dist.get_world_size(),
                           "backend": dist.get_backend(), "workload": wl.name, "tiles_per_rank": int(tiles.size // 1024),
-                          "pixels_covered": int(mine.item()), "gather_ok": ok}), flush=True)
+                          "pixels_covered": int(mine.item()), "gather_ok": ok,
+                          "render_ms": round(float(tm[0]), 4), "gather_ms": round(float(tm[1]), 4),
+                          "gather_bytes": int(world * tiles.size * 4) if world > 1 else 0}), flush=True)
         if not ok:
             sys.exit(1)
 
@@ -346,20 +415,27 @@ def main():
     # PathTracer mode: a frame is 4 samples (setupPathTracer), so spp/4 frames give the same samples
     frames = max(1, wl.spp // 4) if args.integrator == "pathtracer" else wl.spp
 
-    def step(flags=0):
+    def step(flags=0, ev=None):
         # every stage of a step is enqueued on torch's current stream, with no host synchronisation:
-        # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL gather to rank 0 -> rank-0 unpack
+        # render (SPTR_FRAME_ASYNC) -> tile copy -> RCCL gather to rank 0 -> rank-0 unpack.  ev: three
+        # timing events (render start, render + tile copy done, gather + unpack done) on that stream.
+        if ev:
+            ev[0].record()
         r.render(cam, W, H, spp=frames, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
                  flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream, integrator=integ, samples_per_frame=4)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
         send[: local_tiles.numel()].copy_(local_tiles)
+        if ev:
+            ev[1].record()
         if distributed:
             gather_tiles(send, gathered, world, rank)
         else:
             gathered[: send.numel()].copy_(send)
         if rank == 0:
             r.unpack_tiles(gathered.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
+        if ev:
+            ev[2].record()
 
     for _ in range(args.warmup):
         step()
@@ -370,40 +446,52 @@ def main():
     # the timed call shape (its event flag differs from the warmup's) seen twice before timing: the
     # library captures a repeated shape into a launch graph on its second call, so the capture
     # happens here and every timed step replays it, as repeated renders of one frame do
-    timing = sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE
+    # Every timed step recomputes the bounce-0 cull mask (SPTR_FRAME_RECULL): it is a per-camera
+    # structure, and a renderer whose camera moves pays it every frame, so it is inside the timed step.
+    timing = (sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE) | sptr.SPTR_FRAME_RECULL
     for _ in range(2):
         step(timing)
     r.collect_stats()
 
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timing)
+    for i in range(args.steps):
+        step(timing, evs[i])
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stats = [r.collect_stats()]  # the K timed steps' counters and stage events, summed
+    render_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    gather_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
 
     rays = sum(s.rays_closest + s.rays_shadow for s in stats)
     samples = sum(s.samples for s in stats)
-    t = torch.tensor([elapsed, float(rays), float(samples)], dtype=torch.float64, device=dev)
+    traced_p = sum(s.traced_primary for s in stats)
+    t = torch.tensor([elapsed, float(rays), float(samples), float(traced_p), render_ms, gather_ms],
+                     dtype=torch.float64, device=dev)
+    per_rank_render = [render_ms]
     if distributed:
         tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, rays, samples = float(tmax[0]), float(tsum[1]), float(tsum[2])
+        elapsed, rays, samples, traced_p = float(tmax[0]), float(tsum[1]), float(tsum[2]), float(tsum[3])
+        render_ms, gather_ms = float(tmax[4]), float(tmax[5])
+        allr = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(allr, t[4:5].clone())
+        per_rank_render = [float(x.item()) for x in allr]
         # the gathered frame is the same bytes a 1-GPU render gives (tests/test_gpu_parity.py shard union)
         want = W * H * (frames * 4 if args.integrator == "pathtracer" else wl.spp) * args.steps
         assert int(tsum[2]) == want, (int(tsum[2]), want)
 
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
-                    for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum") if args.stage_timing
-                              else ("trace0", "trace"))}
+                    for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum", "cull")
+                              if args.stage_timing else ("trace0", "trace", "shadow", "cull"))}
         knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
@@ -426,10 +514,21 @@ def main():
             "world_size": world,
             "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
-            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, samples),
+            "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
+            "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
             "stage_ms_per_step": stage_ms,
+            "cull_ms": round(sum(s.ms_cull for s in stats) / args.steps, 4),
+            "cull_launches_per_step": sum(s.cull_launches for s in stats) / args.steps,
             "tail_rays_per_step": int(sum(s.rays_tail for s in stats) / args.steps),
             "rays_per_step": int(rays / args.steps),
+            # queries answered without a traversal: the camera rays of frustum-culled pixels (all ranks)
+            "culled_primary_per_step": int((samples - traced_p) / args.steps) if args.integrator == "wavefront" else 0,
+            "traversed_rays_per_step": int((rays - (samples - traced_p if args.integrator == "wavefront" else 0)) / args.steps),
+            # per step: max over ranks of render (+ tile copy) and of gather (+ rank-0 unpack), HIP events
+            "render_ms": round(render_ms, 4),
+            "gather_ms": round(gather_ms, 4),
+            "gather_bytes": int(shards * tiles_per_rank * 4096) if distributed else 0,
+            "render_ms_per_rank": [round(x, 4) for x in per_rank_render],
             "scene": {"prims": info["prims"], "lbvh_nodes": info["nodes"], "bvh_depth": info["depth"],
                       "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"],
                       "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},

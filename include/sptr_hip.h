@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 3
+#define SPTR_ABI_VERSION 4
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -108,10 +108,14 @@ enum sptr_frame_flags {
   SPTR_FRAME_COUNT_VISITS = 4u, /* one instrumented trace pass: count BVH node / primitive fetches */
   SPTR_FRAME_ASYNC = 8u, /* enqueue only: return without waiting; stats are left zero and the call's
                             counters and stage times accumulate until sptr_collect_stats */
-  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace launches only (ms_trace, ms_trace0,
-                                   trace_launches): the other stages run back to back */
-  SPTR_FRAME_NO_CULL = 32u /* diagnostic: bounce 0 traverses every camera ray, without the pixel-frustum
-                              cull (the image is the same either way) */
+  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace, shadow and cull launches only (ms_trace,
+                                   ms_trace0, trace_launches, ms_shadow, shadow_launches, ms_cull): the
+                                   other stages run back to back */
+  SPTR_FRAME_NO_CULL = 32u, /* diagnostic: bounce 0 traverses every camera ray, without the pixel-frustum
+                               cull (the image is the same either way) */
+  SPTR_FRAME_RECULL = 64u /* recompute the bounce-0 pixel-frustum cull mask in this call even when the
+                             camera and scene are unchanged (the per-frame cost of a moving camera;
+                             bench.py times its steps this way) */
 };
 
 /* Integrators (sptr_frame.integrator).  The reference selects between them per frame in
@@ -170,6 +174,17 @@ typedef struct sptr_stats {
   double ms_trace0, ms_shade0; /* SPTR_FRAME_TIMING: bounce-0 parts of ms_trace / ms_shade */
   uint64_t rays_tail;          /* closest-hit queries (of rays_closest) traced by the path-per-thread tail */
   double ms_tail;              /* SPTR_FRAME_TIMING: the tail launch */
+  /* ABI 4: the rays the trace stage (ms_trace / trace_launches) actually traversed.  Camera rays of
+   * frustum-culled pixels count as closest-hit queries (rays_closest) but never reach a traversal:
+   * traced_primary = unculled pixel samples of bounce 0, traced_bounce = queued rays of bounces >= 1
+   * traced by the wavefront trace kernels (not the fused bounce or path-per-thread tail kernels). */
+  uint64_t traced_primary, traced_bounce;
+  uint64_t node_visits_primary, tri_tests_primary, sphere_tests_primary; /* SPTR_FRAME_COUNT_VISITS: the
+                                                                           bounce-0 part of node_visits,
+                                                                           tri_tests, sphere_tests */
+  double ms_cull;              /* SPTR_FRAME_TIMING / _TIMING_TRACE: the pixel-cull launches (k_cull) */
+  uint64_t cull_launches;      /* calls whose cull mask was (re)computed */
+  uint64_t shadow_launches;    /* SPTR_FRAME_TIMING / _TIMING_TRACE: shadow-stage launches (ms_shadow) */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */

@@ -729,7 +729,7 @@ __device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long lon
   if (lane_id() == 0) {
     atomicAdd(&tot[base + 0], a);
     atomicAdd(&tot[base + 1], b);
-    if (base == kTotNodes) atomicAdd(&tot[base + 2], c);
+    if (base == kTotNodes || base == kTotNodesP) atomicAdd(&tot[base + 2], c);
   }
 }
 
@@ -840,24 +840,72 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   }
   return true;
 }
-// bit l of mask: pixel l is culled (see above); one ballot word pair per wave
-// plist: the valid pixels that are not culled, appended per wave (count at plist[P], zeroed before)
+// bit l of mask: pixel l is culled (see above); one ballot word pair per wave.
+// plist: the valid pixels that are not culled (count at plist[P], zeroed before).  One block per local
+// tile (four 256-pixel rounds): the tile's unculled pixels are listed in pixel order at a range that
+// one atomic per tile reserves.  (One atomic per wave on the single count word serialised 32 K waves at
+// one L2 channel: C2 k_cull 108 us.)
 __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  int x = 0, y = 0;
-  const bool valid = l < f.P && local_pixel(f, l, x, y);
-  const bool culled = valid && pixel_frustum_misses(sv, f, x, y);
-  const unsigned long long b = __ballot(culled);
-  const uint32_t lane = lane_id();
-  if ((lane & 31u) == 0u && l < f.P) mask[l >> 5] = (uint32_t)(b >> lane);
-  const unsigned long long m = __ballot(valid && !culled);
-  if (m) {
-    const int leader = __ffsll(m) - 1;
-    uint32_t base = 0u;
-    if ((int)lane == leader) base = atomicAdd(&plist[f.P], (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (valid && !culled) plist[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = l;
+  constexpr uint32_t kRounds = kTilePixels / kBlock;
+  constexpr uint32_t kWaves = kBlock / 64u;
+  __shared__ uint32_t s_cnt[kRounds * kWaves];
+  __shared__ uint32_t s_base;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  unsigned long long keep[kRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kRounds; ++r) {
+    const uint32_t l = blockIdx.x * kTilePixels + r * kBlock + threadIdx.x;
+    int x = 0, y = 0;
+    const bool valid = l < f.P && local_pixel(f, l, x, y);
+    const bool culled = valid && pixel_frustum_misses(sv, f, x, y);
+    const unsigned long long b = __ballot(culled);
+    if ((lane & 31u) == 0u && l < f.P) mask[l >> 5] = (uint32_t)(b >> lane);
+    keep[r] = __ballot(valid && !culled);
+    if (lane == 0u) s_cnt[r * kWaves + wv] = (uint32_t)__popcll(keep[r]);
   }
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    uint32_t run = 0u;
+    for (uint32_t i = 0; i < kRounds * kWaves; ++i) {
+      const uint32_t c = s_cnt[i];
+      s_cnt[i] = run;
+      run += c;
+    }
+    s_base = run ? atomicAdd(&plist[f.P], run) : 0u;
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (uint32_t r = 0; r < kRounds; ++r)
+    if ((keep[r] >> lane) & 1ull)
+      plist[s_base + s_cnt[r * kWaves + wv] + (uint32_t)__popcll(keep[r] & below)] =
+          blockIdx.x * kTilePixels + r * kBlock + threadIdx.x;
+}
+// Path-major bounce 0 over the unculled pixel list (f.plist: nlist pixels x k samples): compacted
+// item i -> path p.  Items run in groups of kPrimaryGroup listed pixels — neighbours, since k_cull lists
+// each tile's unculled pixels in pixel order — times all k samples, sample-major inside a group.  The
+// k samples of a pixel take near-identical paths down the BVH (they differ by the sub-pixel jitter),
+// so a group's rays reuse one small set of nodes and primitives while it is in flight, on one XCD
+// (consecutive chunks go to consecutive logical blocks).  With the whole list as one group (sample
+// layer after sample layer over the frame) a scene larger than the MALL is streamed from HBM once per
+// sample.  The order changes no result: every path is traced and shaded independently and k_accum
+// sums in sample order.  SPTR_PRIMARY_GROUP=0: one group (the order before r03).
+#ifndef SPTR_PRIMARY_GROUP
+#define SPTR_PRIMARY_GROUP 64
+#endif
+__device__ __forceinline__ uint32_t primary_item(const FrameView& f, uint32_t nlist, uint32_t i) {
+  const uint32_t grp = SPTR_PRIMARY_GROUP ? (uint32_t)SPTR_PRIMARY_GROUP : nlist;
+  const uint32_t gk = grp * f.k;
+  const uint32_t g = i / gk, r = i - g * gk;
+  const uint32_t first = g * grp;
+  const uint32_t gs = min(grp, nlist - first);
+  const uint32_t smp = r / gs;
+  return smp * f.P + f.plist[first + (r - smp * gs)];
+}
+// Camera rays a bounce-0 trace kernel traverses: the k samples of every valid pixel that k_cull did
+// not cull (the culled ones are answered without a traversal).  Reported as traced_primary.
+__device__ __forceinline__ unsigned long long primary_traced(const FrameView& f) {
+  return (unsigned long long)(f.unculled ? *f.unculled : f.valid) * f.k;
 }
 __device__ __forceinline__ bool pixel_culled(const FrameView& f, uint32_t l) {
   return f.cull != nullptr && ((f.cull[l >> 5] >> (l & 31u)) & 1u) != 0u;
@@ -993,7 +1041,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<true>(sv, lds);
   __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+    w.tot[kTotTracedP] += primary_traced(f);
+  }
   const ImageDiv idiv = image_div(f);
   Visits vc;
   const Sched sd = block_sched(f.P);
@@ -1046,7 +1097,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   }
   seg_publish(w.segH, &s_cnt, per);
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotNodes);
+    flush_visits(vc, w.tot, kTotNodesP);
+  }
 }
 
 // Bounce 0, lane groups per pixel (f.pixel_major == kFoldWave: LDS-staged scenes in batches of >=
@@ -1070,7 +1124,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   if (threadIdx.x == 0) s_cnt = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
   __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
+    w.tot[kTotTracedP] += primary_traced(f);
+  }
   const ImageDiv idiv = image_div(f);
   Visits vc;
   constexpr uint32_t kPix = kBlock / kFoldLanes;  // pixels per block chunk
@@ -1132,7 +1189,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   }
   seg_publish(w.segH, &s_cnt, per);
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotNodes);
+    flush_visits(vc, w.tot, kTotNodesP);
+  }
 }
 // Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
 // (wf_pt_cpu.cpp:98-103) is added to rad[p] in place, so only hits go on to k_shade, as dense hit
@@ -1161,7 +1221,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   } else {
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += kPrimary ? primary_traced(f) : n;
+  }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
   Visits vc;
@@ -1176,10 +1239,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (kPrimary) {
         Primary pr;
         uint32_t l, p = i;
-        if (f.plist) {
-          const uint32_t smp = i / nlist;
-          p = smp * f.P + f.plist[i - smp * nlist];
-        }
+        if (f.plist) p = primary_item(f, nlist, i);
         id = pid = p;
         active = primary_path(f, idiv, p, pr, l);
         culled = !f.plist && pixel_culled(f, l);
@@ -1219,7 +1279,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   }
   seg_publish(w.segH, &s_cnt, sd.per);
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotNodes);
+    if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
+  }
 }
 
 // BVH2 (LDS-staged) or wide walk over the staged / global scene pointers
@@ -1285,7 +1348,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   } else {
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += kPrimary ? primary_traced(f) : n;
+  }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
   Visits vc;
@@ -1307,10 +1373,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (kPrimary) {
         Primary pr;
         uint32_t l, p = i;
-        if (f.plist) {
-          const uint32_t smp = i / nlist;
-          p = smp * f.P + f.plist[i - smp * nlist];
-        }
+        if (f.plist) p = primary_item(f, nlist, i);
         id = pid = p;
         valid = primary_path(f, idiv, p, pr, l);
         culled = !f.plist && pixel_culled(f, l);
@@ -1358,7 +1421,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   }
   seg_publish(w.segH, &s_cnt, sd.per);
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotNodes);
+    if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
+  }
 }
 
 // --------------------------------------------------------------------------------- shading steps
@@ -2939,7 +3005,7 @@ uint32_t cull_depth_for(uint32_t spp) { return spp >= 16u ? (uint32_t)kCullDepth
 
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s) {
   if (f.P == 0u) return;
-  hipLaunchKernelGGL(k_cull, dim3(f.P / kBlock), dim3(kBlock), 0, s, sv, f, mask, plist);
+  hipLaunchKernelGGL(k_cull, dim3(f.P / kTilePixels), dim3(kBlock), 0, s, sv, f, mask, plist);
 }
 
 unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,

@@ -202,6 +202,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.cull_depth = 4u;
   v.sky_fold = 0u;
   v.plist = nullptr;
+  v.unculled = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -225,9 +226,9 @@ ShadeView shade_view(const Context& c) {
 
 // Stage events on the render stream, kept in the context's pool until collected.  Stages: 0 whole
 // render call (always recorded), 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum +
-// resolve, 5 trace bounce 0 (raygen fused), 6 shade bounce 0, 7 tail; 1-7 only with
-// SPTR_FRAME_TIMING.
-constexpr int kStages = 8;
+// resolve, 5 trace bounce 0 (raygen fused), 6 shade bounce 0, 7 tail, 8 pixel cull; 1-8 only with
+// SPTR_FRAME_TIMING (1, 3, 5 and 8 also with SPTR_FRAME_TIMING_TRACE).
+constexpr int kStages = 9;
 struct StageTimer {
   Context& c;
   bool on;                  // SPTR_FRAME_TIMING or SPTR_FRAME_TIMING_TRACE
@@ -256,7 +257,7 @@ struct StageTimer {
     return i;
   }
   void begin(int stage) {
-    if (!on || (trace_only && stage != 1 && stage != 5)) return;
+    if (!on || (trace_only && stage != 1 && stage != 5 && stage != 3 && stage != 8)) return;
     open = c.marks.size();
     c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
@@ -278,20 +279,21 @@ int collect_pending(Context& c, sptr_stats* stats) {
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (c.pending == 0) return SPTR_OK;
   const hipError_t se = hipStreamSynchronize(c.pending_stream);
-  double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t trace_launches = 0;
+  double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t trace_launches = 0, shadow_launches = 0;
   for (const StageMark& m : c.marks) {
     float t = 0.0f;
     if (se == hipSuccess && m.b < c.events.size() && m.e < c.events.size())
       (void)hipEventElapsedTime(&t, c.events[m.b], c.events[m.e]);
     ms[m.stage] += t;
     if (m.stage == 1 || m.stage == 5) ++trace_launches;
+    if (m.stage == 3) ++shadow_launches;
   }
   c.marks.clear();
   c.events_used = 0;
-  const uint64_t samples = c.pending_samples, waves = c.pending_waves;
+  const uint64_t samples = c.pending_samples, waves = c.pending_waves, culls = c.pending_culls;
   c.pending = 0;
-  c.pending_samples = c.pending_waves = 0;
+  c.pending_samples = c.pending_waves = c.pending_culls = 0;
   if (se != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: ") + hipGetErrorString(se));
   unsigned long long tot[kTotWords];
   API_HIP(hipMemcpy(tot, c.w_tot.p, sizeof(tot), hipMemcpyDeviceToHost));
@@ -318,6 +320,14 @@ int collect_pending(Context& c, sptr_stats* stats) {
   stats->sphere_tests = tot[kTotSph];
   stats->shadow_node_visits = tot[kTotShNodes];
   stats->shadow_prim_tests = tot[kTotShPrims];
+  stats->traced_primary = tot[kTotTracedP];
+  stats->traced_bounce = tot[kTotTracedB];
+  stats->node_visits_primary = tot[kTotNodesP];
+  stats->tri_tests_primary = tot[kTotTrisP];
+  stats->sphere_tests_primary = tot[kTotSphP];
+  stats->ms_cull = ms[8];
+  stats->shadow_launches = shadow_launches;
+  stats->cull_launches = culls;
   return SPTR_OK;
 }
 
@@ -443,19 +453,12 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
 #else
   constexpr bool no_bounce = false;
 #endif
-  // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it)
+  // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it; made
+  // current by refresh_cull ahead of this launch sequence)
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
-    // the mask depends on the scene, the pixel layout (both covered by the epoch) and the camera
     fv.cull_depth = cull_depth_for(f.spp);
-    if (c.cull_epoch != c.epoch || c.cull_depth != fv.cull_depth ||
-        std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) != 0) {
-      API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 4, s));
-      launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
-      c.cull_epoch = c.epoch;
-      c.cull_cam = f.camera;
-      c.cull_depth = fv.cull_depth;
-    }
     fv.cull = static_cast<const uint32_t*>(c.cull.p);
+    fv.unculled = static_cast<const uint32_t*>(c.plist.p) + c.P;
   }
   tm.begin_call();
   uint32_t done = 0, waves = 0;
@@ -525,6 +528,34 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   }
   tm.end_call();
   return waves;
+}
+
+// The bounce-0 pixel-frustum cull mask (and unculled-pixel list) of a wavefront call's camera.  It is
+// launched directly on the render stream ahead of the call's launch sequence, never inside it: a
+// captured launch graph therefore holds no k_cull, and whichever camera a replayed graph was
+// captured for, it runs against the mask of the camera of its own call (a graph key includes the
+// camera; the mask is recomputed here whenever the camera, the cull depth or the state epoch differ
+// from the cached mask's, and on SPTR_FRAME_RECULL).
+int refresh_cull(Context& c, const sptr_frame& f, hipStream_t s, bool timing) {
+  if (f.flags & SPTR_FRAME_NO_CULL) return SPTR_OK;
+  const uint32_t depth = cull_depth_for(f.spp);
+  if (!(f.flags & SPTR_FRAME_RECULL) && c.cull_epoch == c.epoch && c.cull_depth == depth &&
+      std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) == 0)
+    return SPTR_OK;
+  FrameView fv = frame_view(c, f);
+  fv.cull_depth = depth;
+  StageTimer tm{c, timing, true, s};
+  tm.begin(8);
+  API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 4, s));
+  launch_cull(scene_view(c), fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
+  tm.end();
+  API_HIP(hipGetLastError());
+  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: cull events: ") + hipGetErrorString(tm.err));
+  c.cull_epoch = c.epoch;
+  c.cull_cam = f.camera;
+  c.cull_depth = depth;
+  ++c.pending_culls;
+  return SPTR_OK;
 }
 
 bool same_key(const GraphKey& a, const GraphKey& b) { return std::memcmp(&a, &b, sizeof(GraphKey)) == 0; }
@@ -971,6 +1002,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     key.k = k;
     key.tail = (uint32_t)T;
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
+    rc = refresh_cull(c, *f, s, timing || trace_timing);
+    if (rc != SPTR_OK) return rc;
     rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, timing || trace_timing, !timing, s,
                   [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;

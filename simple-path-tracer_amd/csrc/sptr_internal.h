@@ -158,6 +158,7 @@ struct FrameView {
   uint32_t sky_fold;     // path-major bounce 0 with a cull mask: k_sky sums culled pixels into accum
   uint32_t cull_depth;   // BVH2 levels k_cull tests (<= kCullDepthMax)
   const uint32_t* plist; // with sky_fold: the unculled local pixels (count at plist[P]), bounce 0's paths
+  const uint32_t* unculled;  // with cull: the number of unculled valid local pixels (k_cull's plist[P])
 };
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
@@ -176,7 +177,10 @@ enum : int {
   kTotShNodes, kTotShPrims,      // k_shadow visit counts
   kTotOverflow,
   kTotTail,         // closest-hit queries traced by k_tail
-  kTotStackOverflow,  // a traversal push was dropped (cannot happen within the build's stack bound)         // closest-hit queries traced by k_tail
+  kTotStackOverflow,  // a traversal push was dropped (cannot happen within the build's stack bound)
+  kTotTracedP,      // bounce-0 camera rays the trace kernels traversed (unculled pixel samples)
+  kTotTracedB,      // queued rays of bounces >= 1 traversed by k_trace / k_trace_dyn
+  kTotNodesP, kTotTrisP, kTotSphP,  // bounce-0 part of kTotNodes / kTotTris / kTotSph
   kTotWords
 };
 
@@ -303,7 +307,7 @@ struct Context {
   size_t events_used = 0;
   uint32_t pending = 0;                         // render calls since the last collection
   hipStream_t pending_stream = nullptr;
-  uint64_t pending_samples = 0, pending_waves = 0;
+  uint64_t pending_samples = 0, pending_waves = 0, pending_culls = 0;
 };
 
 // kernels_lbvh.hip

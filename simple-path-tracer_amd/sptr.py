@@ -24,6 +24,7 @@ SPTR_FRAME_COUNT_VISITS = 4
 SPTR_FRAME_ASYNC = 8
 SPTR_FRAME_TIMING_TRACE = 16
 SPTR_FRAME_NO_CULL = 32
+SPTR_FRAME_RECULL = 64
 
 SPTR_INTEGRATOR_WAVEFRONT = 0   # WavefrontPathTracerCPU semantics (default)
 SPTR_INTEGRATOR_PATHTRACER = 1  # PathTracer (the reference's default CPU integrator) semantics
@@ -81,7 +82,10 @@ class Stats(C.Structure):
                 ("ms_accum", C.c_double), ("trace_launches", C.c_uint64), ("node_visits", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("shadow_node_visits", C.c_uint64),
                 ("shadow_prim_tests", C.c_uint64), ("ms_trace0", C.c_double), ("ms_shade0", C.c_double),
-                ("rays_tail", C.c_uint64), ("ms_tail", C.c_double)]
+                ("rays_tail", C.c_uint64), ("ms_tail", C.c_double), ("traced_primary", C.c_uint64),
+                ("traced_bounce", C.c_uint64), ("node_visits_primary", C.c_uint64),
+                ("tri_tests_primary", C.c_uint64), ("sphere_tests_primary", C.c_uint64), ("ms_cull", C.c_double),
+                ("cull_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

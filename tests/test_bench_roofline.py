@@ -1,0 +1,78 @@
+"""CPU: bench.py's roofline model.  Every per-launch figure must be a ratio of sums over
+the same timed launches, so the reported fraction cannot depend on how many steps were timed, and
+only the rays the trace launches traversed (not the culled camera rays) are charged."""
+import importlib.util
+import os
+from types import SimpleNamespace
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _step_stats(steps, launches_per_step=6, ms_per_launch=0.3, tp=10_000_000, tb=28_000_000, shadow=12_000_000):
+    """The summed stats of `steps` identical timed steps."""
+    return SimpleNamespace(trace_launches=launches_per_step * steps, ms_trace=ms_per_launch * launches_per_step * steps,
+                           traced_primary=tp * steps, traced_bounce=tb * steps, rays_shadow=shadow * steps,
+                           shadow_launches=6 * steps, ms_shadow=0.8 * 6 * steps)
+
+
+CNT = SimpleNamespace(traced_primary=10_000_000, traced_bounce=28_000_000, node_visits=90_000_000,
+                      tri_tests=40_000_000, sphere_tests=5_000_000, node_visits_primary=30_000_000,
+                      tri_tests_primary=12_000_000, sphere_tests_primary=1_000_000, rays_shadow=12_000_000,
+                      shadow_node_visits=50_000_000, shadow_prim_tests=9_000_000)
+HBM = {"node_bytes": 64 * 1000, "num_nodes": 1000, "tri_bytes": 480_000_000, "sphere_bytes": 16 * 8,
+       "prim_ref_bytes": 40_000_000, "lds_bytes": 0}
+LDS = dict(HBM, tri_bytes=48 * 12, prim_ref_bytes=80, node_bytes=64 * 20, num_nodes=20, lds_bytes=2084)
+
+
+@pytest.mark.parametrize("layout", [HBM, LDS], ids=["hbm", "lds"])
+def test_frac_independent_of_timed_steps(bench, layout):
+    a = bench.roofline(CNT, [_step_stats(1)], layout, "no_such_workload", 1)
+    b = bench.roofline(CNT, [_step_stats(20)], layout, "no_such_workload", 20)
+    for k in ("frac", "frac_s8d", "bytes_per_launch", "avg_launch_us", "launches_per_step", "traversed_rays_per_launch"):
+        assert a[k] == pytest.approx(b[k], rel=1e-9), k
+    sa = bench.shadow_roofline(CNT, [_step_stats(1)], layout, "no_such_workload", 1)
+    sb = bench.shadow_roofline(CNT, [_step_stats(20)], layout, "no_such_workload", 20)
+    assert sa["frac"] == pytest.approx(sb["frac"], rel=1e-9)
+
+
+def test_bytes_follow_s8d(bench):
+    """hbm residency: every visit charged, camera rays 8 B, later rays 36 B."""
+    r = bench.roofline(CNT, [_step_stats(3)], HBM, "no_such_workload", 3)
+    tp, tb = CNT.traced_primary, CNT.traced_bounce
+    scene = 64.0 * CNT.node_visits + 48.0 * CNT.tri_tests + 16.0 * CNT.sphere_tests
+    per_launch = (8.0 * tp + 36.0 * tb + scene) / 6
+    assert r["bytes_per_launch"] == pytest.approx(per_launch, rel=1e-6)
+    assert r["frac"] == pytest.approx(per_launch / 0.3e-3 / 1e9 / 8000.0, rel=1e-3)
+    s8d = (36.0 * (tp + tb) + scene) / 6
+    assert r["frac_s8d"] == pytest.approx(s8d / 0.3e-3 / 1e9 / 8000.0, rel=1e-3)
+    assert r["per_ray"]["primary"]["nodes"] == pytest.approx(3.0)
+    assert r["per_ray"]["bounce"]["nodes"] == pytest.approx(60.0 / 28.0, rel=1e-3)
+
+
+def test_culled_rays_not_charged(bench):
+    """Fewer traversed camera rays (more culling) at the same launch time: fewer bytes, lower frac."""
+    a = bench.roofline(CNT, [_step_stats(2)], HBM, "no_such_workload", 2)
+    b = bench.roofline(CNT, [_step_stats(2, tp=5_000_000)], HBM, "no_such_workload", 2)
+    assert b["bytes_per_launch"] < a["bytes_per_launch"]
+
+
+def test_lds_scene_charges_stream_only(bench):
+    r = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1)
+    assert r["scene_residency"] == "lds"
+    assert r["bytes_per_launch"] == pytest.approx((8.0 * CNT.traced_primary + 36.0 * CNT.traced_bounce) / 6, rel=1e-6)
+
+
+def test_no_shadow_launches_no_entry(bench):
+    st = _step_stats(1)
+    st.shadow_launches = 0
+    assert bench.shadow_roofline(CNT, [st], HBM, "no_such_workload", 1) is None

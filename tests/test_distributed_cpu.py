@@ -89,6 +89,9 @@ def test_bench_gpus_2_launches_two_ranks():
     assert rc == 0, err[-3000:]
     assert line["dry_run"] and line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
     assert line["gather_ok"] and line["pixels_covered"] == 256 * 256
+    # the per-step split of the GPU line: render and gather timed apart, and the bytes gathered
+    assert line["render_ms"] >= 0.0 and line["gather_ms"] > 0.0
+    assert line["gather_bytes"] == 2 * line["tiles_per_rank"] * 4096
 
 
 def test_bench_gpus_1_stays_single_rank():

@@ -466,3 +466,51 @@ def test_pixel_cull_invisible(renderer, scene, p0, p1, spp, W, H):
     c1 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS)
     c0 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS | sptr.SPTR_FRAME_NO_CULL)
     assert c1.node_visits < c0.node_visits
+
+
+@pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])
+def test_graph_replay_after_camera_switch(renderer, scene, p0, p1):
+    """A launch graph captured for camera A must run against A's pixel-cull mask when it is replayed
+    after a call with camera B recomputed the mask (calls A, A [captured], B, A [replayed], A): each
+    call's image equals the direct-launch image of its camera, in the thread-per-pixel (LDS scene) and
+    the path-major cull-list (BVH4 scene) bounce-0 kernels."""
+    W, H = 96, 64
+    sptr.setup_default(renderer, scene, p0, p1)
+    cams = {"A": sptr.camera_lookat(aspect=W / H),
+            "B": sptr.camera_lookat(pos=(4.0, 2.0, 6.0), target=(-1.0, 1.0, 0.0), aspect=W / H)}
+    out = {}
+    try:
+        for mode in (1, 0):
+            renderer.set_launch_mode(mode)
+            out[mode] = []
+            for name in "AABAA":
+                st = renderer.render(cams[name], W, H, spp=16, frame_begin=1)
+                out[mode].append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, st.traced_primary))
+    finally:
+        renderer.set_launch_mode(0)
+    assert not np.array_equal(out[1][0][0], out[1][2][0])  # the two cameras see different images
+    for a, b in zip(out[1], out[0]):
+        assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+        assert a[1:] == b[1:]
+
+
+def test_traced_ray_counts(renderer):
+    """traced_primary counts the camera rays bounce 0 actually traverses (culled pixels' samples are
+    answered without a traversal), traced_bounce the queued rays of the later trace launches; with the
+    path-per-thread tail off and no fused bounce (BVH4 scene), every closest-hit query is one of them
+    or a culled camera ray."""
+    W, H, spp = 96, 64, 4
+    cam = sptr.camera_lookat(aspect=W / H)
+    sptr.setup_default(renderer, "sphere_mesh", 60, 120)
+    try:
+        renderer.set_tail_depth(32)
+        st0 = renderer.render(cam, W, H, spp=spp, flags=sptr.SPTR_FRAME_NO_CULL)
+        st = renderer.render(cam, W, H, spp=spp, flags=sptr.SPTR_FRAME_RECULL)
+    finally:
+        renderer.set_tail_depth(0)
+    assert st0.traced_primary == st0.samples == W * H * spp
+    assert 0 < st.traced_primary < st.samples and st.traced_primary % spp == 0
+    assert st.cull_launches == 1 and st0.cull_launches == 0
+    assert st.traced_bounce == st0.traced_bounce > 0
+    assert st0.rays_closest == st0.traced_primary + st0.traced_bounce
+    assert st.rays_closest == st0.rays_closest

@@ -27,13 +27,19 @@ def short(n):
     return n.split("(")[0][:48]
 
 
+# position of the visit-count flag C among each kernel's template arguments
+_COUNT_ARG = {"k_trace": 1, "k_trace_dyn": 1, "k_trace_wp": 1, "k_trace_pm": 0, "k_shadow": 1, "k_shadow_dyn": 0}
+
+
 def _is_count_variant(name):
-    """k_trace<L, C, P, W> / k_shadow<L, C, W>: the instrumented (C = true) visit-count instantiation
-    runs only in bench.py's untimed counting pass and is left out of the per-launch means."""
+    """The instrumented (C = true) visit-count instantiation of a trace / shadow kernel runs only in
+    bench.py's untimed counting pass and is left out of the per-launch means."""
     if "<" not in name:
         return False
+    base = name.replace("sptr::", "").split("<", 1)[0].split()[-1]
+    pos = _COUNT_ARG.get(base)
     args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
-    return len(args) >= 3 and args[1] == "true"
+    return pos is not None and len(args) > pos and args[pos] == "true"
 
 
 def emit(dirs, kernel, out_path, workload):
