@@ -86,16 +86,24 @@ def _residency(layout):
     return res, footprint
 
 
-def _counter_fracs(wl_name, kernel, avg_launch_s):
-    """counter_frac = FETCH_SIZE x2 + WRITE_SIZE per launch (the newest profiles/r*_pmc_<wl>_<kernel>.json)
-    over the live launch time; valu_issue_frac = SQ_INSTS_VALU per launch (profiles/r*_sq_<wl>_<kernel>.json)
-    over the live launch time and the 1.23e12/s issue peak; salu_per_valu from the same SQ pass."""
+def _counter_fracs(wl_name, kernel, avg_launch_s, stream_read_per_launch):
+    """counter_frac = HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (the newest
+    profiles/r*_pmc_<wl>_<kernel>.json) over the live launch time, with FETCH_SIZE calibrated per access
+    shape (tools/micro/gather_cal.hip, profiles/r03b_fetch_calibration.json): a coalesced 16-B-per-lane
+    stream is counted at half its bytes, a random 48/64-B gather (BVH nodes, triangles) at its bytes.  So
+    traffic = FETCH_SIZE + (the launch's coalesced stream reads, from the model) / 2 + WRITE_SIZE;
+    traffic_x2 (FETCH_SIZE doubled, the stream-only calibration of MI355X_MICROARCH.md) beside it.
+    valu_issue_frac = SQ_INSTS_VALU per launch (profiles/r*_sq_<wl>_<kernel>.json) over the live launch
+    time and the 1.23e12/s issue peak; salu_per_valu from the same SQ pass."""
     pmc, pmc_src = _latest_profile(f"r*_pmc_{wl_name}_{kernel}.json")
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic_x2 = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic = None
+    if pmc and pmc.get("fetch_bytes_per_launch_x2") is not None:
+        traffic = pmc["fetch_bytes_per_launch_x2"] / 2.0 + stream_read_per_launch / 2.0 + pmc["write_bytes_per_launch"]
     sq, sq_src = _latest_profile(f"r*_sq_{wl_name}_{kernel}.json")
     valu = sq.get("valu_per_launch") if sq else None
     salu = sq.get("counters_per_launch", {}).get("SQ_INSTS_SALU") if sq else None
-    return {"traffic": traffic, "traffic_source": pmc_src,
+    return {"traffic": traffic, "traffic_x2": traffic_x2, "traffic_source": pmc_src,
             "counter_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_launch_s else None,
             "valu_issue_frac": round(valu / avg_launch_s / VALU_PEAK_WAVE_INSTR_PER_S, 4) if valu and avg_launch_s else None,
             "salu_per_valu": round(salu / valu, 3) if salu and valu else None, "valu_source": sq_src}
@@ -142,7 +150,7 @@ def roofline(cnt, stats, layout, wl_name, steps):
            + 48.0 * (pp[1] * tp + pb[1] * tb) + 16.0 * (pp[2] * tp + pb[2] * tb)) / max(1, launches)
     out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    out.update(_counter_fracs(wl_name, "trace", avg_launch_s))
+    out.update(_counter_fracs(wl_name, "trace", avg_launch_s, STREAM_READ_BYTES * tb / max(1, launches)))
     out.update({
         "frac_s8d": round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None,
         "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
@@ -151,6 +159,14 @@ def roofline(cnt, stats, layout, wl_name, steps):
         "scene_in_lds": residency == "lds", "scene_residency": residency, "scene_bytes": int(footprint),
         "per_ray": {"primary": {"nodes": round(pp[0], 3), "tris": round(pp[1], 3), "spheres": round(pp[2], 3)},
                     "bounce": {"nodes": round(pb[0], 3), "tris": round(pb[1], 3), "spheres": round(pb[2], 3)}}})
+    # the instrumented step, per bounce: traversed rays and node visits per ray; per-ray visit histogram
+    # (bin b: 2^(b-1) <= visits < 2^b)
+    tbd, nbd = list(getattr(cnt, "traced_by_depth", [])), list(getattr(cnt, "nodes_by_depth", []))
+    out["by_bounce"] = [{"bounce": d, "rays": int(tbd[d]), "nodes_per_ray": round(nbd[d] / tbd[d], 3)}
+                        for d in range(len(tbd)) if tbd[d]]
+    hist = list(getattr(cnt, "trace_visit_hist", []))
+    if any(hist):
+        out["visit_hist_log2"] = [int(x) for x in hist]
     fr = {"hbm_model": out["frac"], "hbm_counters": out["counter_frac"], "valu_issue": out["valu_issue_frac"]}
     known = {k: v for k, v in fr.items() if v is not None}
     out["binding"] = max(known, key=known.get) if known else None
@@ -182,11 +198,14 @@ def shadow_roofline(cnt, stats, layout, wl_name, steps):
     achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     out = {"bound": "hbm", "kernel": "k_shadow", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    out.update(_counter_fracs(wl_name, "shadow", avg_launch_s))
+    out.update(_counter_fracs(wl_name, "shadow", avg_launch_s, 32.0 * tasks / launches))
     out.update({"bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
                 "launches_per_step": round(launches / max(1, steps), 3), "tasks_per_launch": round(tasks / launches),
                 "per_task": {"nodes": round(n_node, 3), "tris": round(n_tri, 3)}, "scene_residency": residency,
                 "ms_per_step": round(sum(s.ms_shadow for s in stats) / max(1, steps), 3)})
+    hist = list(getattr(cnt, "shadow_visit_hist", []))
+    if any(hist):
+        out["visit_hist_log2"] = [int(x) for x in hist]
     return out
 
 

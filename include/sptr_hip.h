@@ -185,6 +185,14 @@ typedef struct sptr_stats {
   double ms_cull;              /* SPTR_FRAME_TIMING / _TIMING_TRACE: the pixel-cull launches (k_cull) */
   uint64_t cull_launches;      /* calls whose cull mask was (re)computed */
   uint64_t shadow_launches;    /* SPTR_FRAME_TIMING / _TIMING_TRACE: shadow-stage launches (ms_shadow) */
+  /* Per bounce d (index 7: bounces >= 7): rays the wavefront trace kernels traversed (every call) and
+   * their BVH node visits (SPTR_FRAME_COUNT_VISITS).  Histograms (SPTR_FRAME_COUNT_VISITS): closest-hit
+   * rays of the trace kernels / any-hit queries of the shadow stage by node visits, bin b counting the
+   * rays with 2^(b-1) <= visits < 2^b (bin 0: no visit, bin 15: >= 2^14). */
+  uint64_t traced_by_depth[8];
+  uint64_t nodes_by_depth[8];
+  uint64_t trace_visit_hist[16];
+  uint64_t shadow_visit_hist[16];
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */
@@ -201,7 +209,7 @@ int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
  * 2^25 paths (e.g. the per-rank share of a sharded 1080p frame), none for larger batches;
  * >= max_depth = none.  The image and the query counts do not depend on it. */
 int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
-/* Maximum primitives per BVH leaf range (1..32; 0 = automatic, the default: 8 for scenes staged in
+/* Maximum primitives per BVH leaf range (1..16; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 1 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,

@@ -31,6 +31,9 @@
 #ifndef SPTR_GREEDY_WEIGHT
 #define SPTR_GREEDY_WEIGHT 0  // 1: the greedy collapse opens the child of largest area x primitives
 #endif
+#ifndef SPTR_WIDE_DIRECT
+#define SPTR_WIDE_DIRECT 1  // wide single-primitive leaves as direct links (0: prim_ref ranges, A/B builds)
+#endif
 #ifndef SPTR_WIDE_GREEDY
 #define SPTR_WIDE_GREEDY 1  // 0: every kWideLevels-th LBVH level becomes a wide level (A/B builds)
 #endif
@@ -517,8 +520,10 @@ __global__ void k_wide_count(uint32_t ncur, const uint2* cur, const BvhNode* nod
 }
 // pass 2: wide node base + j; its m-th internal child becomes next[off[j] + m] = wide node
 // base + ncur + off[j] + m of the next level
+// Single-primitive leaf children become direct links (the primitive's ref in the link: its test
+// needs no prim_ref load) when `direct` (SPTR_WIDE_DIRECT).
 __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, const BvhNode* nodes, const uint32_t* off,
-                            uint2* next, WideNode* out) {
+                            uint2* next, WideNode* out, const uint32_t* prim_ref, uint32_t direct) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ncur; j += gridDim.x * blockDim.x) {
     WideBoxes b;
     const int n = expand_greedy(nodes, cur[j].x, b);
@@ -528,6 +533,10 @@ __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, cons
         next[m] = make_uint2(b.link[e], base + j);
         b.link[e] = base + ncur + m;
         ++m;
+      } else if (direct && (b.link[e] & kLeafRangeMask) == 0u) {
+        const uint32_t ref = prim_ref[(b.link[e] & ~kLeafBit) >> kLeafCountBits];
+        b.link[e] = kLeafBit | ((ref & kIndexMask) << kLeafCountBits) | kLeafDirect |
+                    ((ref & kSphereBit) ? kLeafDirectSphere : 0u);
       }
     out[base + j] = quantize_wide(b, n, cur[j].y);
   }
@@ -667,15 +676,17 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   } else {
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
-    LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
-    hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
-                       leaf_parent);
-    hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, kids, leaf_parent,
-                       nodes, rflags, dmax);
-    LB_CHECK(hipGetLastError());
     uint32_t dep = 0;
-    LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
-    LB_CHECK(hipStreamSynchronize(s));
+    {
+      LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
+      hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
+                         leaf_parent);
+      hipLaunchKernelGGL(k_refit, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, vals_s, blo, bhi, kids, leaf_parent,
+                         nodes, rflags, dmax);
+      LB_CHECK(hipGetLastError());
+      LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
+      LB_CHECK(hipStreamSynchronize(s));
+    }
     c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;
     // a BVH2 node at depth d holds at most d pushed entries and pushes one more; a wide node (BVH2
@@ -714,7 +725,8 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
         LB_CHECK(hipGetLastError());
         LB_CHECK(rocprim::exclusive_scan(stw, sw, flag, off, 0u, ncur, rocprim::plus<uint32_t>(), s));
         hipLaunchKernelGGL(k_wide_emit, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, base, nodes, off, nxt,
-                           static_cast<WideNode*>(c.nodes4.p));
+                           static_cast<WideNode*>(c.nodes4.p), static_cast<const uint32_t*>(c.prim_ref.p),
+                           (uint32_t)SPTR_WIDE_DIRECT);
         LB_CHECK(hipGetLastError());
         uint32_t last[2] = {0u, 0u};  // cnt, off of the level's last node
         LB_CHECK(hipMemcpyAsync(&last[0], flag + (ncur - 1u), 4, hipMemcpyDeviceToHost, s));

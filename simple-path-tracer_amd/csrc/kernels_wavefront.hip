@@ -58,6 +58,15 @@
 #ifndef SPTR_TOP_LDS
 #define SPTR_TOP_LDS 1  // wide-BVH top levels staged in LDS by the refilling kernels (0: A/B builds)
 #endif
+#ifndef SPTR_ANYHIT_FAR
+#define SPTR_ANYHIT_FAR 1  // any-hit wide walks visit the farthest hit child first: a ray leaving a surface has
+                           // no occluder among the boxes around its origin, so the near-first order explores
+                           // them before the far occluder (r03b A/B: C5 shadow 4.42 -> 3.88 ms/step, C3
+                           // 0.81 -> 0.80); 0: nearest first
+#endif
+#ifndef SPTR_ANYHIT_FAR2
+#define SPTR_ANYHIT_FAR2 0  // 1: any-hit BVH2 walks (LDS scenes) visit the farther child first (A/B builds)
+#endif
 #ifndef SPTR_SHADOW4_WAVES
 #define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
@@ -308,8 +317,7 @@ __device__ __forceinline__ float xorsign(float x, float s) {
 
 // Embree default Moeller-Trumbore (restated; see oracle/wf_oracle.cpp tri_hit): accepts
 // tnear*|den| < T <= tfar*|den|.  Triangle record: v0, e1 = v0-v1, e2 = v2-v0, Ng = cross(e2,e1).
-__device__ __forceinline__ bool tri_hit(const float4* tris, uint32_t i, const Ray& r, float tnear, float tfar, float& t) {
-  const float4 a = tris[3 * i + 0], b = tris[3 * i + 1], c = tris[3 * i + 2];
+__device__ __forceinline__ bool tri_hit4(float4 a, float4 b, float4 c, const Ray& r, float tnear, float tfar, float& t) {
   const vec3 v0 = v3(a.x, a.y, a.z), e1 = v3(a.w, b.x, b.y), e2 = v3(b.z, b.w, c.x), ng = v3(c.y, c.z, c.w);
   const vec3 C = v0 - r.o;
   const vec3 R = e_cross(C, r.d);
@@ -322,6 +330,9 @@ __device__ __forceinline__ bool tri_hit(const float4* tris, uint32_t i, const Ra
   if (!(aden * tnear < T && T <= aden * tfar)) return false;
   t = T / aden;
   return true;
+}
+__device__ __forceinline__ bool tri_hit(const float4* tris, uint32_t i, const Ray& r, float tnear, float tfar, float& t) {
+  return tri_hit4(tris[3 * i + 0], tris[3 * i + 1], tris[3 * i + 2], r, tnear, tfar, t);
 }
 
 // EmbreeBackend.cpp:223-314 sphere callbacks, same evaluation order.
@@ -360,15 +371,17 @@ struct Visits {
 };
 
 // Leaf = contiguous range of sorted primitive references (LBVH subtrees cover contiguous ranges):
-// every primitive of the range is tested in a uniform loop.  Closest: updates tfar/ref.  Any-hit:
-// returns on the first occluder.
-template <bool kAny, bool kCount>
+// every primitive of the range is tested in a uniform loop; or, with kDirect (links read from wide
+// nodes), possibly one primitive named by the link itself (kLeafDirect: one dependent load less per
+// leaf).  Closest: updates tfar/ref.  Any-hit: returns on the first occluder.
+template <bool kAny, bool kCount, bool kDirect = false>
 __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_ref, const float4* tris, const float4* sph,
                                           const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc) {
-  const uint32_t start = (link & ~kLeafBit) >> kLeafCountBits, cnt = (link & kLeafCountMask) + 1u;
+  const bool direct = kDirect && (link & kLeafDirect) != 0u;
+  const uint32_t start = (link & ~kLeafBit) >> kLeafCountBits, cnt = direct ? 1u : (link & kLeafRangeMask) + 1u;
   bool hit = false;
   for (uint32_t j = 0; j < cnt; ++j) {
-    const uint32_t pr = prim_ref[start + j];
+    const uint32_t pr = direct ? (start | ((link & kLeafDirectSphere) ? kSphereBit : 0u)) : prim_ref[start + j];
     const uint32_t idx = pr & kIndexMask;
     float t;
     if (pr & kSphereBit) {
@@ -464,7 +477,7 @@ __device__ __forceinline__ bool bvh2_walk(uint32_t& cur, int& sp, bool& hit, Tra
       hr = false;
     }
     if (hl && hr) {
-      if (tr < tl) {
+      if ((kAny && SPTR_ANYHIT_FAR2) ? tl < tr : tr < tl) {
         const uint32_t s = L;
         L = R;
         R = s;
@@ -598,22 +611,28 @@ __device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, con
     bool hc[kWide];
 #pragma unroll
     for (int k = 0; k < kWide; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) && ln[k] != kNoHit;
+    // Hit leaf children, in slot order (a direct link's primitive needs no prim_ref load).  r03 A/B:
+    // fetching the direct leaves of a node two or four at a time before testing them (one memory
+    // latency per batch) spilled at 7 waves/SIMD and read 48 B of the node itself for every non-leaf
+    // child slot of the batch: C5 11.7 -> 21.0 / 33.5 ms per step.
 #pragma unroll
     for (int k = 0; k < kWide; ++k) {
       if (hc[k] && (ln[k] & kLeafBit)) {
-        if (leaf_test<kAny, kCount>(ln[k], prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
+        if (leaf_test<kAny, kCount, true>(ln[k], prim_ref, tris, sph, r, tnear, tfar, ref, vc)) {
           wk.hit = true;
           if (kAny) return true;
         }
         hc[k] = false;
       }
     }
+    // next node: the nearest hit internal child; any-hit walks with SPTR_ANYHIT_FAR take the farthest
     int kn = kWide;
     float tn = __builtin_huge_valf();
     uint32_t npush = 0u;
 #pragma unroll
     for (int k = 0; k < kWide; ++k) {
-      if (hc[k] && (kn == kWide || t[k] < tn)) {
+      const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
+      if (hc[k] && (kn == kWide || better)) {
         tn = t[k];
         kn = k;
       }
@@ -714,6 +733,18 @@ __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv
   return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
 }
 
+// Per-bounce and per-ray statistics (sptr_stats traced_by_depth / nodes_by_depth / *_visit_hist).
+__device__ __forceinline__ uint32_t stat_depth(int depth) { return depth < kStatDepths - 1 ? (uint32_t)depth : kStatDepths - 1u; }
+__device__ __forceinline__ void hist_ray(unsigned long long* tot, int base, uint32_t visits) {
+  const uint32_t b = visits ? (uint32_t)(32 - __clz(visits)) : 0u;
+  atomicAdd(&tot[base + (b < (uint32_t)kHistBins ? b : kHistBins - 1u)], 1ull);
+}
+__device__ __forceinline__ void flush_depth_nodes(const Visits& vc, unsigned long long* tot, int depth) {
+  unsigned long long a = vc.nodes;
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+  if (lane_id() == 0) atomicAdd(&tot[kTotNodesD + stat_depth(depth)], a);
+}
+
 // Sticky stack-overflow report (one store per wave that saw a dropped push).
 __device__ __forceinline__ void report_stack(const Visits& vc, unsigned long long* tot) {
   if (__ballot(vc.stack_overflow != 0u) && lane_id() == 0u) tot[kTotStackOverflow] = 1ull;
@@ -803,10 +834,13 @@ __device__ __forceinline__ bool box_outside(const Box& b, const vec3 n[4], vec3 
   }
   return false;
 }
-__device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const FrameView& f, int x, int y) {
+// The pyramid of the pixel rectangle [x, x + npx) x [y, y + npx) (k_cull tests 2x2 pixel quads: a quad
+// whose pyramid misses every box culls its four pixels, a subset of what per-pixel pyramids would
+// cull, at a quarter of the tests).
+__device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const FrameView& f, int x, int y, int npx = 1) {
   if (sv.num_nodes == 0u || (sv.root & kLeafBit)) return false;
-  const float u0 = (float(x) - kCullMarginPx) / float(f.W), u1 = (float(x) + 1.0f + kCullMarginPx) / float(f.W);
-  const float v0 = (float(y) - kCullMarginPx) / float(f.H), v1 = (float(y) + 1.0f + kCullMarginPx) / float(f.H);
+  const float u0 = (float(x) - kCullMarginPx) / float(f.W), u1 = (float(x + npx) + kCullMarginPx) / float(f.W);
+  const float v0 = (float(y) - kCullMarginPx) / float(f.H), v1 = (float(y + npx) + kCullMarginPx) / float(f.H);
   auto dir = [&](float u, float v) {
     return f.cam_f + ((u - 0.5f) * 2.0f * f.half_w) * f.cam_r + (-(v - 0.5f) * 2.0f * f.half_h) * f.cam_u;
   };
@@ -840,33 +874,66 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   }
   return true;
 }
-// bit l of mask: pixel l is culled (see above); one ballot word pair per wave.
-// plist: the valid pixels that are not culled (count at plist[P], zeroed before).  One block per local
-// tile (four 256-pixel rounds): the tile's unculled pixels are listed in pixel order at a range that
-// one atomic per tile reserves.  (One atomic per wave on the single count word serialised 32 K waves at
-// one L2 channel: C2 k_cull 108 us.)
+// bit l of mask: pixel l is culled (see above).  plist: the valid pixels that are not culled (count at
+// plist[P], zeroed before).  One block per local tile: thread (qx, qy) tests the 2x2 pixel quad at
+// (2qx, 2qy) of the tile and sets the quad's bits in the tile's 32 LDS row words; then each thread
+// lists the unculled valid pixels of 4 consecutive local indices, the tile's list in pixel order at a
+// range one atomic per tile reserves.  (r02: a pyramid per pixel and one atomic per wave, C2 108 us;
+// per pixel and per tile 65-75 us.)
 __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
-  constexpr uint32_t kRounds = kTilePixels / kBlock;
-  constexpr uint32_t kWaves = kBlock / 64u;
-  __shared__ uint32_t s_cnt[kRounds * kWaves];
+  static_assert(kTile == 32 && kBlock == 256, "16 x 16 quads per 32 x 32 tile");
+  __shared__ uint32_t s_row[kTile];
+  __shared__ uint32_t s_cnt[kBlock / 64u];
   __shared__ uint32_t s_base;
-  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  unsigned long long keep[kRounds];
-#pragma unroll
-  for (uint32_t r = 0; r < kRounds; ++r) {
-    const uint32_t l = blockIdx.x * kTilePixels + r * kBlock + threadIdx.x;
+  const uint32_t t0 = blockIdx.x * kTilePixels;  // the tile's first local pixel
+  if (threadIdx.x < (uint32_t)kTile) s_row[threadIdx.x] = 0u;
+  __syncthreads();
+  {
+    const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
     int x = 0, y = 0;
-    const bool valid = l < f.P && local_pixel(f, l, x, y);
-    const bool culled = valid && pixel_frustum_misses(sv, f, x, y);
-    const unsigned long long b = __ballot(culled);
-    if ((lane & 31u) == 0u && l < f.P) mask[l >> 5] = (uint32_t)(b >> lane);
-    keep[r] = __ballot(valid && !culled);
-    if (lane == 0u) s_cnt[r * kWaves + wv] = (uint32_t)__popcll(keep[r]);
+    (void)local_pixel(f, t0 + 2u * qy * kTile + 2u * qx, x, y);  // the quad's corner (in or out of the image)
+    if (x < f.W && y < f.H && pixel_frustum_misses(sv, f, x, y, 2)) {
+      atomicOr(&s_row[2u * qy], 3u << (2u * qx));
+      atomicOr(&s_row[2u * qy + 1u], 3u << (2u * qx));
+    }
   }
+  __syncthreads();
+  // four consecutive local pixels per thread: l = t0 + 4 * tid + j (row tid / 8, columns 4 * (tid % 8) + j)
+  const uint32_t row = threadIdx.x >> 3, col = (threadIdx.x & 7u) * 4u;
+  const uint32_t bits = (s_row[row] >> col) & 0xFu;
+  uint32_t keep = 0u;
+#pragma unroll
+  for (uint32_t j = 0; j < 4u; ++j) {
+    int x, y;
+    if (local_pixel(f, t0 + 4u * threadIdx.x + j, x, y) && !((bits >> j) & 1u)) keep |= 1u << j;
+  }
+  // mask bits of invalid pixels stay 0 (the trace kernels skip them by their own test)
+  const uint32_t valid_bits = [&] {
+    uint32_t v = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) {
+      int x, y;
+      if (local_pixel(f, t0 + 4u * threadIdx.x + j, x, y)) v |= 1u << j;
+    }
+    return v;
+  }();
+  const uint32_t mbits = bits & valid_bits;
+  // mask word (32 pixels) = the nibbles of 8 consecutive threads
+  uint32_t w = mbits << col;
+  for (int off = 1; off < 8; off <<= 1) w |= __shfl_xor(w, off);
+  if ((threadIdx.x & 7u) == 0u) mask[(t0 >> 5) + row] = w;
+  // list the kept pixels: per-thread counts, wave scan, block offsets
+  const uint32_t n = (uint32_t)__popc(keep), lane = lane_id();
+  uint32_t incl = n;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(incl, off);
+    if (lane >= (uint32_t)off) incl += v;
+  }
+  if (lane == 63u) s_cnt[threadIdx.x >> 6] = incl;
   __syncthreads();
   if (threadIdx.x == 0u) {
     uint32_t run = 0u;
-    for (uint32_t i = 0; i < kRounds * kWaves; ++i) {
+    for (uint32_t i = 0; i < kBlock / 64u; ++i) {
       const uint32_t c = s_cnt[i];
       s_cnt[i] = run;
       run += c;
@@ -874,12 +941,10 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
     s_base = run ? atomicAdd(&plist[f.P], run) : 0u;
   }
   __syncthreads();
-  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t o = s_base + s_cnt[threadIdx.x >> 6] + incl - n;
 #pragma unroll
-  for (uint32_t r = 0; r < kRounds; ++r)
-    if ((keep[r] >> lane) & 1ull)
-      plist[s_base + s_cnt[r * kWaves + wv] + (uint32_t)__popcll(keep[r] & below)] =
-          blockIdx.x * kTilePixels + r * kBlock + threadIdx.x;
+  for (uint32_t j = 0; j < 4u; ++j)
+    if ((keep >> j) & 1u) plist[o++] = t0 + 4u * threadIdx.x + j;
 }
 // Path-major bounce 0 over the unculled pixel list (f.plist: nlist pixels x k samples): compacted
 // item i -> path p.  Items run in groups of kPrimaryGroup listed pixels — neighbours, since k_cull lists
@@ -1044,6 +1109,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
     w.tot[kTotTracedP] += primary_traced(f);
+    w.tot[kTotTracedD] += primary_traced(f);
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
@@ -1072,7 +1138,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
         // 1 = constant environment, 4 = primary misses add no radiance
         if (!(ablate(f) & 2u) && !culled) {
           const Ray r = make_ray(f.cam_pos, pr.d);
+          const uint32_t v0 = vc.nodes;
           hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+          if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
         }
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
@@ -1089,7 +1157,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
       }
       const uint32_t j = block_append(&s_cnt, hit);
       if (hit) {
-        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
+        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint3(p, __float_as_uint(tfar), ref);
         else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
       }
     }
@@ -1100,6 +1168,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
     flush_visits(vc, w.tot, kTotNodesP);
+    flush_depth_nodes(vc, w.tot, 0);
   }
 }
 
@@ -1127,6 +1196,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
     w.tot[kTotTracedP] += primary_traced(f);
+    w.tot[kTotTracedD] += primary_traced(f);
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
@@ -1161,7 +1231,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         if (!culled) {
           const Ray r = make_ray(f.cam_pos, pr.d);
+          const uint32_t v0 = vc.nodes;
           hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+          if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
         }
         if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
       }
@@ -1181,7 +1253,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
       if (act && !hit && q >= nfold) w.rad[p] = f4(rv, 0.0f);
       const uint32_t j = block_append(&s_cnt, hit);
       if (hit) {
-        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint4(p, __float_as_uint(tfar), ref, 0u);
+        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint3(p, __float_as_uint(tfar), ref);
         else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
       }
     }
@@ -1192,6 +1264,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
     flush_visits(vc, w.tot, kTotNodesP);
+    flush_depth_nodes(vc, w.tot, 0);
   }
 }
 // Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
@@ -1223,7 +1296,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
-    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += kPrimary ? primary_traced(f) : n;
+    const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
+    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += t;
+    w.tot[kTotTracedD + stat_depth(depth)] += t;
   }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
@@ -1257,7 +1332,11 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       const Ray r = make_ray(o, d);
       // SPTR_ABLATE (timing experiments only, wrong images): 2 = primary rays skip traversal,
       // 1 = constant environment, 4 = primary misses write no radiance
-      if (!(kPrimary && ((ablate(f) & 2u) || culled))) hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+      if (!(kPrimary && ((ablate(f) & 2u) || culled))) {
+        const uint32_t v0 = vc.nodes;
+        hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
+        if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
+      }
       if (kPrimary && !hit && (ablate(f) & 4u)) {
       } else if (!hit) {
         if (sh.debug_mode == 1) {
@@ -1273,7 +1352,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     const uint32_t j = block_append(&s_cnt, hit);
     if (hit) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint3(id, __float_as_uint(tfar), ref);
       else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
     }
   }
@@ -1282,6 +1361,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
     if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
+    flush_depth_nodes(vc, w.tot, depth);
   }
 }
 
@@ -1350,7 +1430,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
-    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += kPrimary ? primary_traced(f) : n;
+    const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
+    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += t;
+    w.tot[kTotTracedD + stat_depth(depth)] += t;
   }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
@@ -1361,6 +1443,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   stack.lds = &s_stack.e[0][threadIdx.x];
   bool have = false, done = false;
   uint32_t id = 0u, pid = 0u, ref = kNoHit;
+  uint32_t v0 = 0u;  // kCount: the lane's node visits when its current ray started
   float tfar = 0.0f;
   Ray r;
   WideWalk wk;
@@ -1390,6 +1473,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         r = make_ray(o, d);
         tfar = __builtin_huge_valf();
         ref = kNoHit;
+        if (kCount) v0 = culled ? ~0u : vc.nodes;  // culled camera rays are not traversals
         done = walk_start<false, kCount, kW4>(wk, sc, culled ? kNoHit : (kW4 ? sv.root4 : sv.root), r, 0.0f, tfar, ref,
                                               vc);
         have = true;
@@ -1401,6 +1485,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc, kDynSteps);
     const bool fin = have && done;
+    if (kCount && fin && v0 != ~0u) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
     if (fin && !wk.hit) {
       if (sh.debug_mode == 1) {
         w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1414,7 +1499,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     const uint32_t j = block_append(&s_cnt, fin && wk.hit);
     if (fin && wk.hit) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint4(id, __float_as_uint(tfar), ref, 0u);
+      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint3(id, __float_as_uint(tfar), ref);
       else w.tot[kTotOverflow] = 1ull;
     }
     if (fin) have = false;
@@ -1424,6 +1509,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
     if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
+    flush_depth_nodes(vc, w.tot, depth);
   }
 }
 
@@ -1623,7 +1709,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     vec3 rd, thr, radv = v3(0.0f, 0.0f, 0.0f), no, nd;
     Surface sf;
     if (active) {
-      const uint4 h = w.hrec[seg_slot(s_off, nseg_in, per_in, i)];
+      const uint3 h = w.hrec[seg_slot(s_off, nseg_in, per_in, i)];
       vec3 ro;
       if (kPrimary) {
         Primary pr;
@@ -1866,7 +1952,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
       float tfar = a.w;
       uint32_t ref = kNoHit;
       ++rays;
+      const uint32_t v0 = vc.nodes;
       const bool occ = traverse_w<kW4, true, kCount>(sc, sv, r, 1e-4f, tfar, ref, vc, s_stack);
+      if (kCount) hist_ray(w.tot, kTotHistS, vc.nodes - v0);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
         any = true;
@@ -1911,6 +1999,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   stack.lds = &s_stack.e[0][threadIdx.x];
   bool have = false, done = false;
   uint32_t p = 0u, ref = kNoHit;
+  uint32_t v0 = 0u;  // kCount: the lane's node visits when its current query started
   float tfar = 0.0f;
   vec3 contrib;
   Ray r;
@@ -1978,6 +2067,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
         tfar = a.w;
         ref = kNoHit;
         ++rays;
+        if (kCount) v0 = vc.nodes;
         done = wide_start<true, kCount>(wk, sv.root4, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref, vc);
         have = true;
       }
@@ -1990,6 +2080,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
       done = wide_walk<true, kCount>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref,
                                      vc, kDynSteps);
     if (have && done) {
+      if (kCount) hist_ray(w.tot, kTotHistS, vc.nodes - v0);
       if (!wk.hit) w.rad[p] = f4(xyz(w.rad[p]) + contrib, 0.0f);
       have = false;
     }

@@ -95,11 +95,11 @@ inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
 
 // device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
 // L shadow tasks of ts float4s
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 16 + 16 + (uint64_t)L * ts * 16; }
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 12 + 16 + (uint64_t)L * ts * 16; }
 // fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
 uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
   const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
-  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * 16;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * 12;
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
@@ -107,7 +107,7 @@ uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
 // other producer needs kMaxSegs * kBlock (k_slack = 1).
 int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
   L = L ? L : 1u;
-  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * 16;
+  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * sizeof(uint3);
   const bool grow = c.w_hrec.bytes < hrec_bytes || !(c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p);
   if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
   if (grow) ++c.epoch;
@@ -140,7 +140,7 @@ WaveView wave_view(Context& c) {
     w.rs[b].d = static_cast<float4*>(c.w_rs[b][1].p);
     w.rs[b].thr = static_cast<float4*>(c.w_rs[b][2].p);
   }
-  w.hrec = static_cast<uint4*>(c.w_hrec.p);
+  w.hrec = static_cast<uint3*>(c.w_hrec.p);
   w.rad = static_cast<float4*>(c.w_rad.p);
   w.stask = static_cast<float4*>(c.w_stask.p);
   uint32_t* seg = static_cast<uint32_t*>(c.w_seg.p);  // 3 tables of kMaxSegs counts + 1 stride
@@ -154,7 +154,7 @@ WaveView wave_view(Context& c) {
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
   w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
-  w.hrec_cap = (uint32_t)std::min<uint64_t>(c.w_hrec.bytes / 16, 0xFFFFFFFFull);
+  w.hrec_cap = (uint32_t)std::min<uint64_t>(c.w_hrec.bytes / sizeof(uint3), 0xFFFFFFFFull);
   return w;
 }
 
@@ -327,6 +327,14 @@ int collect_pending(Context& c, sptr_stats* stats) {
   stats->sphere_tests_primary = tot[kTotSphP];
   stats->ms_cull = ms[8];
   stats->shadow_launches = shadow_launches;
+  for (int d = 0; d < kStatDepths; ++d) {
+    stats->traced_by_depth[d] = tot[kTotTracedD + d];
+    stats->nodes_by_depth[d] = tot[kTotNodesD + d];
+  }
+  for (int b = 0; b < kHistBins; ++b) {
+    stats->trace_visit_hist[b] = tot[kTotHistT + b];
+    stats->shadow_visit_hist[b] = tot[kTotHistS + b];
+  }
   stats->cull_launches = culls;
   return SPTR_OK;
 }
@@ -762,7 +770,7 @@ int sptr_set_debug_mode(sptr_ctx* x, int mode) {
 
 int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   if (!x) return SPTR_ERR_INVALID;
-  if (n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 0 (automatic) or 1..32");
+  if (n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 0 (automatic) or 1..16");
   x->c.leaf_size = n;
   ++x->c.epoch;
   return SPTR_OK;

@@ -28,11 +28,18 @@ namespace sptr {
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kIndexMask = 0x3FFFFFFFu;
-// Leaf link: kLeafBit | start << kLeafCountBits | (count - 1): a contiguous range of up to 32 sorted
-// primitive references (prim_ref[start .. start+count)).  Primitive ref: [kSphereBit] | slot.
-constexpr uint32_t kLeafCountBits = 5;  // start keeps 26 bits: up to 64M primitives
+// Leaf link, two forms (bit kLeafDirect tells them apart):
+//   range : kLeafBit | start << kLeafCountBits | (count - 1): a contiguous range of up to 16 sorted
+//           primitive references (prim_ref[start .. start+count)).  Primitive ref: [kSphereBit] | slot.
+//   direct: kLeafBit | slot << kLeafCountBits | kLeafDirect [| kLeafDirectSphere]: one primitive,
+//           named in the link itself, so its test needs no prim_ref load.  The wide BVH's
+//           single-primitive leaf children take this form (k_wide_emit); BVH2 leaves keep ranges.
+constexpr uint32_t kLeafCountBits = 5;  // start / slot keep 26 bits: up to 64M primitives
+constexpr uint32_t kLeafRangeMask = 0xFu;  // count - 1 of a range
+constexpr uint32_t kLeafDirect = 0x10u;
+constexpr uint32_t kLeafDirectSphere = 0x08u;
 constexpr uint32_t kLeafCountMask = (1u << kLeafCountBits) - 1u;
-constexpr uint32_t kMaxLeafSize = 1u << kLeafCountBits;
+constexpr uint32_t kMaxLeafSize = kLeafRangeMask + 1u;
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kTile = 32;
 constexpr int kTilePixels = kTile * kTile;
@@ -181,8 +188,16 @@ enum : int {
   kTotTracedP,      // bounce-0 camera rays the trace kernels traversed (unculled pixel samples)
   kTotTracedB,      // queued rays of bounces >= 1 traversed by k_trace / k_trace_dyn
   kTotNodesP, kTotTrisP, kTotSphP,  // bounce-0 part of kTotNodes / kTotTris / kTotSph
-  kTotWords
+  kTotTracedD,                       // [kStatDepths] rays the trace kernels traversed, by bounce
+  kTotNodesD = kTotTracedD + 8,      // [kStatDepths] their node visits (SPTR_FRAME_COUNT_VISITS)
+  kTotHistT = kTotNodesD + 8,        // [kHistBins] closest-hit rays by node visits, log2 bins (COUNT_VISITS)
+  kTotHistS = kTotHistT + 16,        // [kHistBins] any-hit queries of the shadow stage, likewise
+  kTotWords = kTotHistS + 16
 };
+
+constexpr int kStatDepths = 8;  // per-bounce statistics: bounces 0..6, and 7 = every later one
+constexpr int kHistBins = 16;   // per-ray visit histograms: bin b holds 2^(b-1) <= visits < 2^b (bin 0: none)
+static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16, "totals layout");
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
@@ -199,7 +214,7 @@ struct RayStream {
 
 struct WaveView {
   RayStream rs[2];  // ping-pong by depth parity: bounce d traces rs[d&1], shade d writes rs[(d+1)&1]
-  uint4* hrec;      // (slot or path id, t bits, prim ref, -) per hit
+  uint3* hrec;      // (slot or path id, t bits, prim ref) per hit: 12 B, one dwordx3 per lane
   float4* rad;      // per path id
   float4* stask;    // per shade slot: L tasks of tstride float4
   SegTable segN, segH, segS;  // next rays, hits, shadow tasks
@@ -263,7 +278,7 @@ struct Context {
   uint32_t tail_depth = 0;  // first bounce traced path-per-thread by k_tail (0 = automatic)
   // scene
   DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
-  uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..32); 0 = automatic
+  uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..16); 0 = automatic
   uint32_t bvh_width = 0;  // traversal width: 2 (LBVH as built), 4 (collapsed), 0 = automatic
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;

@@ -85,10 +85,12 @@ class Stats(C.Structure):
                 ("rays_tail", C.c_uint64), ("ms_tail", C.c_double), ("traced_primary", C.c_uint64),
                 ("traced_bounce", C.c_uint64), ("node_visits_primary", C.c_uint64),
                 ("tri_tests_primary", C.c_uint64), ("sphere_tests_primary", C.c_uint64), ("ms_cull", C.c_double),
-                ("cull_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
+                ("cull_launches", C.c_uint64), ("shadow_launches", C.c_uint64),
+                ("traced_by_depth", C.c_uint64 * 8), ("nodes_by_depth", C.c_uint64 * 8),
+                ("trace_visit_hist", C.c_uint64 * 16), ("shadow_visit_hist", C.c_uint64 * 16)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: (list(v) if isinstance(v, C.Array) else v) for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}
 
 
 class SceneLayout(C.Structure):

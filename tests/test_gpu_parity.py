@@ -514,3 +514,15 @@ def test_traced_ray_counts(renderer):
     assert st.traced_bounce == st0.traced_bounce > 0
     assert st0.rays_closest == st0.traced_primary + st0.traced_bounce
     assert st.rays_closest == st0.rays_closest
+    # per bounce: bounce 0 = the traversed camera rays; the bounces add up to the trace kernels' rays
+    assert st.traced_by_depth[0] == st.traced_primary
+    assert sum(st.traced_by_depth) == st.traced_primary + st.traced_bounce
+    # instrumented pass: every traversed ray lands in one visit-histogram bin, every any-hit query too
+    try:
+        renderer.set_tail_depth(32)
+        sc = renderer.render(cam, W, H, spp=spp, flags=sptr.SPTR_FRAME_COUNT_VISITS)
+    finally:
+        renderer.set_tail_depth(0)
+    assert sum(sc.trace_visit_hist) == sc.traced_primary + sc.traced_bounce
+    assert sum(sc.shadow_visit_hist) == sc.rays_shadow
+    assert sum(sc.nodes_by_depth) == sc.node_visits

@@ -33,17 +33,21 @@ for wl in "$@"; do
       python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_${c}_$wl.log" 2>&1
   done
   python3 tools/prof_summary.py "$out/stats_$wl" "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" > "$out/summary_$wl.txt"
-  python3 tools/prof_summary.py "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" --emit "$out/pmc_${wl}_trace.json" \
-    --kernel k_trace --workload "$wl" > /dev/null
-  cp "$out/pmc_${wl}_trace.json" "profiles/${tag}_pmc_${wl}_trace.json"
+  for k in trace shadow; do
+    python3 tools/prof_summary.py "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" --emit "$out/pmc_${wl}_$k.json" \
+      --kernel k_$k --workload "$wl" > /dev/null
+    cp "$out/pmc_${wl}_$k.json" "profiles/${tag}_pmc_${wl}_$k.json"
+  done
   if [ $sq = 1 ]; then
     echo "[$(date +%T)] pmc SQ $wl"
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
       SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d "$out/pmc_SQ_$wl" -o run -- \
       python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_SQ_$wl.log" 2>&1
     python3 tools/prof_summary.py "$out/pmc_SQ_$wl" > "$out/sq_$wl.txt"
-    python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_trace.json" --kernel k_trace --workload "$wl" > /dev/null
-    cp "$out/sq_${wl}_trace.json" "profiles/${tag}_sq_${wl}_trace.json"
+    for k in trace shadow; do
+      python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_$k.json" --kernel k_$k --workload "$wl" > /dev/null
+      cp "$out/sq_${wl}_$k.json" "profiles/${tag}_sq_${wl}_$k.json"
+    done
   fi
   echo "[$(date +%T)] bench $wl"
   timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"

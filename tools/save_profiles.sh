@@ -10,10 +10,11 @@ for wl in "$@"; do
   [ -f $run/bench_${wl}_stages.json ] && tail -1 $run/bench_${wl}_stages.json > profiles/${tag}_bench_${wl}_stages.json
   cp $run/summary_$wl.txt profiles/${tag}_summary_$wl.txt
   cp $run/stats_$wl/run_kernel_stats.csv profiles/${tag}_kernel_stats_$wl.csv
-  cp $run/pmc_${wl}_trace.json profiles/${tag}_pmc_${wl}_trace.json
-  if [ -f $run/sq_${wl}_trace.json ]; then
-    cp $run/sq_${wl}_trace.json profiles/${tag}_sq_${wl}_trace.json
-    cp $run/sq_$wl.txt profiles/${tag}_sq_$wl.txt
-  fi
+  for k in trace shadow; do
+    [ -f $run/pmc_${wl}_$k.json ] && cp $run/pmc_${wl}_$k.json profiles/${tag}_pmc_${wl}_$k.json
+    [ -f $run/sq_${wl}_$k.json ] && cp $run/sq_${wl}_$k.json profiles/${tag}_sq_${wl}_$k.json
+  done
+  [ -f $run/sq_$wl.txt ] && cp $run/sq_$wl.txt profiles/${tag}_sq_$wl.txt
+  true
 done
 ls profiles/${tag}_*
