@@ -205,9 +205,10 @@ int sptr_set_debug_mode(sptr_ctx* ctx, int mode);
  * 0 = default: 2^29, capped by what half of the device's free memory holds (at least 2^24). */
 int sptr_set_wave_paths(sptr_ctx* ctx, uint64_t max_paths);
 /* First bounce traced path-per-thread (one launch carries every surviving path to its end; earlier
- * bounces run as trace/shade/shadow wavefront stages).  0 = automatic: 4 for batches of at most
- * 2^25 paths (e.g. the per-rank share of a sharded 1080p frame), none for larger batches;
- * >= max_depth = none.  The image and the query counts do not depend on it. */
+ * bounces run as trace/shade/shadow wavefront stages).  0 = automatic: scenes traversed from L2/HBM
+ * 2 (L2-resident) or 3; LDS-staged scenes 4 for batches of at most 2^25 paths (e.g. the per-rank share
+ * of a sharded 1080p frame), none for larger batches; >= max_depth = none.  The image and the query
+ * counts do not depend on it. */
 int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..16; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 1 otherwise); applies to the next sptr_upload_scene. */

@@ -44,7 +44,13 @@
 #define SPTR_BOUNCE_WAVES 6  // r02 ab23 (no packed FP32): 8-way shard 0.548 -> 0.525 ms, 2-way 1.662 -> 1.638; 7 spills
 #endif
 #ifndef SPTR_TAIL_WAVES
-#define SPTR_TAIL_WAVES 1
+#define SPTR_TAIL_WAVES 4  // scenes traversed from L2/HBM; r03: 1 -> 4 waves/SIMD, C5 tail (bounces 3-5) 1.46 ->
+#endif                     // 1.22 ms, C3 (2-5) 0.77 -> 0.50 (8 waves: C3 0.80)
+#ifndef SPTR_PT_WAVES
+#define SPTR_PT_WAVES 1  // the path-per-thread integrators (k_pathtracer, k_optix)
+#endif
+#ifndef SPTR_TAIL_WAVES_LDS
+#define SPTR_TAIL_WAVES_LDS 1  // LDS-staged scenes (sharded C2: 4 waves 0.569 vs 1 wave 0.558 ms per rank at G = 8)
 #endif
 #ifndef SPTR_SHADOW_WAVES
 #define SPTR_SHADOW_WAVES 6  // LDS-staged BVH2 scenes: 7 waves measured slower on C2 (0.409 -> 0.426 ms)
@@ -256,11 +262,14 @@ __device__ __forceinline__ FrameView frame_dyn(FrameView f) {
   }
   return f;
 }
-__global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total) {
+// clear (may be null): a counter the call's launch sequence accumulates from zero (the unculled-pixel
+// count of an in-sequence k_cull), zeroed here instead of by a memset node of its own.
+__global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear) {
   if (threadIdx.x == 0) {
     dyn[0] = frame_begin;
     dyn[1] = reset;
     dyn[2] = total;
+    if (clear) *clear = 0u;
   }
 }
 
@@ -735,9 +744,19 @@ __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv
 
 // Per-bounce and per-ray statistics (sptr_stats traced_by_depth / nodes_by_depth / *_visit_hist).
 __device__ __forceinline__ uint32_t stat_depth(int depth) { return depth < kStatDepths - 1 ? (uint32_t)depth : kStatDepths - 1u; }
-__device__ __forceinline__ void hist_ray(unsigned long long* tot, int base, uint32_t visits) {
+// The instrumented pass bins every ray's node visits into a block-local LDS histogram (s_hist, zeroed
+// before the kernel's first barrier), flushed with one global add per bin per block at its end.
+__device__ __forceinline__ void hist_ray(uint32_t* s_hist, uint32_t visits) {
   const uint32_t b = visits ? (uint32_t)(32 - __clz(visits)) : 0u;
-  atomicAdd(&tot[base + (b < (uint32_t)kHistBins ? b : kHistBins - 1u)], 1ull);
+  atomicAdd(&s_hist[b < (uint32_t)kHistBins ? b : kHistBins - 1u], 1u);
+}
+__device__ __forceinline__ void hist_init(uint32_t* s_hist) {
+  if (threadIdx.x < (uint32_t)kHistBins) s_hist[threadIdx.x] = 0u;
+}
+// call from every thread of the block (barrier)
+__device__ __forceinline__ void hist_flush(const uint32_t* s_hist, unsigned long long* tot, int base) {
+  __syncthreads();
+  if (threadIdx.x < (uint32_t)kHistBins && s_hist[threadIdx.x]) atomicAdd(&tot[base + threadIdx.x], (unsigned long long)s_hist[threadIdx.x]);
 }
 __device__ __forceinline__ void flush_depth_nodes(const Visits& vc, unsigned long long* tot, int depth) {
   unsigned long long a = vc.nodes;
@@ -922,7 +941,7 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
   uint32_t w = mbits << col;
   for (int off = 1; off < 8; off <<= 1) w |= __shfl_xor(w, off);
   if ((threadIdx.x & 7u) == 0u) mask[(t0 >> 5) + row] = w;
-  // list the kept pixels: per-thread counts, wave scan, block offsets
+  // list the kept pixels: per-thread counts, wave scan, block offsets, one atomic per tile
   const uint32_t n = (uint32_t)__popc(keep), lane = lane_id();
   uint32_t incl = n;
   for (int off = 1; off < 64; off <<= 1) {
@@ -1103,7 +1122,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   if (threadIdx.x == 0) s_cnt = 0u;
+  if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<true>(sv, lds);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1140,7 +1161,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
           const Ray r = make_ray(f.cam_pos, pr.d);
           const uint32_t v0 = vc.nodes;
           hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-          if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
+          if (kCount) hist_ray(s_hist, vc.nodes - v0);
         }
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
@@ -1157,7 +1178,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
       }
       const uint32_t j = block_append(&s_cnt, hit);
       if (hit) {
-        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint3(p, __float_as_uint(tfar), ref);
+        if (seg0 + j < w.hrec_cap) w.hrec.put(seg0 + j, p, __float_as_uint(tfar), ref);
         else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
       }
     }
@@ -1169,6 +1190,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
     flush_visits(vc, w.tot, kTotNodes);
     flush_visits(vc, w.tot, kTotNodesP);
     flush_depth_nodes(vc, w.tot, 0);
+    hist_flush(s_hist, w.tot, kTotHistT);
   }
 }
 
@@ -1190,7 +1212,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   if (threadIdx.x == 0) s_cnt = 0u;
+  if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1233,7 +1257,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
           const Ray r = make_ray(f.cam_pos, pr.d);
           const uint32_t v0 = vc.nodes;
           hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-          if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
+          if (kCount) hist_ray(s_hist, vc.nodes - v0);
         }
         if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
       }
@@ -1253,7 +1277,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
       if (act && !hit && q >= nfold) w.rad[p] = f4(rv, 0.0f);
       const uint32_t j = block_append(&s_cnt, hit);
       if (hit) {
-        if (seg0 + j < w.hrec_cap) w.hrec[seg0 + j] = make_uint3(p, __float_as_uint(tfar), ref);
+        if (seg0 + j < w.hrec_cap) w.hrec.put(seg0 + j, p, __float_as_uint(tfar), ref);
         else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
       }
     }
@@ -1265,6 +1289,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
     flush_visits(vc, w.tot, kTotNodes);
     flush_visits(vc, w.tot, kTotNodesP);
     flush_depth_nodes(vc, w.tot, 0);
+    hist_flush(s_hist, w.tot, kTotHistT);
   }
 }
 // Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
@@ -1280,7 +1305,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   if (threadIdx.x == 0) s_cnt = 0u;
+  if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   // Bounce 0 path-major (thread <- path slot): batches of fewer than kWaveFoldMinK samples (e.g.
   // the interactive 1 spp per call).  Later bounces: thread <- queued ray.
@@ -1335,7 +1362,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (!(kPrimary && ((ablate(f) & 2u) || culled))) {
         const uint32_t v0 = vc.nodes;
         hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
-        if (kCount) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
+        if (kCount) hist_ray(s_hist, vc.nodes - v0);
       }
       if (kPrimary && !hit && (ablate(f) & 4u)) {
       } else if (!hit) {
@@ -1352,7 +1379,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     const uint32_t j = block_append(&s_cnt, hit);
     if (hit) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint3(id, __float_as_uint(tfar), ref);
+      if (sd.seg0 + j < w.hrec_cap) w.hrec.put(sd.seg0 + j, id, __float_as_uint(tfar), ref);
       else w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
     }
   }
@@ -1362,6 +1389,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_visits(vc, w.tot, kTotNodes);
     if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
     flush_depth_nodes(vc, w.tot, depth);
+    hist_flush(s_hist, w.tot, kTotHistT);
   }
 }
 
@@ -1415,8 +1443,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt, s_next;
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_cnt = s_next = 0u;
+  if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   const uint32_t ntop = (kW4 && !kLds) ? sv.num_top4 : 0u;
   const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, kLds, kPrimary, nseg_in)) : nullptr;
@@ -1485,7 +1515,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc, kDynSteps);
     const bool fin = have && done;
-    if (kCount && fin && v0 != ~0u) hist_ray(w.tot, kTotHistT, vc.nodes - v0);
+    if (kCount && fin && v0 != ~0u) hist_ray(s_hist, vc.nodes - v0);
     if (fin && !wk.hit) {
       if (sh.debug_mode == 1) {
         w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1499,7 +1529,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
     const uint32_t j = block_append(&s_cnt, fin && wk.hit);
     if (fin && wk.hit) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec[sd.seg0 + j] = make_uint3(id, __float_as_uint(tfar), ref);
+      if (sd.seg0 + j < w.hrec_cap) w.hrec.put(sd.seg0 + j, id, __float_as_uint(tfar), ref);
       else w.tot[kTotOverflow] = 1ull;
     }
     if (fin) have = false;
@@ -1510,6 +1540,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_visits(vc, w.tot, kTotNodes);
     if (kPrimary) flush_visits(vc, w.tot, kTotNodesP);
     flush_depth_nodes(vc, w.tot, depth);
+    hist_flush(s_hist, w.tot, kTotHistT);
   }
 }
 
@@ -1709,7 +1740,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     vec3 rd, thr, radv = v3(0.0f, 0.0f, 0.0f), no, nd;
     Surface sf;
     if (active) {
-      const uint3 h = w.hrec[seg_slot(s_off, nseg_in, per_in, i)];
+      uint3 h;
+      w.hrec.get(seg_slot(s_off, nseg_in, per_in, i), h.x, h.y, h.z);
       vec3 ro;
       if (kPrimary) {
         Primary pr;
@@ -1925,8 +1957,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   if (threadIdx.x == 0) s_rays = 0u;
+  if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
@@ -1954,7 +1988,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
       ++rays;
       const uint32_t v0 = vc.nodes;
       const bool occ = traverse_w<kW4, true, kCount>(sc, sv, r, 1e-4f, tfar, ref, vc, s_stack);
-      if (kCount) hist_ray(w.tot, kTotHistS, vc.nodes - v0);
+      if (kCount) hist_ray(s_hist, vc.nodes - v0);
       if (!occ) {
         if (!any) rv = xyz(w.rad[p]);
         any = true;
@@ -1968,7 +2002,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
   __syncthreads();
   if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotShNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotShNodes);
+    hist_flush(s_hist, w.tot, kTotHistS);
+  }
 }
 
 // k_shadow for wide BVHs traversed from L2/HBM with one light (C3, C5): the any-hit queries of the
@@ -1984,8 +2021,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   __shared__ KernelStack<false> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays, s_next;
+  __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
   if (threadIdx.x == 0) s_rays = s_next = 0u;
+  if (kCount) hist_init(s_hist);
   const uint32_t ntop = sv.num_top4;
   const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, false, false, nseg_in)) : nullptr;
   uint32_t per_in = 0u;
@@ -2080,7 +2119,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
       done = wide_walk<true, kCount>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref,
                                      vc, kDynSteps);
     if (have && done) {
-      if (kCount) hist_ray(w.tot, kTotHistS, vc.nodes - v0);
+      if (kCount) hist_ray(s_hist, vc.nodes - v0);
       if (!wk.hit) w.rad[p] = f4(xyz(w.rad[p]) + contrib, 0.0f);
       have = false;
     }
@@ -2090,7 +2129,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   __syncthreads();
   if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
   report_stack(vc, w.tot);
-  if (kCount) flush_visits(vc, w.tot, kTotShNodes);
+  if (kCount) {
+    flush_visits(vc, w.tot, kTotShNodes);
+    hist_flush(s_hist, w.tot, kTotHistS);
+  }
 }
 
 // --------------------------------------------------------------------------------- k_tail
@@ -2103,7 +2145,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
 // wavefront hands over (test_tail_depth_invariance).  Closest-hit and any-hit queries are tallied
 // per block (bstat_closest / bstat) and folded by k_accum.
 template <bool kLds, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
+__global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL_WAVES) k_tail(SceneView sv, ShadeView sh, FrameView f, WaveView w, int depth0,
                                                  uint32_t nseg_in) {
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -2496,7 +2538,7 @@ __device__ vec3 pt_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 // += the frame's tonemapped colour (the reference's accumulation_buffer, GLRenderer's
 // m_accumulated_samples frames).
 template <bool kLds, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
+__global__ void __launch_bounds__(kBlock, SPTR_PT_WAVES) k_pathtracer(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -2760,7 +2802,7 @@ __device__ void ox_path(const Staged& sc, const SceneView& sv, const ShadeView& 
 }
 
 template <bool kLds, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
+__global__ void __launch_bounds__(kBlock, SPTR_PT_WAVES) k_optix(SceneView sv, ShadeView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -3195,8 +3237,9 @@ void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
       Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
 }
 
-void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, hipStream_t s) {
-  hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total);
+void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total, clear);
 }
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 

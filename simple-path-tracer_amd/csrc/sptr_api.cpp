@@ -65,9 +65,16 @@ constexpr double kWaveMemFraction = 0.5;  // at most this share of the free HBM 
 // wavefront wins (no tail: 4.20 ms vs 4.34 ms with a tail from bounce 4); in the small per-rank
 // batches of a sharded frame the fixed cost of the 3 launches per deep bounce dominates, and the
 // tail from bounce 4 wins (8-way shard: 0.723 ms vs 0.794; 4-way: 1.208 vs 1.238).
+// Scenes traversed from L2/HBM (wide BVH): the late bounces hold few rays, but every wavefront launch
+// lasts as long as its longest traversal (the 64-255-visit grazing rays of a 10M-triangle mesh: ~0.25
+// ms per trace or shadow launch however few rays it holds), so the tail takes over early whatever
+// the batch size.  Measured r03 (SPTR_TAIL_WAVES 4): C3 (L2-resident) tail from bounce 2 4.22 vs 5.07
+// ms/step without a tail (from 3: 4.58); C5 (HBM) from bounce 3 10.67 vs 11.58 (from 2: 12.12).  LDS
+// scenes keep the batch-size rule (C2 1 GPU: no tail 3.21, from 4 3.31, from 3 3.48 ms).
 constexpr uint32_t kSmallBatchTailDepth = 4;
 constexpr uint64_t kSmallBatchPaths = 1ull << 25;  // batches up to this many paths take the tail
-uint32_t auto_tail_depth(uint64_t batch_paths) {
+uint32_t auto_tail_depth(uint64_t batch_paths, const SceneView& sv) {
+  if (sv.lds_bytes == 0u) return sv.scene_bytes <= (4ull << 20) ? 2u : 3u;
   return batch_paths <= kSmallBatchPaths ? kSmallBatchTailDepth : (uint32_t)kMaxDepth;
 }
 
@@ -95,11 +102,11 @@ inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
 
 // device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
 // L shadow tasks of ts float4s
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 12 + 16 + (uint64_t)L * ts * 16; }
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + kHitBytes + 16 + (uint64_t)L * ts * 16; }
 // fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
 uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
   const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
-  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * 12;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * kHitBytes;
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
@@ -107,7 +114,7 @@ uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
 // other producer needs kMaxSegs * kBlock (k_slack = 1).
 int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
   L = L ? L : 1u;
-  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * sizeof(uint3);
+  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * kHitBytes;
   const bool grow = c.w_hrec.bytes < hrec_bytes || !(c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p);
   if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
   if (grow) ++c.epoch;
@@ -140,7 +147,13 @@ WaveView wave_view(Context& c) {
     w.rs[b].d = static_cast<float4*>(c.w_rs[b][1].p);
     w.rs[b].thr = static_cast<float4*>(c.w_rs[b][2].p);
   }
-  w.hrec = static_cast<uint3*>(c.w_hrec.p);
+  const uint64_t hcap = std::min<uint64_t>(c.w_hrec.bytes / kHitBytes, 0xFFFFFFFFull);
+#if SPTR_HREC16
+  w.hrec.r = static_cast<uint4*>(c.w_hrec.p);
+#else
+  w.hrec.tr = static_cast<uint2*>(c.w_hrec.p);
+  w.hrec.id = reinterpret_cast<uint32_t*>(static_cast<char*>(c.w_hrec.p) + hcap * 8u);
+#endif
   w.rad = static_cast<float4*>(c.w_rad.p);
   w.stask = static_cast<float4*>(c.w_stask.p);
   uint32_t* seg = static_cast<uint32_t*>(c.w_seg.p);  // 3 tables of kMaxSegs counts + 1 stride
@@ -154,7 +167,7 @@ WaveView wave_view(Context& c) {
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
   w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
-  w.hrec_cap = (uint32_t)std::min<uint64_t>(c.w_hrec.bytes / sizeof(uint3), 0xFFFFFFFFull);
+  w.hrec_cap = (uint32_t)hcap;
   return w;
 }
 
@@ -461,14 +474,20 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
 #else
   constexpr bool no_bounce = false;
 #endif
-  // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it; made
-  // current by refresh_cull ahead of this launch sequence)
+  // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it): made
+  // current by refresh_cull ahead of this launch sequence, or, with SPTR_FRAME_RECULL, computed as the
+  // sequence's first launch (inside a captured graph, whose key includes the camera and the flag)
   if (!(f.flags & SPTR_FRAME_NO_CULL)) {
     fv.cull_depth = cull_depth_for(f.spp);
     fv.cull = static_cast<const uint32_t*>(c.cull.p);
     fv.unculled = static_cast<const uint32_t*>(c.plist.p) + c.P;
   }
   tm.begin_call();
+  if (fv.cull && (f.flags & SPTR_FRAME_RECULL)) {  // the count at plist[P] was zeroed by k_frame_dyn
+    tm.begin(8);
+    launch_cull(sv, fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
+    tm.end();
+  }
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
   while (done < f.spp) {
@@ -547,6 +566,13 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
 int refresh_cull(Context& c, const sptr_frame& f, hipStream_t s, bool timing) {
   if (f.flags & SPTR_FRAME_NO_CULL) return SPTR_OK;
   const uint32_t depth = cull_depth_for(f.spp);
+  if (f.flags & SPTR_FRAME_RECULL) {  // the call's own launch sequence computes the mask (enqueue_wavefront)
+    c.cull_epoch = c.epoch;
+    c.cull_cam = f.camera;
+    c.cull_depth = depth;
+    ++c.pending_culls;
+    return SPTR_OK;
+  }
   if (!(f.flags & SPTR_FRAME_RECULL) && c.cull_epoch == c.epoch && c.cull_depth == depth &&
       std::memcmp(&c.cull_cam, &f.camera, sizeof(sptr_camera)) == 0)
     return SPTR_OK;
@@ -580,14 +606,14 @@ void drop_graph(Context& c) {
 // as the arguments of the graph's k_frame_dyn node and the timing events re-pointed at fresh pool
 // events per replay.  The launch sequence itself is the same code either way.
 template <class Enqueue>
-int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, bool timing,
-             bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
+int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
+             bool timing, bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
   if (c.launch_mode != 0 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
     StageTimer tm{c, timing, trace_only, s};
-    launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, s);
+    launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
     if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
@@ -617,7 +643,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
       StageTimer td{c, timing, trace_only, s};
-      launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, s);
+      launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
       waves = enqueue(s, td);
       API_HIP(hipGetLastError());
       if (td.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(td.err));
@@ -634,7 +660,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     API_HIP(hipGraphGetRootNodes(g, roots.data(), &nr));
     void* dyn_ptr = c.dyn.p;
     uint32_t a0 = frame_begin, a1 = reset, a2 = total;
-    void* args[4] = {&dyn_ptr, &a0, &a1, &a2};
+    uint32_t* a3 = clear;
+    void* args[5] = {&dyn_ptr, &a0, &a1, &a2, &a3};
     hipKernelNodeParams kp{};
     kp.func = const_cast<void*>(frame_dyn_kernel());
     kp.gridDim = dim3(1);
@@ -685,7 +712,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   GraphCache& gc = c.graph;
   void* dyn_ptr = c.dyn.p;
   uint32_t a0 = frame_begin, a1 = reset, a2 = total;
-  void* args[4] = {&dyn_ptr, &a0, &a1, &a2};
+  uint32_t* a3 = clear;
+  void* args[5] = {&dyn_ptr, &a0, &a1, &a2, &a3};
   hipKernelNodeParams p = gc.dyn_params;
   p.kernelParams = args;
   p.extra = nullptr;
@@ -967,13 +995,13 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   key.frame = *f;
   key.frame.frame_begin = 0;
   key.frame.flags &= (SPTR_FRAME_TIMING | SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_COUNT_VISITS | SPTR_FRAME_NO_RESOLVE |
-                      SPTR_FRAME_NO_CULL);
+                      SPTR_FRAME_NO_CULL | SPTR_FRAME_RECULL);
   uint32_t waves = 0;
   uint64_t samples = 0;
   if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) {
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
     const uint32_t spf = f->integrator == SPTR_INTEGRATOR_PATHTRACER ? (f->samples_per_frame ? f->samples_per_frame : 4u) : 1u;
-    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, timing || trace_timing, false, s,
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, nullptr, timing || trace_timing, false, s,
                   [&](hipStream_t cs, StageTimer& tm) { return enqueue_path_per_thread(c, *f, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
     samples = (uint64_t)frame_view(c, *f).valid * f->spp * spf;
@@ -1005,14 +1033,17 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
       if (rc != SPTR_OK) return rc;
     }
-    const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P)));
+    const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));
     key.epoch = c.epoch;  // ensure_wave may have reallocated
     key.k = k;
     key.tail = (uint32_t)T;
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
     rc = refresh_cull(c, *f, s, timing || trace_timing);
     if (rc != SPTR_OK) return rc;
-    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, timing || trace_timing, !timing, s,
+    // an in-sequence cull (SPTR_FRAME_RECULL) counts its unculled pixels from zero: k_frame_dyn clears it
+    uint32_t* clear = ((f->flags & SPTR_FRAME_RECULL) && !(f->flags & SPTR_FRAME_NO_CULL))
+                          ? static_cast<uint32_t*>(c.plist.p) + c.P : nullptr;
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, clear, timing || trace_timing, !timing, s,
                   [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
     samples = (uint64_t)frame_view(c, *f).valid * f->spp;

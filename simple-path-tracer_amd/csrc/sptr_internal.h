@@ -206,6 +206,44 @@ struct SegTable {
   uint32_t* per;  // [1]
 };
 
+// Hit records: per hit of a trace stage, the ray's input slot (bounce 0: its path id), its t bits and
+// the primitive ref, 12 B in two dense arrays — {t, ref} (8 B, one dwordx2 per lane) and the slot (4 B,
+// one dword) — so every access is a naturally aligned coalesced stream.  SPTR_HREC16 = 1: one uint4
+// record (16 B, A/B builds).  (r03: a packed 12-B uint3 record, one dwordx3 per lane, was 2 % slower on
+// C2 than the 16-B record.)
+#ifndef SPTR_HREC16
+#define SPTR_HREC16 0
+#endif
+#if SPTR_HREC16
+constexpr size_t kHitBytes = 16;
+struct HitStream {
+  uint4* r;
+  __device__ __forceinline__ void put(uint32_t j, uint32_t id, uint32_t tb, uint32_t ref) const { r[j] = make_uint4(id, tb, ref, 0u); }
+  __device__ __forceinline__ void get(uint32_t j, uint32_t& id, uint32_t& tb, uint32_t& ref) const {
+    const uint4 v = r[j];
+    id = v.x;
+    tb = v.y;
+    ref = v.z;
+  }
+};
+#else
+constexpr size_t kHitBytes = 12;
+struct HitStream {
+  uint2* tr;     // {t bits, prim ref}
+  uint32_t* id;  // input slot or path id
+  __device__ __forceinline__ void put(uint32_t j, uint32_t i, uint32_t tb, uint32_t ref) const {
+    tr[j] = make_uint2(tb, ref);
+    id[j] = i;
+  }
+  __device__ __forceinline__ void get(uint32_t j, uint32_t& i, uint32_t& tb, uint32_t& ref) const {
+    const uint2 v = tr[j];
+    i = id[j];
+    tb = v.x;
+    ref = v.y;
+  }
+};
+#endif
+
 struct RayStream {
   float4* o;    // origin.xyz, rng state bits
   float4* d;    // direction.xyz, path id bits
@@ -214,7 +252,7 @@ struct RayStream {
 
 struct WaveView {
   RayStream rs[2];  // ping-pong by depth parity: bounce d traces rs[d&1], shade d writes rs[(d+1)&1]
-  uint3* hrec;      // (slot or path id, t bits, prim ref) per hit: 12 B, one dwordx3 per lane
+  HitStream hrec;   // per hit: slot or path id, t bits, prim ref
   float4* rad;      // per path id
   float4* stask;    // per shade slot: L tasks of tstride float4
   SegTable segN, segH, segS;  // next rays, hits, shadow tasks
@@ -307,7 +345,7 @@ struct Context {
   uint32_t P = 0, local_tiles = 0;
   DevBuf accum, tiles, image;
   DevBuf cull;   // bounce-0 pixel-frustum cull mask, 1 bit per local pixel (k_cull)
-  DevBuf plist;  // the local pixels k_cull did not cull, in no particular order; their count at [P]
+  DevBuf plist;  // the local pixels k_cull did not cull, each tile's run in pixel order; their count at [P]
   // what the mask was computed for (state epoch, camera): k_cull reruns only when these change
   uint64_t cull_epoch = 0;
   sptr_camera cull_cam{};
@@ -356,7 +394,8 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.
-void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, hipStream_t s);
+void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
+                      hipStream_t s);
 const void* frame_dyn_kernel();
 // PathTracer-mode frames (the k frames of f from f.acc0), one launch: accum += tonemapped frames.
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);

@@ -320,8 +320,10 @@ def test_tail_depth_invariance(renderer, scene, p0, p1):
         renderer.set_tail_depth(0)
     ref = out[6]
     assert ref[3] == 0  # tail at max_depth: all bounces are wavefront stages
-    # automatic policy: a small batch (96x64x4 paths) hands over to the tail at bounce 4
-    assert out[0][3] == out[4][3] > 0
+    # automatic policy: an LDS-staged scene's small batch (96x64x4 paths) hands over to the tail at
+    # bounce 4; a scene traversed from L2 (the BVH4 sphere mesh, < 4 MB) at bounce 2
+    auto = 4 if renderer.scene_layout()["lds_bytes"] else 2
+    assert out[0][3] == out[auto][3] > 0
     for t in (1, 2, 3, 4, 5, 0):
         acc, rc, rs, rt = out[t]
         assert np.array_equal(acc.view(np.uint32), ref[0].view(np.uint32)), t

@@ -1,10 +1,11 @@
-"""Print the kernels of the last complete step of a rocprofv3 kernel trace with durations and gaps."""
+"""Print the kernels of the last complete render call of a rocprofv3 kernel trace (calls start at
+k_frame_dyn) with durations and the gaps between them."""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "resolve" in r["Kernel_Name"]]
-a, b = idx[-2] + 1, min(len(rows), idx[-1] + 1)
+idx = [i for i, r in enumerate(rows) if "k_frame_dyn" in r["Kernel_Name"]]
+a, b = idx[-2], idx[-1]
 prev, tot = None, 0.0
 for r in rows[a:b]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
