@@ -46,9 +46,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # VALU issue peak: a wave issues one VALU instruction per 2 cycles on its SIMD (MI355X_MICROARCH.md),
 # 256 CUs x 4 SIMDs x 0.5 x 2.4 GHz = 1.2288e12 wave-instructions/s
 VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 0.5 * 2.4e9
-# SURVEY.md §8(d) ray stream: path id 4 + origin 12 + dir 12 read, t 4 + prim 4 written.  A primary
-# ray reads nothing (raygen is fused into the bounce-0 trace), so it is charged the 8 B it writes.
+# SURVEY.md §8(d) ray stream: path id 4 + origin 12 + dir 12 read, t 4 + prim 4 written (frac_s8d)
 STREAM_READ_BYTES, STREAM_WRITE_BYTES = 28.0, 8.0
+# the product's streams: hit record {t, prim} + slot/path id, ray origin + direction
+# (two float4), throughput and radiance float4, four cubemap texels per environment lookup
+HIT_RECORD_BYTES, RAY_READ_BYTES, THR_READ_BYTES, RAD_BYTES, ENV_TEXEL_BYTES = 12.0, 32.0, 16.0, 16.0, 64.0
 L2_BYTES_PER_XCD = 4 << 20  # MI355X: 4 MB L2 per XCD (MI355X_MICROARCH.md)
 XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 128, "c4": 64, "c5": 64}  # ~1-4 s per run on 16 host threads
@@ -109,39 +111,46 @@ def _counter_fracs(wl_name, kernel, avg_launch_s, stream_read_per_launch):
             "salu_per_valu": round(salu / valu, 3) if salu and valu else None, "valu_source": sq_src}
 
 
-def roofline(cnt, stats, layout, wl_name, steps):
-    """Roofline of the dominant kernel, k_trace (all bounces; one template).
+def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
+    """Roofline of the dominant kernel, k_trace (all its launches: bounce 0 and the wavefront bounces
+    before the path-per-thread tail; one template).
 
-    cnt: the stats of one instrumented (SPTR_FRAME_COUNT_VISITS) step, used only for BVH visits per
-    traversed ray; stats: the K timed steps (launch times, launch counts and the rays the trace
+    cnt: the stats of one instrumented (SPTR_FRAME_COUNT_VISITS) step, used only for per-ray ratios (BVH
+    visits, hit fraction); stats: the K timed steps (launch times, launch counts and the rays the trace
     launches traversed, all summed over the K steps), so every per-launch figure below is a ratio of
     two sums over the same launches and does not depend on K.
 
-    Rays are those the trace launches actually traverse (the library's traced_primary /
-    traced_bounce): camera rays of frustum-culled pixels are answered without a traversal and are not
-    charged.  Algorithmic bytes per ray, SURVEY.md §8(d): B_ray = 36 (28 read: path id, o, d; 8 written:
-    t, prim) + 64 n_node + 48 n_tri + 16 n_sph, with the visit counts per traversed ray of the
-    instrumented pass (bounce 0 and later bounces separately); a camera ray reads no input stream
-    (raygen is fused into the bounce-0 trace) and is charged its 8 written bytes.  Which node/primitive
-    bytes are HBM bytes depends on where the scene lives:
+    Rays are those the trace launches actually traverse (the library's traced_primary / traced_bounce):
+    camera rays of frustum-culled pixels are answered without a traversal and are not charged.
+    Algorithmic HBM bytes per traversed ray: a camera ray reads nothing (raygen is fused)
+    and writes a 12-B hit record (t, prim, path id) on a hit or its 16-B radiance on a miss; a later
+    ray reads its 32-B origin/direction, writes a 12-B hit record on a hit or, on a miss, reads its
+    throughput and read-modify-writes its radiance (48 B); a miss in a cubemap environment also reads 4
+    texels (64 B).  Node/primitive bytes (64 n_node + 48 n_tri + 16 n_sph per ray, the visit counts of
+    the instrumented pass) count as HBM bytes according to where the scene lives:
       lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU;
       l2   scene fits one XCD's 4 MB L2: one scene copy per XCD per launch;
-      hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in §8(d).
+      hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in SURVEY.md §8(d).
     frac_s8d: §8(d) taken literally (36 B per traversed ray and every visit charged, whatever the residency).
     Beside them: counter_frac / valu_issue_frac / salu_per_valu from the session's rocprofv3 passes."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
     tp = sum(s.traced_primary for s in stats)
     tb = sum(s.traced_bounce for s in stats)
-    # visits per traversed ray, bounce 0 and later bounces (instrumented step)
+    # visits and hit fractions per traversed ray, bounce 0 and later bounces (instrumented step)
     vp = [cnt.node_visits_primary, cnt.tri_tests_primary, cnt.sphere_tests_primary]
     vb = [cnt.node_visits - vp[0], cnt.tri_tests - vp[1], cnt.sphere_tests - vp[2]]
     pp = [v / max(1, cnt.traced_primary) for v in vp]
     pb = [v / max(1, cnt.traced_bounce) for v in vb]
+    hp = getattr(cnt, "hits_primary", 0) / max(1, cnt.traced_primary)
+    hb = getattr(cnt, "hits_bounce", 0) / max(1, cnt.traced_bounce)
     node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0
     scene_p = node_b * pp[0] + 48.0 * pp[1] + 16.0 * pp[2]
     scene_b = node_b * pb[0] + 48.0 * pb[1] + 16.0 * pb[2]
-    stream = STREAM_WRITE_BYTES * tp + (STREAM_READ_BYTES + STREAM_WRITE_BYTES) * tb
+    env = ENV_TEXEL_BYTES if cube_env else 0.0
+    stream = (tp * (hp * HIT_RECORD_BYTES + (1.0 - hp) * (RAD_BYTES + env))
+              + tb * (RAY_READ_BYTES + hb * HIT_RECORD_BYTES + (1.0 - hb) * (THR_READ_BYTES + 2 * RAD_BYTES + env)))
+    stream_read = tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))  # coalesced reads
     residency, footprint = _residency(layout)
     scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * tb}[residency]
     per_launch = (stream + scene) / max(1, launches)
@@ -150,12 +159,14 @@ def roofline(cnt, stats, layout, wl_name, steps):
            + 48.0 * (pp[1] * tp + pb[1] * tb) + 16.0 * (pp[2] * tp + pb[2] * tb)) / max(1, launches)
     out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    out.update(_counter_fracs(wl_name, "trace", avg_launch_s, STREAM_READ_BYTES * tb / max(1, launches)))
+    out.update(_counter_fracs(wl_name, "trace", avg_launch_s, stream_read / max(1, launches)))
     out.update({
         "frac_s8d": round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None,
-        "bytes_per_launch": round(per_launch), "avg_launch_us": round(avg_launch_s * 1e6, 2),
+        "bytes_per_launch": round(per_launch), "stream_bytes_per_launch": round(stream / max(1, launches)),
+        "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches_per_step": round(launches / max(1, steps), 3),
         "traversed_rays_per_launch": round((tp + tb) / max(1, launches)),
+        "hit_fraction": {"primary": round(hp, 4), "bounce": round(hb, 4)},
         "scene_in_lds": residency == "lds", "scene_residency": residency, "scene_bytes": int(footprint),
         "per_ray": {"primary": {"nodes": round(pp[0], 3), "tris": round(pp[1], 3), "spheres": round(pp[2], 3)},
                     "bounce": {"nodes": round(pb[0], 3), "tris": round(pb[1], 3), "spheres": round(pb[2], 3)}}})
@@ -533,7 +544,7 @@ def main():
             "world_size": world,
             "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
-            "roofline": roofline(cnt, stats, layout, wl.name, args.steps),
+            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, cube_env=wl.hdr_env),
             "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
             "stage_ms_per_step": stage_ms,
             "cull_ms": round(sum(s.ms_cull for s in stats) / args.steps, 4),

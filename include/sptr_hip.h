@@ -193,6 +193,8 @@ typedef struct sptr_stats {
   uint64_t nodes_by_depth[8];
   uint64_t trace_visit_hist[16];
   uint64_t shadow_visit_hist[16];
+  uint64_t hits_primary, hits_bounce; /* SPTR_FRAME_COUNT_VISITS: closest hits the trace kernels found
+                                         (of traced_primary / traced_bounce) */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */

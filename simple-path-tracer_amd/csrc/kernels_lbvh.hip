@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <chrono>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -30,6 +31,9 @@
 
 #ifndef SPTR_GREEDY_WEIGHT
 #define SPTR_GREEDY_WEIGHT 0  // 1: the greedy collapse opens the child of largest area x primitives
+#endif
+#ifndef SPTR_EXPERIMENT_HOST_SAH
+#define SPTR_EXPERIMENT_HOST_SAH 0
 #endif
 #ifndef SPTR_WIDE_DIRECT
 #define SPTR_WIDE_DIRECT 1  // wide single-primitive leaves as direct links (0: prim_ref ranges, A/B builds)
@@ -542,6 +546,150 @@ __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, cons
   }
 }
 
+#if SPTR_EXPERIMENT_HOST_SAH
+// Timing experiment only (A/B builds): a binned-SAH BVH2 built on the host over the primitives'
+// centroids (16 bins per axis, single-primitive leaves), numbered in preorder from the root (node 0),
+// to measure what BVH2 quality is worth for the device traversal against the Karras LBVH.  Output: the
+// leaf order of the primitives (order[i] = primitive at sorted position i), the nodes with boxes and
+// links (leaf links are ranges of one sorted position), and the tree height.
+struct HostBox {
+  float lo[3], hi[3];
+};
+static void host_sah(const float* pos, const uint32_t* idx, uint32_t ntri, const float* sph, uint32_t nsph,
+                     std::vector<uint32_t>& order, std::vector<BvhNode>& nodes, uint32_t& height) {
+  const uint32_t N = ntri + nsph;
+  std::vector<HostBox> box(N);
+  std::vector<float> cen((size_t)N * 3);
+  for (uint32_t i = 0; i < N; ++i) {
+    HostBox b;
+    if (i < ntri) {
+      for (int a = 0; a < 3; ++a) {
+        float v0 = pos[3 * idx[3 * i] + a], v1 = pos[3 * idx[3 * i + 1] + a], v2 = pos[3 * idx[3 * i + 2] + a];
+        b.lo[a] = std::min(v0, std::min(v1, v2));
+        b.hi[a] = std::max(v0, std::max(v1, v2));
+      }
+    } else {
+      const float* q = sph + 4 * (i - ntri);
+      for (int a = 0; a < 3; ++a) {
+        b.lo[a] = q[a] - q[3];
+        b.hi[a] = q[a] + q[3];
+      }
+    }
+    box[i] = b;
+    for (int a = 0; a < 3; ++a) cen[(size_t)i * 3 + a] = 0.5f * (b.lo[a] + b.hi[a]);
+  }
+  order.resize(N);
+  for (uint32_t i = 0; i < N; ++i) order[i] = i;
+  nodes.assign(N - 1, BvhNode{});
+  auto area = [](const HostBox& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  auto grow = [](HostBox& a, const HostBox& b) {
+    for (int k = 0; k < 3; ++k) {
+      a.lo[k] = std::min(a.lo[k], b.lo[k]);
+      a.hi[k] = std::max(a.hi[k], b.hi[k]);
+    }
+  };
+  const HostBox empty{{FLT_MAX, FLT_MAX, FLT_MAX}, {-FLT_MAX, -FLT_MAX, -FLT_MAX}};
+  struct Task {
+    uint32_t lo, hi, node, depth;  // range [lo, hi) becomes node
+  };
+  uint32_t next = 1;
+  height = 0;
+  std::vector<Task> st{{0u, N, 0u, 0u}};
+  // returns the link of range [lo, hi) and its box (one primitive: a leaf; else a new node index)
+  auto child = [&](uint32_t lo, uint32_t hi, uint32_t depth, HostBox& b, std::vector<Task>& stk) -> uint32_t {
+    b = empty;
+    for (uint32_t i = lo; i < hi; ++i) grow(b, box[order[i]]);
+    if (hi - lo == 1) {
+      height = std::max(height, depth);
+      return kLeafBit | (lo << kLeafCountBits);
+    }
+    const uint32_t id = next++;
+    stk.push_back(Task{lo, hi, id, depth});
+    return id;
+  };
+  while (!st.empty()) {
+    const Task t = st.back();
+    st.pop_back();
+    const uint32_t n = t.hi - t.lo;
+    HostBox cb = empty;
+    for (uint32_t i = t.lo; i < t.hi; ++i)
+      for (int a = 0; a < 3; ++a) {
+        cb.lo[a] = std::min(cb.lo[a], cen[(size_t)order[i] * 3 + a]);
+        cb.hi[a] = std::max(cb.hi[a], cen[(size_t)order[i] * 3 + a]);
+      }
+    constexpr int B = 16;
+    float best = FLT_MAX;
+    int bax = -1, bsplit = 0;
+    for (int a = 0; a < 3; ++a) {
+      const float ext = cb.hi[a] - cb.lo[a];
+      if (!(ext > 0.0f)) continue;
+      HostBox bb[B];
+      uint32_t bc[B] = {0};
+      for (int k = 0; k < B; ++k) bb[k] = empty;
+      for (uint32_t i = t.lo; i < t.hi; ++i) {
+        int k = (int)((cen[(size_t)order[i] * 3 + a] - cb.lo[a]) / ext * B);
+        k = std::min(std::max(k, 0), B - 1);
+        grow(bb[k], box[order[i]]);
+        ++bc[k];
+      }
+      HostBox L = empty;
+      uint32_t nl = 0;
+      float al[B];
+      uint32_t cl[B];
+      for (int k = 0; k < B - 1; ++k) {
+        grow(L, bb[k]);
+        nl += bc[k];
+        al[k] = nl ? area(L) : 0.0f;
+        cl[k] = nl;
+      }
+      HostBox R = empty;
+      uint32_t nr = 0;
+      for (int k = B - 1; k >= 1; --k) {
+        grow(R, bb[k]);
+        nr += bc[k];
+        if (cl[k - 1] == 0 || nr == 0) continue;
+        const float cost = al[k - 1] * (float)cl[k - 1] + area(R) * (float)nr;
+        if (cost < best) {
+          best = cost;
+          bax = a;
+          bsplit = k;
+        }
+      }
+    }
+    uint32_t mid;
+    if (bax < 0) {
+      mid = t.lo + n / 2;
+    } else {
+      const float ext = cb.hi[bax] - cb.lo[bax];
+      auto it = std::partition(order.begin() + t.lo, order.begin() + t.hi, [&](uint32_t pi) {
+        int k = (int)((cen[(size_t)pi * 3 + bax] - cb.lo[bax]) / ext * B);
+        k = std::min(std::max(k, 0), B - 1);
+        return k < bsplit;
+      });
+      mid = (uint32_t)(it - order.begin());
+      if (mid == t.lo || mid == t.hi) mid = t.lo + n / 2;
+    }
+    HostBox lb, rb;
+    BvhNode nd{};
+    const uint32_t l = child(t.lo, mid, t.depth + 1, lb, st);
+    const uint32_t r = child(mid, t.hi, t.depth + 1, rb, st);
+    nd.lxy = make_float4(lb.lo[0], lb.hi[0], lb.lo[1], lb.hi[1]);
+    nd.rxy = make_float4(rb.lo[0], rb.hi[0], rb.lo[1], rb.hi[1]);
+    nd.z = make_float4(lb.lo[2], lb.hi[2], rb.lo[2], rb.hi[2]);
+    nd.link = make_uint4(l, r, kNoHit, n);
+    nodes[t.node] = nd;
+  }
+  for (uint32_t i = 0; i < N - 1; ++i) {
+    const BvhNode& nd = nodes[i];
+    if (!(nd.link.x & kLeafBit)) nodes[nd.link.x].link.z = i;
+    if (!(nd.link.y & kLeafBit)) nodes[nd.link.y].link.z = i;
+  }
+}
+#endif
+
 struct Tmp {
   std::vector<void*> ptrs;
   ~Tmp() {
@@ -647,6 +795,18 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   void* tstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
   LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, N, 0, 63, s));
+#if SPTR_EXPERIMENT_HOST_SAH
+  std::vector<uint32_t> sah_order;
+  std::vector<BvhNode> sah_nodes;
+  uint32_t sah_height = 0;
+  const bool use_sah = N > 1 && c.leaf_size != 8 &&
+                       ((uint64_t)(N - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)N + 3) / 4 * 16) >
+                           kLdsSceneBytes;
+  if (use_sah) {
+    host_sah(h_pos, h_idx, ntris, h_sph, nsph, sah_order, sah_nodes, sah_height);
+    LB_CHECK(hipMemcpyAsync(vals_s, sah_order.data(), (size_t)N * 4, hipMemcpyHostToDevice, s));
+  }
+#endif
   hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(N)), dim3(256), 0, s, N, ntris, vals_s, flag);
   size_t sbytes = 0;
   LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, N, rocprim::plus<uint32_t>(), s));
@@ -677,6 +837,13 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
     uint32_t dep = 0;
+#if SPTR_EXPERIMENT_HOST_SAH
+    if (use_sah) {
+      LB_CHECK(hipMemcpyAsync(nodes, sah_nodes.data(), (size_t)(N - 1) * sizeof(BvhNode), hipMemcpyHostToDevice, s));
+      LB_CHECK(hipStreamSynchronize(s));
+      dep = sah_height;
+    } else
+#endif
     {
       LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
       hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,

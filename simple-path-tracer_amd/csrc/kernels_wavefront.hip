@@ -1185,6 +1185,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
     if (l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
   }
   seg_publish(w.segH, &s_cnt, per);
+  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kTotHitP], (unsigned long long)s_cnt);
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
@@ -1284,6 +1285,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
     if (q == 0u && l < f.P) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(valid ? resume : f.k));
   }
   seg_publish(w.segH, &s_cnt, per);
+  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kTotHitP], (unsigned long long)s_cnt);
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
@@ -1384,6 +1386,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     }
   }
   seg_publish(w.segH, &s_cnt, sd.per);
+  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kPrimary ? kTotHitP : kTotHitB], (unsigned long long)s_cnt);
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
@@ -1535,6 +1538,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     if (fin) have = false;
   }
   seg_publish(w.segH, &s_cnt, sd.per);
+  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kPrimary ? kTotHitP : kTotHitB], (unsigned long long)s_cnt);
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);

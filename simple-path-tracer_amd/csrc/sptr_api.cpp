@@ -348,6 +348,8 @@ int collect_pending(Context& c, sptr_stats* stats) {
     stats->trace_visit_hist[b] = tot[kTotHistT + b];
     stats->shadow_visit_hist[b] = tot[kTotHistS + b];
   }
+  stats->hits_primary = tot[kTotHitP];
+  stats->hits_bounce = tot[kTotHitB];
   stats->cull_launches = culls;
   return SPTR_OK;
 }

@@ -192,12 +192,14 @@ enum : int {
   kTotNodesD = kTotTracedD + 8,      // [kStatDepths] their node visits (SPTR_FRAME_COUNT_VISITS)
   kTotHistT = kTotNodesD + 8,        // [kHistBins] closest-hit rays by node visits, log2 bins (COUNT_VISITS)
   kTotHistS = kTotHistT + 16,        // [kHistBins] any-hit queries of the shadow stage, likewise
-  kTotWords = kTotHistS + 16
+  kTotHitP = kTotHistS + 16,         // closest hits found by the bounce-0 trace kernels (COUNT_VISITS)
+  kTotHitB,                          // closest hits found by the later trace kernels (COUNT_VISITS)
+  kTotWords
 };
 
 constexpr int kStatDepths = 8;  // per-bounce statistics: bounces 0..6, and 7 = every later one
 constexpr int kHistBins = 16;   // per-ray visit histograms: bin b holds 2^(b-1) <= visits < 2^b (bin 0: none)
-static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16, "totals layout");
+static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 2, "totals layout");
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.

@@ -87,7 +87,8 @@ class Stats(C.Structure):
                 ("tri_tests_primary", C.c_uint64), ("sphere_tests_primary", C.c_uint64), ("ms_cull", C.c_double),
                 ("cull_launches", C.c_uint64), ("shadow_launches", C.c_uint64),
                 ("traced_by_depth", C.c_uint64 * 8), ("nodes_by_depth", C.c_uint64 * 8),
-                ("trace_visit_hist", C.c_uint64 * 16), ("shadow_visit_hist", C.c_uint64 * 16)]
+                ("trace_visit_hist", C.c_uint64 * 16), ("shadow_visit_hist", C.c_uint64 * 16),
+                ("hits_primary", C.c_uint64), ("hits_bounce", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(v) if isinstance(v, C.Array) else v) for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}

@@ -28,7 +28,8 @@ def _step_stats(steps, launches_per_step=6, ms_per_launch=0.3, tp=10_000_000, tb
 CNT = SimpleNamespace(traced_primary=10_000_000, traced_bounce=28_000_000, node_visits=90_000_000,
                       tri_tests=40_000_000, sphere_tests=5_000_000, node_visits_primary=30_000_000,
                       tri_tests_primary=12_000_000, sphere_tests_primary=1_000_000, rays_shadow=12_000_000,
-                      shadow_node_visits=50_000_000, shadow_prim_tests=9_000_000)
+                      shadow_node_visits=50_000_000, shadow_prim_tests=9_000_000, hits_primary=4_000_000,
+                      hits_bounce=7_000_000)
 HBM = {"node_bytes": 64 * 1000, "num_nodes": 1000, "tri_bytes": 480_000_000, "sphere_bytes": 16 * 8,
        "prim_ref_bytes": 40_000_000, "lds_bytes": 0}
 LDS = dict(HBM, tri_bytes=48 * 12, prim_ref_bytes=80, node_bytes=64 * 20, num_nodes=20, lds_bytes=2084)
@@ -45,12 +46,17 @@ def test_frac_independent_of_timed_steps(bench, layout):
     assert sa["frac"] == pytest.approx(sb["frac"], rel=1e-9)
 
 
+def _stream(tp, tb, hp, hb, env=0.0):
+    return tp * (hp * 12.0 + (1 - hp) * (16.0 + env)) + tb * (32.0 + hb * 12.0 + (1 - hb) * (48.0 + env))
+
+
 def test_bytes_follow_s8d(bench):
-    """hbm residency: every visit charged, camera rays 8 B, later rays 36 B."""
+    """hbm residency: every visit charged; the ray streams by hit and miss; frac_s8d the
+    literal SURVEY.md §8(d) figure (36 B per ray)."""
     r = bench.roofline(CNT, [_step_stats(3)], HBM, "no_such_workload", 3)
     tp, tb = CNT.traced_primary, CNT.traced_bounce
     scene = 64.0 * CNT.node_visits + 48.0 * CNT.tri_tests + 16.0 * CNT.sphere_tests
-    per_launch = (8.0 * tp + 36.0 * tb + scene) / 6
+    per_launch = (_stream(tp, tb, 0.4, 0.25) + scene) / 6
     assert r["bytes_per_launch"] == pytest.approx(per_launch, rel=1e-6)
     assert r["frac"] == pytest.approx(per_launch / 0.3e-3 / 1e9 / 8000.0, rel=1e-3)
     s8d = (36.0 * (tp + tb) + scene) / 6
@@ -69,7 +75,11 @@ def test_culled_rays_not_charged(bench):
 def test_lds_scene_charges_stream_only(bench):
     r = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1)
     assert r["scene_residency"] == "lds"
-    assert r["bytes_per_launch"] == pytest.approx((8.0 * CNT.traced_primary + 36.0 * CNT.traced_bounce) / 6, rel=1e-6)
+    assert r["bytes_per_launch"] == pytest.approx(_stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25) / 6,
+                                                  rel=1e-6)
+    c = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1, cube_env=True)
+    assert c["bytes_per_launch"] == pytest.approx(
+        _stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25, env=64.0) / 6, rel=1e-6)
 
 
 def test_no_shadow_launches_no_entry(bench):
