@@ -149,16 +149,29 @@ __device__ __forceinline__ uint32_t logical_block() {
 // blocks that drew the expensive region; dealing chunks balances statistically and keeps all CUs
 // on one band of the frame at a time (shared BVH working set).  Every block processes at most
 // `per` items, which is the stride of its output segment: seg0 = logical block * per.
+// SPTR_SCHED_CONTIG (timing experiment): block b takes the contiguous items [b*per, b*per + per)
+// instead, so every output segment keeps its input's order.
+#ifndef SPTR_SCHED_CONTIG
+#define SPTR_SCHED_CONTIG 0
+#endif
 struct Sched {
-  uint32_t first, step, per, seg0;
+  uint32_t first, step, per, seg0, end;  // items first + j*step + [0, kBlock), below end
 };
 __device__ __forceinline__ Sched block_sched(uint32_t n) {
   Sched s;
   const uint32_t lb = logical_block();
-  s.first = lb * kBlock;
-  s.step = gridDim.x * kBlock;
-  s.per = (n + s.step - 1) / s.step * kBlock;
+  const uint32_t span = gridDim.x * kBlock;
+  s.per = (n + span - 1) / span * kBlock;
   s.seg0 = lb * s.per;
+  if (SPTR_SCHED_CONTIG) {
+    s.first = s.seg0;
+    s.step = kBlock;
+    s.end = min(n, s.seg0 + s.per);
+  } else {
+    s.first = lb * kBlock;
+    s.step = span;
+    s.end = n;
+  }
   return s;
 }
 
@@ -1137,7 +1150,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   const Sched sd = block_sched(f.P);
   const uint32_t per = sd.per * f.k;  // hit-record segment stride: all samples of the block's pixels
   const uint32_t seg0 = sd.seg0 * f.k;
-  for (uint32_t base = sd.first; base < f.P; base += sd.step) {
+  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
     const uint32_t l = base + threadIdx.x;
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
@@ -1333,7 +1346,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   const RayStream rs = w.rs[depth & 1];
   Visits vc;
   const Sched sd = block_sched(n);
-  for (uint32_t base = sd.first; base < n; base += sd.step) {
+  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
     bool active = i < n, hit = false, culled = false;
     uint32_t id = 0u, pid = 0u, ref = kNoHit;
@@ -1431,8 +1444,8 @@ constexpr int kDynSteps = SPTR_DYN_STEPS;
 #endif
 constexpr bool kDynLds = SPTR_DYN_LDS != 0;
 __device__ __forceinline__ uint32_t block_items(const Sched& sd, uint32_t n) {
-  if (sd.first >= n) return 0u;
-  const uint32_t rest = n - sd.first, full = rest / sd.step, tail = rest - full * sd.step;
+  if (sd.first >= sd.end) return 0u;
+  const uint32_t rest = sd.end - sd.first, full = rest / sd.step, tail = rest - full * sd.step;
   return full * kBlock + (tail < kBlock ? tail : kBlock);
 }
 __device__ __forceinline__ uint32_t block_item(const Sched& sd, uint32_t k) {
@@ -1736,7 +1749,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   const ImageDiv idiv = image_div(f);
   const uint32_t ts = w.tstride, L = w.L;
   const Sched sd = block_sched(n);
-  for (uint32_t base = sd.first; base < n; base += sd.step) {
+  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
     const bool active = i < n;
     bool cont = false, shadow = false, dirty = kPrimary;
@@ -1884,7 +1897,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
   Visits vc;
   uint32_t rays = 0u;
   const Sched sd = block_sched(n);
-  for (uint32_t base = sd.first; base < n; base += sd.step) {
+  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
     bool cont = false, dirty = false, lit = false;
     uint32_t p = 0u, rng = 0u;
@@ -1972,7 +1985,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
   Visits vc;
   uint32_t rays = 0u;
   const Sched sd = block_sched(n);
-  for (uint32_t i = sd.first + threadIdx.x; i < n; i += sd.step) {
+  for (uint32_t i = sd.first + threadIdx.x; i < sd.end; i += sd.step) {
     const float4* task = w.stask + (size_t)seg_slot(s_off, nseg_in, per_in, i) * L * ts;
     bool any = false;
     uint32_t p = 0u;
@@ -2154,10 +2167,11 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ DevMaterial smat[32];
-  __shared__ uint32_t s_rays[2];
+  __shared__ uint32_t s_rays[2], s_next;
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
   const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x < 2u) s_rays[threadIdx.x] = 0u;
+  if (threadIdx.x == 0u) s_next = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
@@ -2166,15 +2180,31 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   Visits vc;
   uint32_t n_closest = 0u, n_shadow = 0u;
   const Sched sd = block_sched(n);
-  for (uint32_t i = sd.first + threadIdx.x; i < n; i += sd.step) {
-    const uint32_t id = seg_slot(s_off, nseg_in, per_in, i);
-    const float4 o4 = rin.o[id], d4 = rin.d[id];
-    vec3 ro = xyz(o4), rd = xyz(d4), thr = xyz(rin.thr[id]);
-    uint32_t rng = __float_as_uint(o4.w);
-    const uint32_t p = __float_as_uint(d4.w);
-    vec3 radv = v3(0.0f, 0.0f, 0.0f);
-    bool loaded = false;  // rad[p] is read at the first update
-    for (uint32_t depth = (uint32_t)depth0; depth < D; ++depth) {
+  const uint32_t nb = block_items(sd, n);
+  // Lanes are refilled per bounce: a lane whose path ended takes the block's next path, so a wave
+  // waits on its slowest lane for one bounce at a time instead of for whole paths.
+  bool have = false, loaded = false;  // loaded: rad[p] is read at the first update
+  vec3 ro, rd, thr, radv;
+  uint32_t rng = 0u, p = 0u, depth = 0u;
+  for (;;) {
+    const uint32_t k = block_take(&s_next, !have);
+    if (!have && k < nb) {
+      const uint32_t id = seg_slot(s_off, nseg_in, per_in, block_item(sd, k));
+      const float4 o4 = rin.o[id], d4 = rin.d[id];
+      ro = xyz(o4);
+      rd = xyz(d4);
+      thr = xyz(rin.thr[id]);
+      rng = __float_as_uint(o4.w);
+      p = __float_as_uint(d4.w);
+      radv = v3(0.0f, 0.0f, 0.0f);
+      loaded = false;
+      depth = (uint32_t)depth0;
+      have = depth < D;
+    }
+    if (__ballot(have) == 0ull) break;  // every lane idle after a take: the block's paths are done
+    if (!have) continue;
+    bool fin = true;
+    do {  // one bounce of this lane's path; fin = false when it continues
       ++n_closest;
       float tfar = __builtin_huge_valf();
       uint32_t ref = kNoHit;
@@ -2209,8 +2239,12 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
       if (!continue_path(sf, rd, depth, thr, rng, no, nd)) break;
       ro = no;
       rd = nd;
+      fin = ++depth >= D;
+    } while (false);
+    if (fin) {
+      if (loaded) w.rad[p] = f4(radv, 0.0f);
+      have = false;
     }
-    if (loaded) w.rad[p] = f4(radv, 0.0f);
   }
   for (int off = 32; off > 0; off >>= 1) {
     n_closest += __shfl_xor(n_closest, off);
@@ -2554,7 +2588,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_PT_WAVES) k_pathtracer(SceneView 
   Visits vc;
   uint32_t n_closest = 0u, n_shadow = 0u;
   const Sched sd = block_sched(f.P);
-  for (uint32_t l = sd.first + threadIdx.x; l < f.P; l += sd.step) {
+  for (uint32_t l = sd.first + threadIdx.x; l < sd.end; l += sd.step) {
     int x = 0, y = 0;
     if (!local_pixel(f, l, x, y)) continue;
     const uint32_t ps = (uint32_t)(y * f.W + x);
@@ -2818,7 +2852,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_PT_WAVES) k_optix(SceneView sv, S
   Visits vc;
   uint32_t n_closest = 0u;
   const Sched sd = block_sched(f.P);
-  for (uint32_t l = sd.first + threadIdx.x; l < f.P; l += sd.step) {
+  for (uint32_t l = sd.first + threadIdx.x; l < sd.end; l += sd.step) {
     int x = 0, y = 0;
     if (!local_pixel(f, l, x, y)) continue;
     const uint32_t pixel = (uint32_t)(y * f.W + x);
