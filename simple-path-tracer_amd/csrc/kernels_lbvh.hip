@@ -12,6 +12,8 @@
 //                   (write-through 8-byte box pairs, drained before one agent-scope exchange that
 //                   also carries the subtree height — the fence-free hand-off of the gfx950 guide,
 //                   Guideline 16 R1)
+//   k_treelet     : (L2/HBM scenes) SAH treelet restructuring after k_refit, bottom-up by subtree height, 3 passes;
+//                   never deepens a subtree (k_heights, k_height_hist / k_height_scatter order the launches)
 //   k_wide_count + scan + k_wide_emit, one wide level at a time (SPTR_WIDE_GREEDY, the default):
 //                   wide BVH (4 or 8 children) by the greedy surface-area collapse — a wide node
 //                   opens its largest-area internal child until it has kWide children; leaves stay
@@ -25,6 +27,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cstring>
+#include <vector>
 #include <rocprim/rocprim.hpp>
 
 #include "sptr_internal.h"
@@ -40,6 +43,12 @@
 #endif
 #ifndef SPTR_WIDE_GREEDY
 #define SPTR_WIDE_GREEDY 1  // 0: every kWideLevels-th LBVH level becomes a wide level (A/B builds)
+#endif
+#ifndef SPTR_TREELET_HCAP
+#define SPTR_TREELET_HCAP 0  // a restructured treelet may deepen its subtree up to this height (A/B builds)
+#endif
+#ifndef SPTR_TREELET
+#define SPTR_TREELET 5  // treelet size (leaves) of the SAH restructuring of L2/HBM scenes' LBVH; 0: off (r03u/v A/B)
 #endif
 
 namespace sptr {
@@ -302,6 +311,307 @@ __global__ void k_refit(int N, const uint32_t* vals, const float4* blo, const fl
       }
       child = par;
       par = nd->link.z;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- treelet restructuring
+// SAH optimisation of the Karras tree by treelet restructuring (Karras & Aila, "Fast Parallel
+// Construction of High-Quality Bounding Volume Hierarchies", HPG 2013), for the scenes traversed from
+// L2/HBM (single-primitive leaves).  Bottom-up, one launch per subtree height: every node of height h
+// grows a treelet of up to kTreeletLeaves leaves below it (repeatedly opening the treelet leaf with the
+// largest surface area), finds the treelet topology of least SAH cost over all subsets of its leaves
+// (dynamic programming, subsets in increasing order, each split enumerated once), and rewrites the
+// treelet's internal nodes if that beats the current topology.  A node's treelet lies inside its own
+// subtree, whose nodes all have smaller heights and were finalised by earlier launches, and the
+// treelets of one launch are disjoint, so the launches need no synchronisation beyond their order.
+// Primitives do not move: only links, child boxes, parents and counts change.  SAH constants: a node
+// visit 1.2, a primitive test 1 (per primitive of a leaf), areas as half surface areas.
+constexpr float kSahNode = 1.2f, kSahPrim = 1.0f;
+constexpr int kTreeletBlock = 64;
+
+struct Box3 {
+  float lo[3], hi[3];
+};
+__device__ __forceinline__ float half_area(const Box3& b) {
+  const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+__device__ __forceinline__ Box3 node_child_box(const BvhNode& n, bool right) {
+  Box3 b;
+  const float4 xy = right ? n.rxy : n.lxy;
+  b.lo[0] = xy.x;
+  b.hi[0] = xy.y;
+  b.lo[1] = xy.z;
+  b.hi[1] = xy.w;
+  b.lo[2] = right ? n.z.z : n.z.x;
+  b.hi[2] = right ? n.z.w : n.z.y;
+  return b;
+}
+__device__ __forceinline__ void box_merge(Box3& a, const Box3& b) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    a.lo[k] = fminf(a.lo[k], b.lo[k]);
+    a.hi[k] = fmaxf(a.hi[k], b.hi[k]);
+  }
+}
+__device__ __forceinline__ Box3 box_empty() {
+  Box3 b;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b.lo[k] = FLT_MAX;
+    b.hi[k] = -FLT_MAX;
+  }
+  return b;
+}
+__device__ __forceinline__ uint32_t prims_of(uint32_t link) { return (link & kLeafRangeMask) + 1u; }
+
+// Subtree heights of the Karras tree (the launch order of the first pass): each primitive walks up,
+// the first child to arrive at a node stops, the second carries max(heights) + 1 on.  The payload is
+// the value of the arrival word itself, so no other data crosses between threads.
+__global__ void k_heights(int N, const uint32_t* leaf_parent, const BvhNode* nodes, uint32_t* flags, uint32_t* height) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    uint32_t par = leaf_parent[i], h = 0u;
+    for (;;) {
+      const uint32_t old = __hip_atomic_exchange(flags + par, h + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == 0u) break;
+      h = max(h, old - 1u) + 1u;
+      height[par] = h;
+      if (par == 0u) break;
+      par = nodes[par].link.z;
+    }
+  }
+}
+
+// Nodes grouped by height (the launch order of a pass): per-block histograms, then a wave-aggregated
+// scatter (one atomic per distinct height in a wave) into the height-ordered node list.
+constexpr uint32_t kMaxHeight = 256;
+__global__ void k_height_hist(uint32_t nn, const uint32_t* label, uint32_t* hist) {
+  __shared__ uint32_t s_h[kMaxHeight];
+  for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x) s_h[i] = 0u;
+  __syncthreads();
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += gridDim.x * blockDim.x)
+    atomicAdd(&s_h[min(label[x], kMaxHeight - 1u)], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x)
+    if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+__global__ void k_height_scatter(uint32_t nn, const uint32_t* label, uint32_t* cursor, uint32_t* order) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t base = blockIdx.x * blockDim.x; base < nn; base += gridDim.x * blockDim.x) {
+    const uint32_t x = base + threadIdx.x;
+    const bool valid = x < nn;
+    const uint32_t h = valid ? min(label[x], kMaxHeight - 1u) : 0u;
+    unsigned long long todo = __ballot(valid);
+    while (todo) {
+      const int leader = __ffsll(todo) - 1;
+      const uint32_t hl = __shfl(h, leader);
+      const unsigned long long m = __ballot(valid && h == hl) & todo;
+      uint32_t b = 0u;
+      if ((int)lane == leader) b = atomicAdd(&cursor[hl], (uint32_t)__popcll(m));
+      b = __shfl(b, leader);
+      if ((m >> lane) & 1ull) order[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = x;
+      todo &= ~m;
+    }
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kTreeletBlock) k_treelet(const uint32_t* order, uint32_t count, BvhNode* nodes,
+                                                            float* cost, uint32_t* newh) {
+  constexpr int S = 1 << K;
+  __shared__ float s_copt[S][kTreeletBlock];     // least SAH cost of a subset of the treelet's leaves
+  __shared__ uint16_t s_part[S][kTreeletBlock];  // its best split (low byte) and height (high byte)
+  __shared__ uint8_t s_sub[K][kTreeletBlock];    // restructuring work list: subsets, node ids, parents
+  __shared__ uint32_t s_id[K][kTreeletBlock];
+  const int t = threadIdx.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + t; i < count; i += gridDim.x * blockDim.x) {
+    const uint32_t x = order[i];
+    const BvhNode nd = nodes[x];
+    // treelet leaves (registers, fully unrolled) and internal nodes (inter[0] = x)
+    uint32_t lk[K], lh[K], lc[K], inter[K];
+    Box3 lb[K];
+    float la[K], lcost[K];
+    int nl = 2;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      lk[j] = kNoHit;
+      lh[j] = lc[j] = inter[j] = 0u;
+      la[j] = lcost[j] = 0.0f;
+      lb[j] = box_empty();
+    }
+    inter[0] = x;
+    lk[0] = nd.link.x;
+    lk[1] = nd.link.y;
+    lb[0] = node_child_box(nd, false);
+    lb[1] = node_child_box(nd, true);
+    la[0] = half_area(lb[0]);
+    la[1] = half_area(lb[1]);
+    for (int ni = 1; nl < K; ++ni) {
+      int best = -1;
+      float ba = -1.0f;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j < nl && !(lk[j] & kLeafBit) && la[j] > ba) {
+          ba = la[j];
+          best = j;
+        }
+      if (best < 0) break;
+      uint32_t m = 0u;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j == best) m = lk[j];
+      const BvhNode c = nodes[m];
+      const Box3 bl = node_child_box(c, false), br = node_child_box(c, true);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (j == best) {
+          lk[j] = c.link.x;
+          lb[j] = bl;
+          la[j] = half_area(bl);
+        }
+        if (j == nl) {
+          lk[j] = c.link.y;
+          lb[j] = br;
+          la[j] = half_area(br);
+        }
+        if (j == ni) inter[j] = m;
+      }
+      ++nl;
+    }
+    // leaf costs, heights and primitive counts
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j >= nl) continue;
+      if (lk[j] & kLeafBit) {
+        lc[j] = prims_of(lk[j]);
+        lcost[j] = kSahPrim * (float)lc[j] * la[j];
+        lh[j] = 0u;
+      } else {
+        lc[j] = nodes[lk[j]].link.w;
+        lcost[j] = cost[lk[j]];
+        lh[j] = newh[lk[j]];
+      }
+    }
+    const int full = (1 << nl) - 1;
+    // the current topology's cost: the node over its two children
+    Box3 ball = lb[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j)
+      if (j < nl) box_merge(ball, lb[j]);
+    const float a_full = half_area(ball);
+    float cur_l, cur_r;
+    uint32_t h_l, h_r;
+    if (nd.link.x & kLeafBit) {
+      const Box3 b = node_child_box(nd, false);
+      cur_l = kSahPrim * (float)prims_of(nd.link.x) * half_area(b);
+      h_l = 0u;
+    } else {
+      cur_l = cost[nd.link.x];
+      h_l = newh[nd.link.x];
+    }
+    if (nd.link.y & kLeafBit) {
+      const Box3 b = node_child_box(nd, true);
+      cur_r = kSahPrim * (float)prims_of(nd.link.y) * half_area(b);
+      h_r = 0u;
+    } else {
+      cur_r = cost[nd.link.y];
+      h_r = newh[nd.link.y];
+    }
+    const float cur = kSahNode * a_full + cur_l + cur_r;
+    if (nl <= 2) {  // nothing to rearrange
+      cost[x] = cur;
+      newh[x] = max(h_l, h_r) + 1u;
+      continue;
+    }
+    // dynamic programming over the leaf subsets
+    for (int sb = 1; sb <= full; ++sb) {
+      if ((sb & (sb - 1)) == 0) {  // one leaf
+        float c = 0.0f;
+        uint32_t h = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (sb == (1 << j)) {
+            c = lcost[j];
+            h = lh[j];
+          }
+        s_copt[sb][t] = c;
+        s_part[sb][t] = (uint16_t)(h << 8);
+        continue;
+      }
+      Box3 b = box_empty();
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if ((sb >> j) & 1) box_merge(b, lb[j]);
+      const int low = sb & -sb;
+      float best = FLT_MAX;
+      int bp = 0;
+      for (int q = (sb - 1) & sb; q > 0; q = (q - 1) & sb) {
+        if (!(q & low)) continue;
+        const float c = s_copt[q][t] + s_copt[sb ^ q][t];
+        if (c < best) {
+          best = c;
+          bp = q;
+        }
+      }
+      const uint32_t h = max(s_part[bp][t] >> 8, s_part[sb ^ bp][t] >> 8) + 1u;
+      s_copt[sb][t] = kSahNode * half_area(b) + best;
+      s_part[sb][t] = (uint16_t)((h << 8) | (uint32_t)bp);
+    }
+    const float opt = s_copt[full][t];
+    // kept unless cheaper and no deeper: the traversal stacks are sized by the tree height (the wide
+    // collapse of a deeper tree can exceed the BVH4 stack bound, sptr_internal.h kStack)
+    const uint32_t h_old = max(h_l, h_r) + 1u, h_new = (uint32_t)(s_part[full][t] >> 8);
+    if (!(opt < cur * 0.99999f) || (h_new > h_old && h_new > (uint32_t)SPTR_TREELET_HCAP)) {
+      cost[x] = cur;
+      newh[x] = max(h_l, h_r) + 1u;
+      continue;
+    }
+    // rewrite the treelet's internal nodes top-down; the root keeps its id and parent
+    s_sub[0][t] = (uint8_t)full;
+    s_id[0][t] = x;
+    int n = 1;
+    const uint32_t parent_x = nd.link.z;
+    for (int k = 0; k < n; ++k) {
+      const int sb = s_sub[k][t];
+      const uint32_t id = s_id[k][t];
+      const int p = s_part[sb][t] & 0xFF, qs = sb ^ p;
+      uint32_t link[2], cnt = 0u;
+      Box3 bx[2];
+      for (int side = 0; side < 2; ++side) {
+        const int ts = side ? qs : p;
+        bx[side] = box_empty();
+        uint32_t c = 0u, lkj = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if ((ts >> j) & 1) {
+            box_merge(bx[side], lb[j]);
+            c += lc[j];
+            lkj = lk[j];
+          }
+        cnt += c;
+        if ((ts & (ts - 1)) == 0) {
+          link[side] = lkj;  // a treelet leaf keeps its link (and its subtree)
+        } else {
+          uint32_t cid = 0u;
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (j == n) cid = inter[j];
+          s_sub[n][t] = (uint8_t)ts;
+          s_id[n][t] = cid;
+          ++n;
+          link[side] = cid;
+          nodes[cid].link.z = id;
+        }
+      }
+      BvhNode o;
+      o.lxy = make_float4(bx[0].lo[0], bx[0].hi[0], bx[0].lo[1], bx[0].hi[1]);
+      o.rxy = make_float4(bx[1].lo[0], bx[1].hi[0], bx[1].lo[1], bx[1].hi[1]);
+      o.z = make_float4(bx[0].lo[2], bx[0].hi[2], bx[1].lo[2], bx[1].hi[2]);
+      o.link = make_uint4(link[0], link[1], k == 0 ? parent_x : nodes[id].link.z, cnt);
+      nodes[id] = o;
+      cost[id] = s_copt[sb][t];
+      newh[id] = (uint32_t)(s_part[sb][t] >> 8);
     }
   }
 }
@@ -853,6 +1163,45 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       LB_CHECK(hipGetLastError());
       LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
       LB_CHECK(hipStreamSynchronize(s));
+#if SPTR_TREELET
+      // SAH treelet restructuring (k_treelet) for the single-primitive-leaf trees of L2/HBM scenes:
+      // launch h rewrites the nodes of height h; each pass's new heights order the next pass
+      if (leaf_max == 1u && N >= 3u && c.treelet_passes > 0u) {
+        uint32_t *lab = nullptr, *nh = nullptr, *order = nullptr, *hist = nullptr;
+        float* cst = nullptr;
+        LB_CHECK(tmp.alloc(&lab, N));
+        LB_CHECK(tmp.alloc(&nh, N));
+        LB_CHECK(tmp.alloc(&order, N));
+        LB_CHECK(tmp.alloc(&hist, kMaxHeight));
+        LB_CHECK(tmp.alloc(&cst, N));
+        LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
+        hipLaunchKernelGGL(k_heights, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_parent, nodes, rflags, lab);
+        LB_CHECK(hipGetLastError());
+        const uint32_t nn = N - 1u;
+        std::vector<uint32_t> hh(kMaxHeight), off(kMaxHeight);
+        for (uint32_t pass = 0; pass < c.treelet_passes; ++pass) {
+          LB_CHECK(hipMemsetAsync(hist, 0, kMaxHeight * 4, s));
+          hipLaunchKernelGGL(k_height_hist, dim3(blocks_for(nn)), dim3(256), 0, s, nn, lab, hist);
+          LB_CHECK(hipMemcpyAsync(hh.data(), hist, kMaxHeight * 4, hipMemcpyDeviceToHost, s));
+          LB_CHECK(hipStreamSynchronize(s));
+          uint32_t run = 0u;
+          for (uint32_t h = 0; h < kMaxHeight; ++h) {
+            off[h] = run;
+            run += hh[h];
+          }
+          LB_CHECK(hipMemcpyAsync(hist, off.data(), kMaxHeight * 4, hipMemcpyHostToDevice, s));
+          hipLaunchKernelGGL(k_height_scatter, dim3(blocks_for(nn)), dim3(256), 0, s, nn, lab, hist, order);
+          for (uint32_t h = 1; h < kMaxHeight; ++h)
+            if (hh[h])
+              hipLaunchKernelGGL(k_treelet<SPTR_TREELET>, dim3((hh[h] + kTreeletBlock - 1) / kTreeletBlock),
+                                 dim3(kTreeletBlock), 0, s, order + off[h], hh[h], nodes, cst, nh);
+          LB_CHECK(hipGetLastError());
+          LB_CHECK(hipMemcpyAsync(&dep, nh, 4, hipMemcpyDeviceToHost, s));  // the root's new height
+          LB_CHECK(hipStreamSynchronize(s));
+          std::swap(lab, nh);
+        }
+      }
+#endif
     }
     c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;

@@ -63,6 +63,9 @@ constexpr int kMaxDepth = 32;
 // (kTotStackOverflow), never silent.
 constexpr int kStack = kWide == 8 ? 112 : 96;
 constexpr int kBlock = 256;
+#ifndef SPTR_TREELET_PASSES
+#define SPTR_TREELET_PASSES 3
+#endif
 constexpr uint32_t kLdsSceneBytes = 48 * 1024;  // scenes up to this size are staged whole into LDS
 
 // BVH2 node, 64 B: both child boxes + child links.  Link: internal node index, or a leaf range.
@@ -321,6 +324,7 @@ struct Context {
   uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..16); 0 = automatic
   uint32_t bvh_width = 0;  // traversal width: 2 (LBVH as built), 4 (collapsed), 0 = automatic
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
+  uint32_t treelet_passes = SPTR_TREELET_PASSES;  // SAH treelet passes over L2/HBM scenes' LBVH (kernels_lbvh.hip)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_nodes4 = 0, root4 = 0;
   uint32_t num_top4 = 0;  // wide nodes numbered first: the top kTopLevels levels

@@ -5,7 +5,7 @@
       the same flat scene and faces;
   C4  3840x2160: pixel/tile indexing and the 8-way interleaved shard union at full 4K size, and the
       whole 4K frame (2 spp) vs the oracle;
-  C5  the 10M-triangle sphere mesh at full tessellation (1250 x 4000; BVH height ~45, BVH4 traversed
+  C5  the 10M-triangle sphere mesh at full tessellation (1250 x 4000; BVH height ~41, BVH4 traversed
       from HBM): first hits on camera + random rays and a small render vs the oracle with its own BVH.
 
 Tolerances as in test_gpu_parity.py's docstring (bit-exact first hits >= 99.99 %, images >= 99.9 %

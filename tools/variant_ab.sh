@@ -8,5 +8,5 @@ for v in "$@"; do
   lib=$GRAFT_REPO_ROOT/variants/$v/libsptr_hip.so; [ "$v" = tree ] && lib=$GRAFT_REPO_ROOT/simple-path-tracer_amd/libsptr_hip.so
   SPTR_LIB=$lib timeout -k 10 300 python3 bench.py --workload $wl --steps 5 --warmup 1 \
     --no-cpu-baseline --no-interactive --stage-timing > $o/${wl}_$v.json 2> $o/${wl}_$v.err
-  python3 -c "import json;d=json.loads(open('$o/${wl}_$v.json').read().splitlines()[-1]);print('$wl $v',d['ms_per_step'],d['stage_ms_per_step'])"
+  python3 -c "import json;d=json.loads(open('$o/${wl}_$v.json').read().splitlines()[-1]);sc=d.get('scene',{});print('$wl $v',d['ms_per_step'],d['stage_ms_per_step'],{k:sc[k] for k in ('bvh_depth','bvh_width','lbvh_build_ms') if k in sc})"
 done
