@@ -1043,10 +1043,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   c.num_sph = nsph;
   c.num_nodes = N > 1 ? N - 1 : 0;
   c.bvh_depth = 0;
-  LB_CHECK(realloc_buf(c.tris, (size_t)ntris * 48));
+  // + 64 B: the unified wide walk (wide_walk_u) reads a node's 56 B from a direct leaf's primitive address
+  LB_CHECK(realloc_buf(c.tris, (size_t)ntris * 48 + 64));
   LB_CHECK(realloc_buf(c.tri_geom, (size_t)ntris * 4));
   LB_CHECK(realloc_buf(c.tri_orig, (size_t)ntris * 4));
-  LB_CHECK(realloc_buf(c.sph, (size_t)nsph * 16));
+  LB_CHECK(realloc_buf(c.sph, (size_t)nsph * 16 + 64));
   LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));

@@ -585,7 +585,7 @@ struct WideWalk {
 // top / ntop: an LDS copy of the wide nodes 0..ntop-1 (the top kTopLevels levels, stage_top), read
 // instead of L2/HBM for those indices (ntop = 0: every node from `nodes`).
 template <bool kAny, bool kCount, int N>
-__device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
+__device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
                                           uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
                                           const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
   for (int it = 0; it < steps; ++it) {
@@ -672,6 +672,128 @@ __device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, con
     }
   }
   return false;
+}
+// The same traversal with one fetch per lane per step (SPTR_WALK_UNIFIED): a step visits one item,
+// an internal node or a leaf.  A node's hit children — leaves included — are ordered like internal
+// children (the nearest is visited next, the others pushed), so a leaf's primitive is tested on a
+// step of its own.  Every lane issues its step's loads from one selected address (the node's 56 B,
+// or a direct leaf's triangle / sphere record; the primitive buffers carry a 64-B tail so that the
+// node-sized read stays in bounds) before any lane branches, so a wave waits for one memory latency
+// per step, where wide_walk serialises a latency per hit leaf child inside the node's step.  Range
+// leaves (leaf size > 1) are tested with leaf_test on their step.  Same hits: the closest hit is the
+// minimum over the same set of primitives tested against the same rays (ties at exactly equal t
+// may resolve to another primitive, as with any change of traversal order).
+#ifndef SPTR_WALK_UNIFIED
+#define SPTR_WALK_UNIFIED 1
+#endif
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
+                                            uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                            const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  static_assert(kWide == 4, "unified walk: 4-wide nodes");
+  for (int it = 0; it < steps; ++it) {
+    const uint32_t cur = wk.cur;
+    const bool leaf = (cur & kLeafBit) != 0u;
+    const bool direct = (cur & (kLeafBit | kLeafDirect)) == (kLeafBit | kLeafDirect);
+    const bool dsph = direct && (cur & kLeafDirectSphere) != 0u;
+    const uint32_t slot = (cur & ~kLeafBit) >> kLeafCountBits;
+    const uint4* a = !leaf ? reinterpret_cast<const uint4*>(nodes + cur)
+                           : (dsph ? reinterpret_cast<const uint4*>(sph + slot)
+                                   : reinterpret_cast<const uint4*>(tris + (direct ? 3u * slot : 0u)));
+    uint4 h, l4, q4;
+    uint2 q2;
+    if (cur < ntop) {
+      const uint4* t = top + 4u * cur;
+      h = t[0];
+      l4 = t[1];
+      q4 = t[2];
+      q2 = *reinterpret_cast<const uint2*>(t + 3);
+      asm volatile("" ::"v"(h.x), "v"(l4.x), "v"(q4.x), "v"(q2.x));
+    } else {
+      h = a[0];
+      l4 = a[1];
+      q4 = a[2];
+      q2 = *reinterpret_cast<const uint2*>(a + 3);
+    }
+    if (leaf) {
+      bool hit = false;
+      if (direct) {
+        const float4 p0 = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
+        float t;
+        if (dsph) {
+          if (kCount) ++vc.sph;
+          if (kAny) hit = sphere_occ(p0, r, tnear, tfar);
+          else if (sphere_hit(p0, r, tnear, tfar, t)) {
+            tfar = t;
+            ref = slot | kSphereBit;
+            hit = true;
+          }
+        } else {
+          if (kCount) ++vc.tris;
+          const float4 p1 = make_float4(__uint_as_float(l4.x), __uint_as_float(l4.y), __uint_as_float(l4.z), __uint_as_float(l4.w));
+          const float4 p2 = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z), __uint_as_float(q4.w));
+          if (tri_hit4(p0, p1, p2, r, tnear, tfar, t)) {
+            if (!kAny) {
+              tfar = t;
+              ref = slot;
+            }
+            hit = true;
+          }
+        }
+      } else {
+        hit = leaf_test<kAny, kCount>(cur, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
+      }
+      if (hit) {
+        wk.hit = true;
+        if (kAny) return true;
+      }
+      if (wk.sp == 0) return true;
+      wk.cur = stack.get(--wk.sp);
+      continue;
+    }
+    const uint32_t ln[4] = {l4.x, l4.y, l4.z, l4.w};
+    const uint32_t qw[6] = {q4.x, q4.y, q4.z, q4.w, q2.x, q2.y};
+    if (kCount) ++vc.nodes;
+    const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0, qw + 1, r.o.x, r.inv.x);
+    const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2, qw + 3, r.o.y, r.inv.y);
+    const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4, qw + 5, r.o.z, r.inv.z);
+    float t[4];
+    bool hc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) && ln[k] != kNoHit;
+    int kn = 4;
+    float tn = __builtin_huge_valf();
+    uint32_t npush = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
+      if (hc[k] && (kn == 4 || better)) {
+        tn = t[k];
+        kn = k;
+      }
+      npush += hc[k] ? 1u : 0u;
+    }
+    if (kn < 4) {
+      if (wk.sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
+#pragma unroll
+      for (int k = 3; k >= 0; --k)
+        if (hc[k] && k != kn && wk.sp < kStack) stack.put(wk.sp++, ln[k]);
+      wk.cur = ln[kn];
+    } else {
+      if (wk.sp == 0) return true;
+      wk.cur = stack.get(--wk.sp);
+    }
+  }
+  return false;
+}
+// kU: the unified walk (default SPTR_WALK_UNIFIED); callers choose per ray class (see the kernels)
+template <bool kAny, bool kCount, bool kU = (SPTR_WALK_UNIFIED != 0), int N>
+__device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
+                                          uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                          const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  if constexpr (kU && kWide == 4)
+    return wide_walk_u<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
+  return wide_walk_inl<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
 }
 // Starts a walk at root; true when it is already over (empty scene, or a root leaf tested here).
 template <bool kAny, bool kCount>
@@ -1415,12 +1537,12 @@ __device__ __forceinline__ bool walk_start(WideWalk& wk, const Staged& sc, uint3
                                            float& tfar, uint32_t& ref, Visits& vc) {
   return wide_start<kAny, kCount>(wk, root, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc);
 }
-template <bool kAny, bool kCount, bool kW4, int N>
+template <bool kAny, bool kCount, bool kW4, bool kU = (SPTR_WALK_UNIFIED != 0), int N>
 __device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const uint4* top,
                                            uint32_t ntop, const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
                                            int steps) {
   if (kW4)
-    return wide_walk<kAny, kCount>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
+    return wide_walk<kAny, kCount, kU>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
                                    steps);
   return bvh2_walk<kAny, kCount>(wk.cur, wk.sp, wk.hit, stack, sc.nodes, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref,
                                  vc, steps);
@@ -1529,7 +1651,12 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
       continue;                                       // only invalid (outside-image) items taken
     }
-    if (have && !done) done = walk_steps<false, kCount, kW4>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc, kDynSteps);
+    // camera rays keep the leaf-inline walk: coherent lanes reach their leaves together, and testing a
+    // node's leaves before descending tightens tfar early (r03x A/B: C5 bounce 0 2.15 ms inline vs 2.37
+    // unified; bounces 1-2 3.06 vs 2.71)
+    if (have && !done)
+      done = walk_steps<false, kCount, kW4, !kPrimary && SPTR_WALK_UNIFIED>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
+                                                                          kDynSteps);
     const bool fin = have && done;
     if (kCount && fin && v0 != ~0u) hist_ray(s_hist, vc.nodes - v0);
     if (fin && !wk.hit) {
@@ -2132,9 +2259,12 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
       if (!more) break;  // every lane idle and nothing left to take
       continue;          // only unlit tasks taken
     }
+    // the unified walk for scenes beyond an XCD's L2 (kQueue): one memory latency per step instead of one
+    // per hit leaf (r03x A/B: C5 shadow 2.65 -> 2.12 ms/step); L2-resident scenes keep the leaf-inline
+    // walk, whose serial leaf fetches are L2 hits (C3 0.30 inline vs 0.35 unified)
     if (have && !done)
-      done = wide_walk<true, kCount>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris, sv.sph, r, 1e-4f, tfar, ref,
-                                     vc, kDynSteps);
+      done = wide_walk<true, kCount, kQueue && SPTR_WALK_UNIFIED>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris,
+                                                                   sv.sph, r, 1e-4f, tfar, ref, vc, kDynSteps);
     if (have && done) {
       if (kCount) hist_ray(s_hist, vc.nodes - v0);
       if (!wk.hit) w.rad[p] = f4(xyz(w.rad[p]) + contrib, 0.0f);
