@@ -56,7 +56,7 @@ XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 128, "c4": 64, "c5": 64}  # ~1-4 s per run on 16 host threads
 # experiment knobs of the library and the build (timing studies only); a bench line records any that
 # is set, so a stray variable cannot silently change a measured number
-KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU")
+KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU", "SPTR_OVERLAP")
 
 
 class _DevArray:
@@ -373,6 +373,8 @@ def main():
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
+    ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1],
+                    help="0: replay captured launch graphs (default); 1: direct launches (timing studies)")
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="timing experiment on one GPU: render only shard 0 of G (the per-rank work of a G-GPU run); "
                          "the line is marked emulated and is not a G-GPU measurement")
@@ -425,6 +427,8 @@ def main():
         r.set_bvh_width(args.bvh_width)
     if args.tail_depth:
         r.set_tail_depth(args.tail_depth)
+    if args.launch_mode:
+        r.set_launch_mode(args.launch_mode)
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
     cam = workloads.camera(wl)
@@ -523,6 +527,8 @@ def main():
                     for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum", "cull")
                               if args.stage_timing else ("trace0", "trace", "shadow", "cull"))}
         knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
+        if args.launch_mode:
+            knobs["launch_mode"] = args.launch_mode
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),

@@ -1580,10 +1580,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt, s_next;
+  __shared__ uint32_t s_cnt, s_next, s_hits;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
-  if (threadIdx.x == 0) s_cnt = s_next = 0u;
+  if (threadIdx.x == 0) s_cnt = s_next = s_hits = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   const uint32_t ntop = (kW4 && !kLds) ? sv.num_top4 : 0u;
@@ -1612,6 +1612,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   bool have = false, done = false;
   uint32_t id = 0u, pid = 0u, ref = kNoHit;
   uint32_t v0 = 0u;  // kCount: the lane's node visits when its current ray started
+#ifdef SPTR_EXPERIMENT_STEP_CAP  // timing experiment only (wrong hits): a ray ends after this many refill rounds
+  uint32_t rounds = 0u;
+#endif
   float tfar = 0.0f;
   Ray r;
   WideWalk wk;
@@ -1642,6 +1645,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         tfar = __builtin_huge_valf();
         ref = kNoHit;
         if (kCount) v0 = culled ? ~0u : vc.nodes;  // culled camera rays are not traversals
+#ifdef SPTR_EXPERIMENT_STEP_CAP
+        rounds = 0u;
+#endif
         done = walk_start<false, kCount, kW4>(wk, sc, culled ? kNoHit : (kW4 ? sv.root4 : sv.root), r, 0.0f, tfar, ref,
                                               vc);
         have = true;
@@ -1657,10 +1663,16 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     if (have && !done)
       done = walk_steps<false, kCount, kW4, !kPrimary && SPTR_WALK_UNIFIED>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
                                                                           kDynSteps);
+#ifdef SPTR_EXPERIMENT_STEP_CAP
+    if (have && !done && ++rounds >= (uint32_t)SPTR_EXPERIMENT_STEP_CAP) done = true;
+#endif
     const bool fin = have && done;
     if (kCount && fin && v0 != ~0u) hist_ray(s_hist, vc.nodes - v0);
+    const bool defer = !kPrimary && w.defer_miss != 0u;
     if (fin && !wk.hit) {
-      if (sh.debug_mode == 1) {
+      if (defer) {  // the miss record's slot carries thr * env (k_shade adds it to rad[pid])
+        if (sh.debug_mode != 1) rs.thr[id] = f4(xyz(rs.thr[id]) * env_color<kCube>(sh, safe_renormalize_dir(r.d)), 0.0f);
+      } else if (sh.debug_mode == 1) {
         w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       } else {
         const vec3 e = env_color<kCube>(sh, safe_renormalize_dir(r.d));
@@ -1670,15 +1682,20 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         w.rad[pid] = f4(rv, 0.0f);
       }
     }
-    const uint32_t j = block_append(&s_cnt, fin && wk.hit);
-    if (fin && wk.hit) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec.put(sd.seg0 + j, id, __float_as_uint(tfar), ref);
+    const bool rec = fin && (wk.hit || defer);
+    const uint32_t j = block_append(&s_cnt, rec);
+    if (kCount) {
+      const uint32_t nh = (uint32_t)__popcll(__ballot(fin && wk.hit));
+      if (nh && lane_id() == 0u) atomicAdd(&s_hits, nh);
+    }
+    if (rec) {
+      if (sd.seg0 + j < w.hrec_cap) w.hrec.put(sd.seg0 + j, id, wk.hit ? __float_as_uint(tfar) : pid, wk.hit ? ref : kNoHit);
       else w.tot[kTotOverflow] = 1ull;
     }
     if (fin) have = false;
   }
   seg_publish(w.segH, &s_cnt, sd.per);
-  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kPrimary ? kTotHitP : kTotHitB], (unsigned long long)s_cnt);
+  if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kPrimary ? kTotHitP : kTotHitB], (unsigned long long)s_hits);
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotNodes);
@@ -1878,14 +1895,22 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   const Sched sd = block_sched(n);
   for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
     const uint32_t i = base + threadIdx.x;
-    const bool active = i < n;
+    bool active = i < n;
     bool cont = false, shadow = false, dirty = kPrimary;
     uint32_t p = 0u, rng = 0u;
     vec3 rd, thr, radv = v3(0.0f, 0.0f, 0.0f), no, nd;
     Surface sf;
+    uint3 h = make_uint3(0u, 0u, 0u);
+    if (active) w.hrec.get(seg_slot(s_off, nseg_in, per_in, i), h.x, h.y, h.z);
+    if (!kPrimary && active && h.z == kNoHit) {
+      // a deferred miss of this bounce's trace (WaveView::defer_miss): rad[p] + thr * env, the update
+      // the trace makes itself otherwise (record: slot, path id, kNoHit; the slot's throughput holds
+      // thr * env)
+      p = h.y;
+      w.rad[p] = sh.debug_mode == 1 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : f4(xyz(w.rad[p]) + xyz(rin.thr[h.x]), 0.0f);
+      active = false;
+    }
     if (active) {
-      uint3 h;
-      w.hrec.get(seg_slot(s_off, nseg_in, per_in, i), h.x, h.y, h.z);
       vec3 ro;
       if (kPrimary) {
         Primary pr;
@@ -3277,6 +3302,12 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         }(fl);
       },
       Flags<>{}, L, count, P, W, cube);
+}
+
+// the any-hit stage runs as k_shadow_dyn and the bounce traces as k_trace_dyn (scenes traversed from
+// L2/HBM, one light): the pair enqueue_wavefront overlaps (bounce traces defer their misses to k_shade)
+bool shadow_overlaps(const SceneView& sv, const WaveView& w) {
+  return sv.lds_bytes == 0 && sv.width == (uint32_t)kWide && w.L == 1u && !no_dyn();
 }
 
 bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count) {

@@ -166,6 +166,7 @@ WaveView wave_view(Context& c) {
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
+  w.defer_miss = 0u;
   w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
   w.hrec_cap = (uint32_t)hcap;
   return w;
@@ -466,7 +467,7 @@ constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
-  const WaveView w = wave_view(c);
+  WaveView w = wave_view(c);
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
@@ -492,6 +493,24 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   }
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
+  // launches overlapped on a second stream (SPTR_OVERLAP=0: everything on s, for A/B timing)
+  static const bool overlap = [] {
+    const char* e = getenv("SPTR_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  hipStream_t side = s == c.cap_stream ? c.cap_side : c.side_stream;
+  bool join = false, join_sky = false;  // pending side-stream work: shadow(d) (ev_join), k_sky (ev_sky)
+  auto fork_err = [&](hipError_t e) {
+    if (e != hipSuccess && tm.err == hipSuccess) tm.err = e;
+  };
+  // any-hit launches of their own (k_shadow_dyn: scenes traversed from L2/HBM) run on the side stream
+  // beside the next bounce's trace: shadow(d) only adds to rad[], which the bounce traces then leave
+  // alone (misses deferred to k_shade, WaveView::defer_miss); k_shade(d + 1) overwrites the shadow
+  // tasks and updates rad[], so it, the tail and k_accum wait for shadow(d) (ev_join)
+  const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, w);
+  w.defer_miss = shadow_side ? 1u : 0u;
+  StageTimer tside{c, tm.on, tm.trace_only, side};
+  tside.capturing = tm.capturing;
   while (done < f.spp) {
     const uint32_t kk = std::min<uint32_t>(k, f.spp - done);
     fv.k = kk;
@@ -511,6 +530,9 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     SegTable rays_tab = w.segN, spare_tab = w.segH;
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
+        if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));
+        if (join_sky) fork_err(hipStreamWaitEvent(s, c.ev_sky, 0));
+        join = join_sky = false;
         WaveView wt = w;
         wt.segN = rays_tab;
         tm.begin(7);
@@ -529,17 +551,38 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         continue;
       }
       if (d == 0 && fv.sky_fold) {  // the culled pixels' environment sums: accumulation, not k_trace
-        tm.begin(4);
-        launch_sky(sh, fv, s);
-        tm.end();
+        if (overlap) {
+          // on the side stream, concurrent with the bounce-0 trace (it writes only the culled pixels'
+          // accum words, which nothing reads before this batch's k_accum, the join point): its VALU-bound
+          // blocks fill the CUs the latency-bound trace leaves idle, above all in the trace's tail
+          fork_err(hipEventRecord(c.ev_fork, s));
+          fork_err(hipStreamWaitEvent(side, c.ev_fork, 0));
+          launch_sky(sh, fv, side);
+          fork_err(hipEventRecord(c.ev_sky, side));
+          join_sky = true;
+        } else {
+          tm.begin(4);
+          launch_sky(sh, fv, s);
+          tm.end();
+        }
       }
       tm.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
+      if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));  // shadow(d - 1) (and k_sky) before shade(d)
+      join = false;
       tm.begin(d == 0 ? 6 : 2);
       g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
       tm.end();
-      if (!fuse) {
+      if (!fuse && shadow_side) {
+        fork_err(hipEventRecord(c.ev_fork, s));
+        fork_err(hipStreamWaitEvent(side, c.ev_fork, 0));
+        tside.begin(3);
+        launch_shadow(sv, sh, w, d, count, g_shade, side);
+        tside.end();
+        fork_err(hipEventRecord(c.ev_join, side));
+        join = true;
+      } else if (!fuse) {
         tm.begin(3);
         launch_shadow(sv, sh, w, d, count, g_shade, s);
         tm.end();
@@ -548,6 +591,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     // the call's last batch resolves in the same launch (k_accum<true>: each thread resolves the
     // sum it holds, as k_resolve would next)
     const bool resolve = done + kk >= f.spp && !(f.flags & SPTR_FRAME_NO_RESOLVE);
+    if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));
+    if (join_sky) fork_err(hipStreamWaitEvent(s, c.ev_sky, 0));
+    join = join_sky = false;
+    if (tside.err != hipSuccess && tm.err == hipSuccess) tm.err = tside.err;
     tm.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
                       static_cast<uint8_t*>(c.image.p), resolve, s);
@@ -753,7 +800,15 @@ int sptr_create(int device, sptr_ctx** out) {
   Context& c = x->c;
   c.device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess ||
+      // the side streams at the lowest priority: a priority of its own puts a stream on a hardware
+      // queue of its own, so that its launches can run beside the main sequence's
+      hipDeviceGetStreamPriorityRange(&c.prio_lo, &c.prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c.side_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c.cap_side, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
+      hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c.ev_sky, hipEventDisableTiming) != hipSuccess) {
     delete x;
     return SPTR_ERR_HIP;
   }
@@ -785,6 +840,11 @@ int sptr_destroy(sptr_ctx* x) {
   for (hipEvent_t e : c.events) (void)hipEventDestroy(e);
   if (c.stream) (void)hipStreamDestroy(c.stream);
   if (c.cap_stream) (void)hipStreamDestroy(c.cap_stream);
+  if (c.side_stream) (void)hipStreamDestroy(c.side_stream);
+  if (c.cap_side) (void)hipStreamDestroy(c.cap_side);
+  if (c.ev_fork) (void)hipEventDestroy(c.ev_fork);
+  if (c.ev_join) (void)hipEventDestroy(c.ev_join);
+  if (c.ev_sky) (void)hipEventDestroy(c.ev_sky);
   delete x;
   return SPTR_OK;
 }

@@ -269,6 +269,10 @@ struct WaveView {
   uint32_t hrec_cap;  // hit records allocated (bounce 0 segments span k samples per pixel slot)
   uint32_t L;        // lights (tasks per shaded path)
   uint32_t tstride;  // float4 slots per shadow task: 2, or 3 when a point light is present
+  // bounce traces (k_trace_dyn, d >= 1) defer a miss's radiance update to the next k_shade: the ray
+  // slot's throughput becomes thr * env and a record with prim kNoHit is queued, so that no kernel of
+  // the bounce but k_shade writes rad[] and k_shadow_dyn(d - 1) may run beside it (enqueue_wavefront)
+  uint32_t defer_miss;
 };
 
 struct DevBuf {
@@ -309,6 +313,11 @@ struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t cap_stream = nullptr;  // launch-graph capture
+  // second streams for launches that overlap the main sequence (direct launches / inside a capture),
+  // forked from and joined back into it by ev_fork / ev_join (enqueue_wavefront)
+  hipStream_t side_stream = nullptr, cap_side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sky = nullptr;
+  int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
   uint32_t launch_mode = 0;          // 0: replay a captured graph for repeated call shapes; 1: direct launches
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
@@ -380,6 +389,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
                   uint32_t nseg_in, hipStream_t s);
 // k_shade traces the shadow ray in place (LDS-staged one-light scenes outside the visit-count pass)
 bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count);
+bool shadow_overlaps(const SceneView& sv, const WaveView& w);
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                       uint32_t nseg, bool fuse, hipStream_t s);
 // one fused bounce (k_bounce): rays of w.segN in, continuation rays of w.segH out
