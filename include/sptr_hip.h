@@ -218,9 +218,15 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
  * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument;
- * 1: direct kernel launches for every call.  Results are identical either way. */
+ * 1: direct kernel launches for every call; 2: direct launches, all on the render stream (no launch
+ * overlapped on the context's second stream).  Results are identical in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
-/* Traversal width: 2 (the LBVH as built), 4 (collapsed to 128-B BVH4 nodes), or 0 = automatic (the
+/* Sample-batch lanes of a wavefront call: 2 runs consecutive batches of the call's samples at the same
+ * time on two buffer sets and streams (scenes traversed from L2/HBM only; each lane holds half the
+ * batch); 1 keeps one batch at a time; 0 = automatic (the default: 1 — two lanes measured slower on
+ * MI355X).  Results are identical either way (tests/test_gpu_configs.py::test_c3_batches_bit_exact). */
+int sptr_set_lanes(sptr_ctx* ctx, uint32_t lanes);
+/* Traversal width: 2 (the LBVH as built), 4 (collapsed to 64-B quantised BVH4 nodes), or 0 = automatic (the
  * default: 2 for scenes staged in LDS, 4 otherwise). */
 int sptr_set_bvh_width(sptr_ctx* ctx, uint32_t width);
 

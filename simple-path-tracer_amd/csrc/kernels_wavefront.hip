@@ -387,6 +387,15 @@ __device__ __forceinline__ bool sphere_occ(float4 s, const Ray& r, float tnear, 
   return (t1 > tnear && t1 < tfar) || (t2 > tnear && t2 < tfar);
 }
 
+// Closest-hit order of candidate hits: by t, then by primitive reference (a hit at exactly the current
+// distance replaces the current one only if its reference is smaller).  With it the closest hit is the
+// minimum over the primitives a ray intersects, whatever order they are tested in — so traversal order
+// cannot change a result.  (Embree keeps the later of two
+// hits at equal t; such exact ties are the documented parity residue.)
+__device__ __forceinline__ bool closer(float t, uint32_t pr, float tfar, uint32_t ref) {
+  return t < tfar || (t == tfar && pr < ref);
+}
+
 struct Visits {
   uint32_t nodes = 0, tris = 0, sph = 0;
   uint32_t stack_overflow = 0;  // a push was dropped (reported through kTotStackOverflow)
@@ -411,7 +420,7 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
       const float4 s = sph[idx];
       if (kAny) {
         if (sphere_occ(s, r, tnear, tfar)) return true;
-      } else if (sphere_hit(s, r, tnear, tfar, t)) {
+      } else if (sphere_hit(s, r, tnear, tfar, t) && closer(t, pr, tfar, ref)) {
         tfar = t;
         ref = pr;
         hit = true;
@@ -420,9 +429,11 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
       if (kCount) ++vc.tris;
       if (tri_hit(tris, idx, r, tnear, tfar, t)) {
         if (kAny) return true;
-        tfar = t;
-        ref = pr;
-        hit = true;
+        if (closer(t, pr, tfar, ref)) {
+          tfar = t;
+          ref = pr;
+          hit = true;
+        }
       }
     }
   }
@@ -723,7 +734,7 @@ __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, c
         if (dsph) {
           if (kCount) ++vc.sph;
           if (kAny) hit = sphere_occ(p0, r, tnear, tfar);
-          else if (sphere_hit(p0, r, tnear, tfar, t)) {
+          else if (sphere_hit(p0, r, tnear, tfar, t) && closer(t, slot | kSphereBit, tfar, ref)) {
             tfar = t;
             ref = slot | kSphereBit;
             hit = true;
@@ -733,11 +744,13 @@ __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, c
           const float4 p1 = make_float4(__uint_as_float(l4.x), __uint_as_float(l4.y), __uint_as_float(l4.z), __uint_as_float(l4.w));
           const float4 p2 = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z), __uint_as_float(q4.w));
           if (tri_hit4(p0, p1, p2, r, tnear, tfar, t)) {
-            if (!kAny) {
+            if (kAny) {
+              hit = true;
+            } else if (closer(t, slot, tfar, ref)) {
               tfar = t;
               ref = slot;
+              hit = true;
             }
-            hit = true;
           }
         }
       } else {
@@ -1263,9 +1276,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   const Staged sc = stage_scene<true>(sv, lds);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
-    w.tot[kTotTracedP] += primary_traced(f);
-    w.tot[kTotTracedD] += primary_traced(f);
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)((unsigned long long)f.valid * f.k));
+    atomicAdd(&w.tot[kTotTracedP], (unsigned long long)(primary_traced(f)));
+    atomicAdd(&w.tot[kTotTracedD], (unsigned long long)(primary_traced(f)));
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
@@ -1354,9 +1367,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   const Staged sc = stage_scene<kLds>(sv, lds);
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.tot[kTotClosest] += (unsigned long long)f.valid * f.k;
-    w.tot[kTotTracedP] += primary_traced(f);
-    w.tot[kTotTracedD] += primary_traced(f);
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)((unsigned long long)f.valid * f.k));
+    atomicAdd(&w.tot[kTotTracedP], (unsigned long long)(primary_traced(f)));
+    atomicAdd(&w.tot[kTotTracedD], (unsigned long long)(primary_traced(f)));
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
@@ -1459,10 +1472,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)(kPrimary ? (unsigned long long)f.valid * f.k : n));
     const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
-    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += t;
-    w.tot[kTotTracedD + stat_depth(depth)] += t;
+    atomicAdd(&w.tot[kPrimary ? kTotTracedP : kTotTracedB], (unsigned long long)(t));
+    atomicAdd(&w.tot[kTotTracedD + stat_depth(depth)], (unsigned long long)(t));
   }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
@@ -1597,10 +1610,10 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     n = seg_scan(w.segN, nseg_in, s_off, per_in);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.tot[kTotClosest] += kPrimary ? (unsigned long long)f.valid * f.k : n;
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)(kPrimary ? (unsigned long long)f.valid * f.k : n));
     const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
-    w.tot[kPrimary ? kTotTracedP : kTotTracedB] += t;
-    w.tot[kTotTracedD + stat_depth(depth)] += t;
+    atomicAdd(&w.tot[kPrimary ? kTotTracedP : kTotTracedB], (unsigned long long)(t));
+    atomicAdd(&w.tot[kTotTracedD + stat_depth(depth)], (unsigned long long)(t));
   }
   const ImageDiv idiv = image_div(f);
   const RayStream rs = w.rs[depth & 1];
@@ -2043,7 +2056,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
   const Staged sc = stage_scene<true>(sv, lds);
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.tot[kTotClosest] += n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&w.tot[kTotClosest], (unsigned long long)(n));
   const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
   Visits vc;
@@ -2423,16 +2436,21 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
 // accum in sample order — the adds k_trace (rad[p] = 0 + 1 * env) and k_accum would make, in the
 // same order — and marks the pixel complete (resume slot k); k_trace skips those paths and writes no
 // radiance for them, k_accum no longer reads it.  Other pixels get resume slot 0.
+// a culled valid pixel of a path-major batch with sky_fold: k_sky sums its samples, k_accum none
+__device__ __forceinline__ bool sky_pixel(const FrameView& f, uint32_t l, int& x, int& y) {
+  return pixel_culled(f, l) && local_pixel(f, l, x, y);
+}
 template <bool kCube>
 __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
   const FrameView f = frame_dyn(fin);
   const ImageDiv idiv = image_div(f);
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
-    vec3 a = v3(0.0f, 0.0f, 0.0f);
-    if (!f.reset) a = xyz(f.accum[l]);
     int x, y;
-    uint32_t resume = 0u;
-    if (pixel_culled(f, l) && local_pixel(f, l, x, y)) {
+    // only the culled pixels' words: k_accum sums the others (sky_pixel), so a batch's k_sky may run
+    // beside the previous batch's k_accum (two-lane calls, enqueue_wavefront)
+    if (sky_pixel(f, l, x, y)) {
+      vec3 a = v3(0.0f, 0.0f, 0.0f);
+      if (!f.reset) a = xyz(f.accum[l]);
       const uint32_t ps = (uint32_t)(y * f.W + x);
       auto sample = [&](uint32_t smp) {
         Primary pr;
@@ -2453,9 +2471,8 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
         for (uint32_t j = 0; j < kSkyIlp; ++j) a = a + rv[j];
       }
       for (; smp < f.k; ++smp) a = a + sample(smp);
-      resume = f.k;
+      f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(f.k));
     }
-    f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(resume));
   }
 }
 
@@ -2511,12 +2528,17 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
     uint32_t s0 = 0u;
     vec3 a = v3(0.0f, 0.0f, 0.0f);
     bool sum = true;
-    if (f.pixel_major || f.sky_fold) {
+    if (f.pixel_major) {
       const float4 a4 = accum[l];
       s0 = __float_as_uint(a4.w);
       a = xyz(a4);
       sum = s0 < f.k;
       if (!kResolve && !sum) continue;
+    } else if (f.sky_fold) {  // k_sky summed the culled pixels; the others start from the previous batch
+      int x, y;
+      sum = !sky_pixel(f, l, x, y);
+      if (!kResolve && !sum) continue;
+      if (!sum || !f.reset) a = xyz(accum[l]);
     } else if (!f.reset) {
       a = xyz(accum[l]);
     }

@@ -15,6 +15,10 @@
 
 #include "sptr_internal.h"
 
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
+
 struct sptr_ctx {
   sptr::Context c;
 };
@@ -100,6 +104,9 @@ inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
   return shard_pixel(c.W, c.H, c.G, c.R, l, x, y);
 }
 
+// segment tables (3 x (kMaxSegs + 4) u32), per-block tallies (2 x kMaxSegs u64), work counters
+size_t seg_table_bytes() { return 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kWorkWords * 4; }
+
 // device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
 // L shadow tasks of ts float4s
 uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + kHitBytes + 16 + (uint64_t)L * ts * 16; }
@@ -112,25 +119,30 @@ uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
 // pixel slot it owns, so its segment slack is kMaxSegs * kBlock * k records (k_slack = k); every
 // other producer needs kMaxSegs * kBlock (k_slack = 1).
-int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
+int ensure_wave(Context& c, int lane, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
+  WaveBufs& b = c.wb[lane];
   L = L ? L : 1u;
   const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * kHitBytes;
-  const bool grow = c.w_hrec.bytes < hrec_bytes || !(c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p);
+  const bool grow = b.hrec.bytes < hrec_bytes || !(b.cap >= cap && b.L * b.ts >= L * ts && b.rad.p) || !b.seg.p;
   if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
   if (grow) ++c.epoch;
-  API_HIP(ensure_buf(c.w_hrec, hrec_bytes));
-  if (c.wave_cap >= cap && c.wave_L * c.wave_ts >= L * ts && c.w_rad.p) return SPTR_OK;
+  if (!b.seg.p) {  // segment tables, per-block tallies and work counters, zeroed once
+    API_HIP(ensure_buf(b.seg, seg_table_bytes()));
+    API_HIP(hipMemset(b.seg.p, 0, seg_table_bytes()));
+  }
+  API_HIP(ensure_buf(b.hrec, hrec_bytes));
+  if (b.cap >= cap && b.L * b.ts >= L * ts && b.rad.p) return SPTR_OK;
   // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
   // with per = ceil(n / (G*kBlock)) * kBlock, so the segment space G*per can exceed n by up to
   // G*kBlock - 1 records: every segmented stream carries kMaxSegs*kBlock records of slack.
   const size_t n = (size_t)cap, ns = n + (size_t)kMaxSegs * kBlock;
-  for (auto& b : c.w_rs)
-    for (DevBuf& x : b) API_HIP(ensure_buf(x, ns * 16));
-  API_HIP(ensure_buf(c.w_rad, n * 16));
-  API_HIP(ensure_buf(c.w_stask, ns * L * ts * 16));
-  c.wave_cap = cap;
-  c.wave_L = L;
-  c.wave_ts = ts;
+  for (auto& r : b.rs)
+    for (DevBuf& x : r) API_HIP(ensure_buf(x, ns * 16));
+  API_HIP(ensure_buf(b.rad, n * 16));
+  API_HIP(ensure_buf(b.stask, ns * L * ts * 16));
+  b.cap = cap;
+  b.L = L;
+  b.ts = ts;
   return SPTR_OK;
 }
 
@@ -140,23 +152,24 @@ uint32_t task_stride(const Context& c) {
   return 2u;
 }
 
-WaveView wave_view(Context& c) {
+WaveView wave_view(Context& c, int lane) {
+  const WaveBufs& wb = c.wb[lane];
   WaveView w;
   for (int b = 0; b < 2; ++b) {
-    w.rs[b].o = static_cast<float4*>(c.w_rs[b][0].p);
-    w.rs[b].d = static_cast<float4*>(c.w_rs[b][1].p);
-    w.rs[b].thr = static_cast<float4*>(c.w_rs[b][2].p);
+    w.rs[b].o = static_cast<float4*>(wb.rs[b][0].p);
+    w.rs[b].d = static_cast<float4*>(wb.rs[b][1].p);
+    w.rs[b].thr = static_cast<float4*>(wb.rs[b][2].p);
   }
-  const uint64_t hcap = std::min<uint64_t>(c.w_hrec.bytes / kHitBytes, 0xFFFFFFFFull);
+  const uint64_t hcap = std::min<uint64_t>(wb.hrec.bytes / kHitBytes, 0xFFFFFFFFull);
 #if SPTR_HREC16
-  w.hrec.r = static_cast<uint4*>(c.w_hrec.p);
+  w.hrec.r = static_cast<uint4*>(wb.hrec.p);
 #else
-  w.hrec.tr = static_cast<uint2*>(c.w_hrec.p);
-  w.hrec.id = reinterpret_cast<uint32_t*>(static_cast<char*>(c.w_hrec.p) + hcap * 8u);
+  w.hrec.tr = static_cast<uint2*>(wb.hrec.p);
+  w.hrec.id = reinterpret_cast<uint32_t*>(static_cast<char*>(wb.hrec.p) + hcap * 8u);
 #endif
-  w.rad = static_cast<float4*>(c.w_rad.p);
-  w.stask = static_cast<float4*>(c.w_stask.p);
-  uint32_t* seg = static_cast<uint32_t*>(c.w_seg.p);  // 3 tables of kMaxSegs counts + 1 stride
+  w.rad = static_cast<float4*>(wb.rad.p);
+  w.stask = static_cast<float4*>(wb.stask.p);
+  uint32_t* seg = static_cast<uint32_t*>(wb.seg.p);  // 3 tables of kMaxSegs counts + 1 stride
   w.segN = SegTable{seg, seg + kMaxSegs};
   w.segH = SegTable{seg + (kMaxSegs + 4), seg + (kMaxSegs + 4) + kMaxSegs};
   w.segS = SegTable{seg + 2 * (kMaxSegs + 4), seg + 2 * (kMaxSegs + 4) + kMaxSegs};
@@ -167,7 +180,7 @@ WaveView wave_view(Context& c) {
   w.L = (uint32_t)c.lights_host.size();
   w.tstride = task_stride(c);
   w.defer_miss = 0u;
-  w.seg_cap = (uint32_t)(c.wave_cap + (uint64_t)kMaxSegs * kBlock);
+  w.seg_cap = (uint32_t)(wb.cap + (uint64_t)kMaxSegs * kBlock);
   w.hrec_cap = (uint32_t)hcap;
   return w;
 }
@@ -293,6 +306,11 @@ int collect_pending(Context& c, sptr_stats* stats) {
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (c.pending == 0) return SPTR_OK;
   const hipError_t se = hipStreamSynchronize(c.pending_stream);
+  // the auxiliary streams' work was joined into pending_stream, so it is complete; synchronising them
+  // as well lets the runtime retire their command chains.  (Without it, a long run of direct-launch
+  // calls with cross-stream event waits ended in a stack overflow inside libamdhip64: a recursive walk
+  // over the accumulated fork/join chain, seen in the GPU test suite.)
+  for (hipStream_t st : {c.side_stream, c.lane_stream, c.side2_stream}) (void)hipStreamSynchronize(st);
   double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t trace_launches = 0, shadow_launches = 0;
   for (const StageMark& m : c.marks) {
@@ -430,7 +448,7 @@ constexpr uint32_t kPtFramesPerLaunch = 4;
 uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
-  WaveView w = wave_view(c);
+  WaveView w = wave_view(c, 0);
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool optix = f.integrator == SPTR_INTEGRATOR_OPTIX;
@@ -464,10 +482,17 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
 constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 
 // Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
-uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
+//
+// lanes == 2 (scenes traversed from L2/HBM, path-major bounce 0): consecutive sample batches alternate
+// between two buffer sets ("lanes") and run at the same time, lane 1 on a stream of its own — each
+// launch of these scenes is latency-bound and ends in a long tail, and two independent chains fill
+// each other's idle CUs.  The batches share only the accumulator: the culled pixels' k_sky sums and the
+// k_accum sums must reach accum in sample order, so batch i's k_sky and k_accum wait for batch i-1's.
+// (LDS scenes fold bounce 0 into accum inside the trace kernel, which couples whole batches: 1 lane.)
+uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, int lanes, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
-  WaveView w = wave_view(c);
+  WaveView wl[2] = {wave_view(c, 0), wave_view(c, lanes > 1 ? 1 : 0)};
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
@@ -494,12 +519,17 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
   // launches overlapped on a second stream (SPTR_OVERLAP=0: everything on s, for A/B timing)
-  static const bool overlap = [] {
+  static const bool overlap_env = [] {
     const char* e = getenv("SPTR_OVERLAP");
     return !(e && e[0] == '0');
   }();
-  hipStream_t side = s == c.cap_stream ? c.cap_side : c.side_stream;
-  bool join = false, join_sky = false;  // pending side-stream work: shadow(d) (ev_join), k_sky (ev_sky)
+  const bool overlap = overlap_env && c.launch_mode != 2;
+  const bool cap = s == c.cap_stream;
+  hipStream_t main_s[2] = {s, cap ? c.cap_lane : c.lane_stream};
+  hipStream_t side_s[2] = {cap ? c.cap_side : c.side_stream, cap ? c.cap_side2 : c.side2_stream};
+  // per lane: pending side-stream work (shadow(d): ev_join, k_sky: ev_sky), and whether ev_sky / ev_acc
+  // hold a record the other lane must order after
+  bool join[2] = {false, false}, join_sky[2] = {false, false}, sky_rec[2] = {false, false}, acc_rec[2] = {false, false};
   auto fork_err = [&](hipError_t e) {
     if (e != hipSuccess && tm.err == hipSuccess) tm.err = e;
   };
@@ -507,11 +537,25 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   // beside the next bounce's trace: shadow(d) only adds to rad[], which the bounce traces then leave
   // alone (misses deferred to k_shade, WaveView::defer_miss); k_shade(d + 1) overwrites the shadow
   // tasks and updates rad[], so it, the tail and k_accum wait for shadow(d) (ev_join)
-  const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, w);
-  w.defer_miss = shadow_side ? 1u : 0u;
-  StageTimer tside{c, tm.on, tm.trace_only, side};
-  tside.capturing = tm.capturing;
-  while (done < f.spp) {
+  const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, wl[0]);
+  wl[0].defer_miss = wl[1].defer_miss = shadow_side ? 1u : 0u;
+  StageTimer tmain1{c, tm.on, tm.trace_only, main_s[1]};
+  StageTimer tside0{c, tm.on, tm.trace_only, side_s[0]}, tside1{c, tm.on, tm.trace_only, side_s[1]};
+  tmain1.capturing = tside0.capturing = tside1.capturing = tm.capturing;
+  StageTimer* tmain[2] = {&tm, &tmain1};
+  StageTimer* tside[2] = {&tside0, &tside1};
+  // lane 1 starts after the call's head on s (k_frame_dyn, k_cull), before lane 0's first batch
+  const bool lane1_forked = lanes > 1 && k < f.spp;
+  if (lane1_forked) {
+    fork_err(hipEventRecord(c.ev_lane, s));
+    fork_err(hipStreamWaitEvent(main_s[1], c.ev_lane, 0));
+  }
+  for (uint32_t batch = 0; done < f.spp; ++batch) {
+    const int j = lanes > 1 ? (int)(batch & 1u) : 0;
+    hipStream_t ms = main_s[j], ss = side_s[j];
+    StageTimer& tmj = *tmain[j];
+    StageTimer& tsj = *tside[j];
+    const WaveView& w = wl[j];
     const uint32_t kk = std::min<uint32_t>(k, f.spp - done);
     fv.k = kk;
     fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
@@ -528,80 +572,90 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     uint32_t g_shade = 0;
     // fused bounces alternate the ray tables: the table holding the current rays, and the other
     SegTable rays_tab = w.segN, spare_tab = w.segH;
+    auto wait_side = [&]() {
+      if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));
+      if (join_sky[j]) fork_err(hipStreamWaitEvent(ms, c.ev_sky[j], 0));
+      join[j] = join_sky[j] = false;
+    };
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
-        if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));
-        if (join_sky) fork_err(hipStreamWaitEvent(s, c.ev_sky, 0));
-        join = join_sky = false;
+        wait_side();
         WaveView wt = w;
         wt.segN = rays_tab;
-        tm.begin(7);
-        launch_tail(sv, sh, fv, wt, d, g_shade, s);
-        tm.end();
+        tmj.begin(7);
+        launch_tail(sv, sh, fv, wt, d, g_shade, ms);
+        tmj.end();
         break;
       }
       if (d >= 1 && fuse_bounce) {  // trace + shade (+ shadow) of this bounce in one launch
         WaveView wf = w;
         wf.segN = rays_tab;
         wf.segH = spare_tab;
-        tm.begin(2);
-        g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, s);
-        tm.end();
+        tmj.begin(2);
+        g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, ms);
+        tmj.end();
         std::swap(rays_tab, spare_tab);
         continue;
       }
       if (d == 0 && fv.sky_fold) {  // the culled pixels' environment sums: accumulation, not k_trace
-        if (overlap) {
+        const bool after_other = lanes > 1 && sky_rec[1 - j];  // sample order in accum: the previous batch's k_sky first
+        if (overlap || lanes > 1) {
           // on the side stream, concurrent with the bounce-0 trace (it writes only the culled pixels'
           // accum words, which nothing reads before this batch's k_accum, the join point): its VALU-bound
           // blocks fill the CUs the latency-bound trace leaves idle, above all in the trace's tail
-          fork_err(hipEventRecord(c.ev_fork, s));
-          fork_err(hipStreamWaitEvent(side, c.ev_fork, 0));
-          launch_sky(sh, fv, side);
-          fork_err(hipEventRecord(c.ev_sky, side));
-          join_sky = true;
+          fork_err(hipEventRecord(c.ev_fork[j], ms));
+          fork_err(hipStreamWaitEvent(ss, c.ev_fork[j], 0));
+          if (after_other) fork_err(hipStreamWaitEvent(ss, c.ev_sky[1 - j], 0));
+          launch_sky(sh, fv, ss);
+          fork_err(hipEventRecord(c.ev_sky[j], ss));
+          join_sky[j] = sky_rec[j] = true;
         } else {
-          tm.begin(4);
-          launch_sky(sh, fv, s);
-          tm.end();
+          tmj.begin(4);
+          launch_sky(sh, fv, ms);
+          tmj.end();
         }
       }
-      tm.begin(d == 0 ? 5 : 1);
-      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
-      tm.end();
-      if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));  // shadow(d - 1) (and k_sky) before shade(d)
-      join = false;
-      tm.begin(d == 0 ? 6 : 2);
-      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
-      tm.end();
+      tmj.begin(d == 0 ? 5 : 1);
+      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, ms);
+      tmj.end();
+      if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));  // shadow(d - 1) before shade(d)
+      join[j] = false;
+      tmj.begin(d == 0 ? 6 : 2);
+      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, ms);
+      tmj.end();
       if (!fuse && shadow_side) {
-        fork_err(hipEventRecord(c.ev_fork, s));
-        fork_err(hipStreamWaitEvent(side, c.ev_fork, 0));
-        tside.begin(3);
-        launch_shadow(sv, sh, w, d, count, g_shade, side);
-        tside.end();
-        fork_err(hipEventRecord(c.ev_join, side));
-        join = true;
+        fork_err(hipEventRecord(c.ev_fork[j], ms));
+        fork_err(hipStreamWaitEvent(ss, c.ev_fork[j], 0));
+        tsj.begin(3);
+        launch_shadow(sv, sh, w, d, count, g_shade, ss);
+        tsj.end();
+        fork_err(hipEventRecord(c.ev_join[j], ss));
+        join[j] = true;
       } else if (!fuse) {
-        tm.begin(3);
-        launch_shadow(sv, sh, w, d, count, g_shade, s);
-        tm.end();
+        tmj.begin(3);
+        launch_shadow(sv, sh, w, d, count, g_shade, ms);
+        tmj.end();
       }
     }
     // the call's last batch resolves in the same launch (k_accum<true>: each thread resolves the
     // sum it holds, as k_resolve would next)
     const bool resolve = done + kk >= f.spp && !(f.flags & SPTR_FRAME_NO_RESOLVE);
-    if (join) fork_err(hipStreamWaitEvent(s, c.ev_join, 0));
-    if (join_sky) fork_err(hipStreamWaitEvent(s, c.ev_sky, 0));
-    join = join_sky = false;
-    if (tside.err != hipSuccess && tm.err == hipSuccess) tm.err = tside.err;
-    tm.begin(4);
+    wait_side();
+    if (lanes > 1 && acc_rec[1 - j]) fork_err(hipStreamWaitEvent(ms, c.ev_acc[1 - j], 0));  // sample order
+    tmj.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
-                      static_cast<uint8_t*>(c.image.p), resolve, s);
-    tm.end();
+                      static_cast<uint8_t*>(c.image.p), resolve, ms);
+    tmj.end();
+    if (lanes > 1) {
+      fork_err(hipEventRecord(c.ev_acc[j], ms));
+      acc_rec[j] = true;
+    }
     done += kk;
     ++waves;
   }
+  if (lane1_forked) fork_err(hipStreamWaitEvent(s, c.ev_acc[1], 0));  // join lane 1 (its last k_accum)
+  for (StageTimer* t : {&tmain1, &tside0, &tside1})
+    if (t->err != hipSuccess && tm.err == hipSuccess) tm.err = t->err;
   tm.end_call();
   return waves;
 }
@@ -660,7 +714,10 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
-  if (c.launch_mode != 0 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+  // two-lane calls launch directly: their launches are long (L2/HBM scenes, ~20 launches of 0.1-2 ms),
+  // so a graph saves nothing measurable, and capturing the four-stream fork/join sequence repeatedly
+  // ended in a stack overflow inside libamdhip64 (recursion at +0x2d34a8) in the GPU test suite
+  if (c.launch_mode != 0 || key.lanes > 1 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
     StageTimer tm{c, timing, trace_only, s};
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
@@ -790,8 +847,48 @@ extern "C" {
 
 int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
 
+namespace sptr {
+namespace {
+std::vector<hipEvent_t*> dep_events(Context& c) {
+  std::vector<hipEvent_t*> v{&c.ev_lane};
+  for (int j = 0; j < 2; ++j)
+    for (hipEvent_t* e : {&c.ev_fork[j], &c.ev_join[j], &c.ev_sky[j], &c.ev_acc[j]}) v.push_back(e);
+  return v;
+}
+bool create_events(Context& c) {
+  for (hipEvent_t* e : dep_events(c))
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
+  return true;
+}
+}  // namespace
+}  // namespace sptr
+
+// SPTR_SEGV_TRACE=1 (diagnostics): a host SIGSEGV prints the native backtrace before the default action
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+static void install_segv_trace() {
+  static const bool on = getenv("SPTR_SEGV_TRACE") != nullptr;
+  if (!on) return;
+  static char alt[1 << 16];
+  stack_t ss{};
+  ss.ss_sp = alt;
+  ss.ss_size = sizeof(alt);
+  sigaltstack(&ss, nullptr);
+  struct sigaction sa{};
+  sa.sa_handler = segv_trace;
+  sa.sa_flags = SA_ONSTACK;
+  sigaction(SIGSEGV, &sa, nullptr);
+}
+
 int sptr_create(int device, sptr_ctx** out) {
   if (!out) return SPTR_ERR_INVALID;
+  install_segv_trace();
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SPTR_ERR_NO_DEVICE;
@@ -806,16 +903,17 @@ int sptr_create(int device, sptr_ctx** out) {
       hipDeviceGetStreamPriorityRange(&c.prio_lo, &c.prio_hi) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.cap_side, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
-      hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c.ev_sky, hipEventDisableTiming) != hipSuccess) {
+      hipStreamCreateWithPriority(&c.side2_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c.cap_side2, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
+      // lane 1's main stream at the highest priority: a hardware queue apart from the caller's stream
+      hipStreamCreateWithPriority(&c.lane_stream, hipStreamNonBlocking, c.prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c.cap_lane, hipStreamNonBlocking, c.prio_hi) != hipSuccess ||
+      !create_events(c)) {
     delete x;
     return SPTR_ERR_HIP;
   }
-  const size_t seg_bytes = 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kWorkWords * 4;
-  if (ensure_buf(c.w_seg, seg_bytes) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
-      ensure_buf(c.dyn, 64) != hipSuccess ||
-      hipMemset(c.w_seg.p, 0, seg_bytes) != hipSuccess) {
+  if (ensure_buf(c.wb[0].seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
+      ensure_buf(c.dyn, 64) != hipSuccess || hipMemset(c.wb[0].seg.p, 0, seg_table_bytes()) != hipSuccess) {
     delete x;
     return SPTR_ERR_OOM;
   }
@@ -830,11 +928,16 @@ int sptr_destroy(sptr_ctx* x) {
   if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
   (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
-                    &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_hrec, &c.w_rad,   &c.w_stask,
-                    &c.w_seg,  &c.w_tot,    &c.accum, &c.tiles, &c.image,  &c.qbuf, &c.nodes4, &c.cull, &c.plist};
+                    &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
+                    &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist};
   for (DevBuf* b : bufs) free_buf(*b);
-  for (auto& b : c.w_rs)
-    for (DevBuf& x : b) free_buf(x);
+  for (WaveBufs& wb : c.wb) {
+    for (DevBuf* b : {&wb.hrec, &wb.rad, &wb.stask, &wb.seg}) free_buf(*b);
+    for (auto& r : wb.rs)
+      for (DevBuf& x : r) free_buf(x);
+  }
+  for (hipStream_t st : {c.lane_stream, c.cap_lane, c.side2_stream, c.cap_side2})
+    if (st) (void)hipStreamDestroy(st);
   drop_graph(c);
   free_buf(c.dyn);
   for (hipEvent_t e : c.events) (void)hipEventDestroy(e);
@@ -842,9 +945,8 @@ int sptr_destroy(sptr_ctx* x) {
   if (c.cap_stream) (void)hipStreamDestroy(c.cap_stream);
   if (c.side_stream) (void)hipStreamDestroy(c.side_stream);
   if (c.cap_side) (void)hipStreamDestroy(c.cap_side);
-  if (c.ev_fork) (void)hipEventDestroy(c.ev_fork);
-  if (c.ev_join) (void)hipEventDestroy(c.ev_join);
-  if (c.ev_sky) (void)hipEventDestroy(c.ev_sky);
+  for (hipEvent_t* e : dep_events(c))
+    if (*e) (void)hipEventDestroy(*e);
   delete x;
   return SPTR_OK;
 }
@@ -1025,6 +1127,7 @@ int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
 
 int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
   if (!x || !f) return SPTR_ERR_INVALID;
+  install_segv_trace();
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
   if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "render: no scene uploaded");
@@ -1071,10 +1174,11 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     uint64_t wave_paths = c.wave_paths;
     if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
       wave_paths = kDefaultWavePaths;
-      if (c.wave_cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
+      if (c.wb[0].cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
-          const uint64_t held = c.wave_cap ? c.wave_cap * wave_path_bytes(c.wave_L, c.wave_ts) : 0ull;
+          uint64_t held = 0;
+          for (const WaveBufs& wb : c.wb) held += wb.cap ? wb.cap * wave_path_bytes(wb.L, wb.ts) : 0ull;
           const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
           // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
           const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
@@ -1086,19 +1190,35 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     }
     uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
     k = std::min<uint32_t>(k, f->spp);
+    int lanes = 1;
     {
-      // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
       const SceneView sv = scene_view(c);
+      // two sample-batch lanes (enqueue_wavefront) for scenes traversed from L2/HBM, whose bounce 0 is
+      // path-major: the call's samples in batches of at most half, each lane sized for its batch (so the
+      // two lanes hold what one lane of k samples would)
+      static const int lanes_env = getenv("SPTR_LANES") ? atoi(getenv("SPTR_LANES")) : 0;
+      // default 1: measured slower (r03zj: C5 8.5-8.6 -> 8.9, C3 3.9 -> 4.6-4.8 ms/step): the refilling
+      // kernels' resident grids occupy every CU slot, so two lanes time-slice rather than overlap, and
+      // each launch keeps its tail at half the batch
+      const uint32_t want = c.lanes ? c.lanes : (lanes_env ? (uint32_t)lanes_env : 1u);
+      if (want >= 2 && sv.lds_bytes == 0 && f->spp >= 2 && c.launch_mode != 2) {
+        lanes = 2;
+        k = std::max<uint32_t>(1u, std::min<uint32_t>((f->spp + 1u) / 2u, k >= f->spp ? k : k / 2u));
+      }
+      // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
       FrameView probe = frame_view(c, *f);
       probe.k = k;
       const uint32_t k_slack = bounce0_pixel_major(sv, probe) ? k : 1u;
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
-      if (rc != SPTR_OK) return rc;
+      for (int j = 0; j < lanes; ++j) {
+        rc = ensure_wave(c, j, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
+        if (rc != SPTR_OK) return rc;
+      }
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));
     key.epoch = c.epoch;  // ensure_wave may have reallocated
     key.k = k;
     key.tail = (uint32_t)T;
+    key.lanes = (uint32_t)lanes;
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
     rc = refresh_cull(c, *f, s, timing || trace_timing);
     if (rc != SPTR_OK) return rc;
@@ -1106,7 +1226,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     uint32_t* clear = ((f->flags & SPTR_FRAME_RECULL) && !(f->flags & SPTR_FRAME_NO_CULL))
                           ? static_cast<uint32_t*>(c.plist.p) + c.P : nullptr;
     rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, clear, timing || trace_timing, !timing, s,
-                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
+                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, lanes, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
     samples = (uint64_t)frame_view(c, *f).valid * f->spp;
   }
@@ -1122,9 +1242,16 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   return collect_pending(c, stats);
 }
 
+int sptr_set_lanes(sptr_ctx* x, uint32_t lanes) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (lanes > 2) return fail(x->c, SPTR_ERR_INVALID, "lanes must be 0 (automatic), 1 or 2");
+  x->c.lanes = lanes;
+  return SPTR_OK;
+}
+
 int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
   if (!x) return SPTR_ERR_INVALID;
-  if (mode > 1) return fail(x->c, SPTR_ERR_INVALID, "launch mode must be 0 (graphs) or 1 (direct)");
+  if (mode > 2) return fail(x->c, SPTR_ERR_INVALID, "launch mode must be 0 (graphs), 1 (direct) or 2 (direct, one stream)");
   x->c.launch_mode = mode;
   return SPTR_OK;
 }

@@ -279,6 +279,13 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
 };
+// One lane's path-state streams: ray streams, hit records, radiance, shadow tasks, and
+// the segment tables / per-block tallies / work counters (seg).
+struct WaveBufs {
+  uint64_t cap = 0;  // paths
+  uint32_t L = 0, ts = 0;
+  DevBuf rs[2][3], hrec, rad, stask, seg;
+};
 
 struct StageMark {
   int stage;
@@ -292,7 +299,7 @@ struct StageMark {
 struct GraphKey {
   uint64_t epoch;
   sptr_frame frame;
-  uint32_t k, tail, pad0, pad1;
+  uint32_t k, tail, lanes, pad1;
 };
 struct GraphMark {
   int stage;
@@ -316,7 +323,10 @@ struct Context {
   // second streams for launches that overlap the main sequence (direct launches / inside a capture),
   // forked from and joined back into it by ev_fork / ev_join (enqueue_wavefront)
   hipStream_t side_stream = nullptr, cap_side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sky = nullptr;
+  // lane 1 of a two-lane call: its main stream (a priority of its own) and its side stream
+  hipStream_t lane_stream = nullptr, cap_lane = nullptr, side2_stream = nullptr, cap_side2 = nullptr;
+  // per lane: fork to the side stream, shadow join, k_sky done, k_accum done; lane-1 fork
+  hipEvent_t ev_fork[2] = {}, ev_join[2] = {}, ev_sky[2] = {}, ev_acc[2] = {}, ev_lane = nullptr;
   int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
   uint32_t launch_mode = 0;          // 0: replay a captured graph for repeated call shapes; 1: direct launches
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
@@ -351,10 +361,10 @@ struct Context {
   DevBuf env;
   int32_t env_size = 0;
   float env_intensity = 0.8f, env_clamp = 5.0f;
-  // wavefront buffers
-  uint64_t wave_cap = 0;  // paths
-  uint32_t wave_L = 0, wave_ts = 0;
-  DevBuf w_rs[2][3], w_hrec, w_rad, w_stask, w_seg, w_tot;
+  // wavefront buffers: lane 0, and lane 1 when a call runs two sample batches at once (enqueue_wavefront)
+  WaveBufs wb[2];
+  DevBuf w_tot;
+  uint32_t lanes = 0;  // sample-batch lanes: 1, 2, or 0 = automatic (sptr_set_lanes)
   // pixel buffers
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;

@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_lanes", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -138,6 +138,7 @@ def lib() -> C.CDLL:
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_launch_mode": (C.c_int, [vp, u32]),
+        "sptr_set_lanes": (C.c_int, [vp, u32]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
@@ -397,6 +398,10 @@ class Renderer:
 
     def set_wave_paths(self, n: int):
         self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
+
+    def set_lanes(self, lanes: int):
+        """sptr_set_lanes: 2 sample-batch lanes at once (L2/HBM scenes), 1, or 0 = automatic."""
+        self._check(self._L.sptr_set_lanes(self._h, lanes), "set_lanes")
 
     def set_launch_mode(self, mode: int):
         """0: replay captured launch graphs for repeated call shapes (default); 1: direct launches."""

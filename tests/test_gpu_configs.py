@@ -106,17 +106,28 @@ def test_c3_batches_bit_exact(renderer):
     flat = sptr.setup_default(renderer, wl.scene, wl.p0, wl.p1, env_faces=faces)
     W, H, S = 96, 64, 32
     cam = sptr.camera_lookat(aspect=W / H)
-    st = renderer.render(cam, W, H, spp=S)
-    assert st.waves == 1
-    acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
-    renderer.set_wave_paths(3 * 2 * 1024 * 8)
+    renderer.set_lanes(1)
     try:
+        st = renderer.render(cam, W, H, spp=S)
+        assert st.waves == 1
+        acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
+        renderer.set_wave_paths(3 * 2 * 1024 * 8)
         st8 = renderer.render(cam, W, H, spp=S)
+        assert st8.waves == S // 8
+        assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
+        assert np.array_equal(rgb, renderer.read_rgb8())
+        # two sample-batch lanes (sptr_set_lanes): batches of half the budget, two at a time
+        renderer.set_lanes(2)
+        for paths, waves in ((3 * 2 * 1024 * 8, S // 4), (0, 2)):
+            renderer.set_wave_paths(paths)
+            st2 = renderer.render(cam, W, H, spp=S)
+            assert st2.waves == waves
+            assert (st2.rays_closest, st2.rays_shadow) == (st.rays_closest, st.rays_shadow)
+            assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
+            assert np.array_equal(rgb, renderer.read_rgb8())
     finally:
         renderer.set_wave_paths(0)
-    assert st8.waves == S // 8
-    assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
-    assert np.array_equal(rgb, renderer.read_rgb8())
+        renderer.set_lanes(0)
     P = oracle.Prepared(_flat_dict(flat), bvh=True)
     oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
                                 frames=S, env_faces=faces, threads=THREADS)

@@ -376,15 +376,17 @@ def test_wave_fold_bounce0_invariance(renderer, scene, p0, p1, spp):
     W, H = 96, 64
     cam = sptr.camera_lookat(aspect=W / H)
     sptr.setup_default(renderer, scene, p0, p1)
-    st = renderer.render(cam, W, H, spp=spp)
-    assert st.waves == 1
-    acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
-    P = 3 * 2 * 1024  # local pixels: 3 x 2 tiles
-    renderer.set_wave_paths(P * 8)
+    renderer.set_lanes(1)  # one batch at a time (the sample-batch lanes are tested in test_c3_batches_bit_exact)
     try:
+        st = renderer.render(cam, W, H, spp=spp)
+        assert st.waves == 1
+        acc, rgb = renderer.read_accum().copy(), renderer.read_rgb8().copy()
+        P = 3 * 2 * 1024  # local pixels: 3 x 2 tiles
+        renderer.set_wave_paths(P * 8)
         st8 = renderer.render(cam, W, H, spp=spp)
     finally:
         renderer.set_wave_paths(0)
+        renderer.set_lanes(0)
     assert st8.waves == (spp + 7) // 8
     assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
     assert np.array_equal(rgb, renderer.read_rgb8())
@@ -468,6 +470,34 @@ def test_pixel_cull_invisible(renderer, scene, p0, p1, spp, W, H):
     c1 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS)
     c0 = renderer.render(cam, W, H, spp=1, flags=sptr.SPTR_FRAME_COUNT_VISITS | sptr.SPTR_FRAME_NO_CULL)
     assert c1.node_visits < c0.node_visits
+
+
+@pytest.mark.parametrize("scene,p0,p1,spp", [("sphere_mesh", 60, 120, 16), ("sphere_mesh", 300, 600, 8)])
+def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
+    """Scenes traversed from L2/HBM run k_shadow_dyn(d) on a second stream beside k_trace_dyn(d + 1)
+    (bounce-trace misses deferred to k_shade) and k_sky beside the bounce-0 trace, in captured graphs
+    (launch mode 0) and direct launches (1); mode 2 keeps every launch on one stream.  The images and
+    ray counts must be equal bit for bit, and repeated renders too."""
+    W, H = 160, 96
+    sptr.setup_default(renderer, scene, p0, p1)
+    cam = sptr.camera_lookat(aspect=W / H)
+    out = {}
+    try:
+        for mode in (2, 1, 0):
+            renderer.set_launch_mode(mode)
+            runs = []
+            for _ in range(3):  # mode 0: direct, then captured and replayed where a call is captured
+                st = renderer.render(cam, W, H, spp=spp, frame_begin=1)
+                runs.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow))
+            out[mode] = runs
+    finally:
+        renderer.set_launch_mode(0)
+    ref = out[2][0]
+    assert ref[2] > 0  # shadow rays traced
+    for mode in (2, 1, 0):
+        for a in out[mode]:
+            assert np.array_equal(a[0].view(np.uint32), ref[0].view(np.uint32)), mode
+            assert a[1:] == ref[1:], mode
 
 
 @pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])
