@@ -387,15 +387,6 @@ __device__ __forceinline__ bool sphere_occ(float4 s, const Ray& r, float tnear, 
   return (t1 > tnear && t1 < tfar) || (t2 > tnear && t2 < tfar);
 }
 
-// Closest-hit order of candidate hits: by t, then by primitive reference (a hit at exactly the current
-// distance replaces the current one only if its reference is smaller).  With it the closest hit is the
-// minimum over the primitives a ray intersects, whatever order they are tested in — so traversal order
-// cannot change a result.  (Embree keeps the later of two
-// hits at equal t; such exact ties are the documented parity residue.)
-__device__ __forceinline__ bool closer(float t, uint32_t pr, float tfar, uint32_t ref) {
-  return t < tfar || (t == tfar && pr < ref);
-}
-
 struct Visits {
   uint32_t nodes = 0, tris = 0, sph = 0;
   uint32_t stack_overflow = 0;  // a push was dropped (reported through kTotStackOverflow)
@@ -420,7 +411,7 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
       const float4 s = sph[idx];
       if (kAny) {
         if (sphere_occ(s, r, tnear, tfar)) return true;
-      } else if (sphere_hit(s, r, tnear, tfar, t) && closer(t, pr, tfar, ref)) {
+      } else if (sphere_hit(s, r, tnear, tfar, t)) {
         tfar = t;
         ref = pr;
         hit = true;
@@ -429,11 +420,9 @@ __device__ __forceinline__ bool leaf_test(uint32_t link, const uint32_t* prim_re
       if (kCount) ++vc.tris;
       if (tri_hit(tris, idx, r, tnear, tfar, t)) {
         if (kAny) return true;
-        if (closer(t, pr, tfar, ref)) {
-          tfar = t;
-          ref = pr;
-          hit = true;
-        }
+        tfar = t;
+        ref = pr;
+        hit = true;
       }
     }
   }
@@ -734,7 +723,7 @@ __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, c
         if (dsph) {
           if (kCount) ++vc.sph;
           if (kAny) hit = sphere_occ(p0, r, tnear, tfar);
-          else if (sphere_hit(p0, r, tnear, tfar, t) && closer(t, slot | kSphereBit, tfar, ref)) {
+          else if (sphere_hit(p0, r, tnear, tfar, t)) {
             tfar = t;
             ref = slot | kSphereBit;
             hit = true;
@@ -744,13 +733,11 @@ __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, c
           const float4 p1 = make_float4(__uint_as_float(l4.x), __uint_as_float(l4.y), __uint_as_float(l4.z), __uint_as_float(l4.w));
           const float4 p2 = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z), __uint_as_float(q4.w));
           if (tri_hit4(p0, p1, p2, r, tnear, tfar, t)) {
-            if (kAny) {
-              hit = true;
-            } else if (closer(t, slot, tfar, ref)) {
+            if (!kAny) {
               tfar = t;
               ref = slot;
-              hit = true;
             }
+            hit = true;
           }
         }
       } else {
