@@ -481,6 +481,14 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
 #endif
 constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 
+// launches overlapped on second streams (SPTR_OVERLAP=0 or launch mode 2: everything on one stream)
+bool overlap_enabled(const Context& c) {
+  static const bool env = [] {
+    const char* e = getenv("SPTR_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return env && c.launch_mode != 2;
+}
 // Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
 //
 // lanes == 2 (scenes traversed from L2/HBM, path-major bounce 0): consecutive sample batches alternate
@@ -519,11 +527,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
   // launches overlapped on a second stream (SPTR_OVERLAP=0: everything on s, for A/B timing)
-  static const bool overlap_env = [] {
-    const char* e = getenv("SPTR_OVERLAP");
-    return !(e && e[0] == '0');
-  }();
-  const bool overlap = overlap_env && c.launch_mode != 2;
+  const bool overlap = overlap_enabled(c);
   const bool cap = s == c.cap_stream;
   hipStream_t main_s[2] = {s, cap ? c.cap_lane : c.lane_stream};
   hipStream_t side_s[2] = {cap ? c.cap_side : c.side_stream, cap ? c.cap_side2 : c.side2_stream};
@@ -579,7 +583,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
     };
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
-        wait_side();
+        // (shadow(d - 1) adds to rad[], which the tail reads; k_sky only to the culled pixels' accum,
+        // joined before k_accum, so the tail runs beside it: C3's k_sky outlasts the whole bounce chain)
+        if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));
+        join[j] = false;
         WaveView wt = w;
         wt.segN = rays_tab;
         tmj.begin(7);
@@ -597,27 +604,32 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
         std::swap(rays_tab, spare_tab);
         continue;
       }
-      if (d == 0 && fv.sky_fold) {  // the culled pixels' environment sums: accumulation, not k_trace
-        const bool after_other = lanes > 1 && sky_rec[1 - j];  // sample order in accum: the previous batch's k_sky first
-        if (overlap || lanes > 1) {
-          // on the side stream, concurrent with the bounce-0 trace (it writes only the culled pixels'
-          // accum words, which nothing reads before this batch's k_accum, the join point): its VALU-bound
-          // blocks fill the CUs the latency-bound trace leaves idle, above all in the trace's tail
-          fork_err(hipEventRecord(c.ev_fork[j], ms));
-          fork_err(hipStreamWaitEvent(ss, c.ev_fork[j], 0));
-          if (after_other) fork_err(hipStreamWaitEvent(ss, c.ev_sky[1 - j], 0));
-          launch_sky(sh, fv, ss);
-          fork_err(hipEventRecord(c.ev_sky[j], ss));
-          join_sky[j] = sky_rec[j] = true;
-        } else {
-          tmj.begin(4);
-          launch_sky(sh, fv, ms);
-          tmj.end();
-        }
+      const bool sky = d == 0 && fv.sky_fold;  // the culled pixels' environment sums: accumulation, not k_trace
+      const bool sky_side = sky && (overlap || lanes > 1);
+      if (sky && !sky_side) {
+        tmj.begin(4);
+        launch_sky(sh, fv, ms);
+        tmj.end();
       }
+      if (sky_side) fork_err(hipEventRecord(c.ev_fork[j], ms));
       tmj.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, ms);
       tmj.end();
+      if (sky_side) {
+        // on the side stream, concurrent with the bounce-0 trace (it writes only the culled pixels'
+        // accum words, which nothing reads before this batch's k_accum, the join point): its VALU-bound
+        // blocks fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.
+        // Submitted after the trace (both wait for the same point), so the trace's grid is dispatched first.
+        // One-lane calls put it on the second side stream, so that the shadow launches queued on the
+        // first one do not wait behind it.
+        const bool after_other = lanes > 1 && sky_rec[1 - j];  // sample order in accum: the previous batch's k_sky first
+        hipStream_t ks = lanes > 1 ? ss : side_s[1];
+        fork_err(hipStreamWaitEvent(ks, c.ev_fork[j], 0));
+        if (after_other) fork_err(hipStreamWaitEvent(ks, c.ev_sky[1 - j], 0));
+        launch_sky(sh, fv, ks);
+        fork_err(hipEventRecord(c.ev_sky[j], ks));
+        join_sky[j] = sky_rec[j] = true;
+      }
       if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));  // shadow(d - 1) before shade(d)
       join[j] = false;
       tmj.begin(d == 0 ? 6 : 2);
