@@ -178,6 +178,9 @@ def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
     hist = list(getattr(cnt, "trace_visit_hist", []))
     if any(hist):
         out["visit_hist_log2"] = [int(x) for x in hist]
+    if residency != "lds":
+        out["overlap"] = ("launch durations include the time shared with the launches the library overlaps on "
+                          "its second stream (k_sky beside bounce 0, k_shadow_dyn(d-1) beside bounce d; DESIGN.md §3)")
     fr = {"hbm_model": out["frac"], "hbm_counters": out["counter_frac"], "valu_issue": out["valu_issue_frac"]}
     known = {k: v for k, v in fr.items() if v is not None}
     out["binding"] = max(known, key=known.get) if known else None
