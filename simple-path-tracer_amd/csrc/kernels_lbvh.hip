@@ -13,7 +13,7 @@
 //                   also carries the subtree height — the fence-free hand-off of the gfx950 guide,
 //                   Guideline 16 R1)
 //   k_treelet     : (L2/HBM scenes) SAH treelet restructuring after k_refit, bottom-up by subtree height, 3 passes;
-//                   never deepens a subtree (k_heights, k_height_hist / k_height_scatter order the launches)
+//                   never deepens a subtree (k_heights, k_height_count / k_height_scatter order the launches)
 //   k_wide_count + scan + k_wide_emit, one wide level at a time (SPTR_WIDE_GREEDY, the default):
 //                   wide BVH (4 or 8 children) by the greedy surface-area collapse — a wide node
 //                   opens its largest-area internal child until it has kWide children; leaves stay
@@ -383,24 +383,31 @@ __global__ void k_heights(int N, const uint32_t* leaf_parent, const BvhNode* nod
   }
 }
 
-// Nodes grouped by height (the launch order of a pass): per-block histograms, then a wave-aggregated
-// scatter (one atomic per distinct height in a wave) into the height-ordered node list.
+// Nodes grouped by height (the launch order of a pass): a counting sort over kHeightBlocks blocks,
+// each owning a contiguous range of nodes — per-block histograms (height-major table), an exclusive
+// scan of the table on the host, then each block scatters its range from its own offsets with LDS
+// counters.  (r03: a single global cursor per height took one atomic per height per wave, ~150 K
+// atomics on the few bottom heights' words: 14 ms of a 10M-triangle build, per pass.)
 constexpr uint32_t kMaxHeight = 256;
-__global__ void k_height_hist(uint32_t nn, const uint32_t* label, uint32_t* hist) {
+constexpr uint32_t kHeightBlocks = 512;
+__global__ void k_height_count(uint32_t nn, uint32_t per, const uint32_t* label, uint32_t* bh) {
   __shared__ uint32_t s_h[kMaxHeight];
   for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x) s_h[i] = 0u;
   __syncthreads();
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += gridDim.x * blockDim.x)
-    atomicAdd(&s_h[min(label[x], kMaxHeight - 1u)], 1u);
+  const uint32_t lo = blockIdx.x * per, hi = min(nn, lo + per);
+  for (uint32_t x = lo + threadIdx.x; x < hi; x += blockDim.x) atomicAdd(&s_h[min(label[x], kMaxHeight - 1u)], 1u);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x)
-    if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+  for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x) bh[(size_t)i * gridDim.x + blockIdx.x] = s_h[i];
 }
-__global__ void k_height_scatter(uint32_t nn, const uint32_t* label, uint32_t* cursor, uint32_t* order) {
+__global__ void k_height_scatter(uint32_t nn, uint32_t per, const uint32_t* label, const uint32_t* boff, uint32_t* order) {
+  __shared__ uint32_t s_run[kMaxHeight];
+  for (uint32_t i = threadIdx.x; i < kMaxHeight; i += blockDim.x) s_run[i] = boff[(size_t)i * gridDim.x + blockIdx.x];
+  __syncthreads();
   const uint32_t lane = __lane_id();
-  for (uint32_t base = blockIdx.x * blockDim.x; base < nn; base += gridDim.x * blockDim.x) {
+  const uint32_t lo = blockIdx.x * per, hi = min(nn, lo + per);
+  for (uint32_t base = lo; base < hi; base += blockDim.x) {
     const uint32_t x = base + threadIdx.x;
-    const bool valid = x < nn;
+    const bool valid = x < hi;
     const uint32_t h = valid ? min(label[x], kMaxHeight - 1u) : 0u;
     unsigned long long todo = __ballot(valid);
     while (todo) {
@@ -408,7 +415,7 @@ __global__ void k_height_scatter(uint32_t nn, const uint32_t* label, uint32_t* c
       const uint32_t hl = __shfl(h, leader);
       const unsigned long long m = __ballot(valid && h == hl) & todo;
       uint32_t b = 0u;
-      if ((int)lane == leader) b = atomicAdd(&cursor[hl], (uint32_t)__popcll(m));
+      if ((int)lane == leader) b = atomicAdd(&s_run[hl], (uint32_t)__popcll(m));
       b = __shfl(b, leader);
       if ((m >> lane) & 1ull) order[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = x;
       todo &= ~m;
@@ -1173,25 +1180,30 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
         LB_CHECK(tmp.alloc(&lab, N));
         LB_CHECK(tmp.alloc(&nh, N));
         LB_CHECK(tmp.alloc(&order, N));
-        LB_CHECK(tmp.alloc(&hist, kMaxHeight));
+        LB_CHECK(tmp.alloc(&hist, (size_t)kMaxHeight * kHeightBlocks));
         LB_CHECK(tmp.alloc(&cst, N));
         LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
         hipLaunchKernelGGL(k_heights, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_parent, nodes, rflags, lab);
         LB_CHECK(hipGetLastError());
         const uint32_t nn = N - 1u;
-        std::vector<uint32_t> hh(kMaxHeight), off(kMaxHeight);
+        std::vector<uint32_t> hh(kMaxHeight), off(kMaxHeight), bh((size_t)kMaxHeight * kHeightBlocks);
+        const uint32_t per = (nn + kHeightBlocks - 1u) / kHeightBlocks;
         for (uint32_t pass = 0; pass < c.treelet_passes; ++pass) {
-          LB_CHECK(hipMemsetAsync(hist, 0, kMaxHeight * 4, s));
-          hipLaunchKernelGGL(k_height_hist, dim3(blocks_for(nn)), dim3(256), 0, s, nn, lab, hist);
-          LB_CHECK(hipMemcpyAsync(hh.data(), hist, kMaxHeight * 4, hipMemcpyDeviceToHost, s));
+          hipLaunchKernelGGL(k_height_count, dim3(kHeightBlocks), dim3(256), 0, s, nn, per, lab, hist);
+          LB_CHECK(hipMemcpyAsync(bh.data(), hist, bh.size() * 4, hipMemcpyDeviceToHost, s));
           LB_CHECK(hipStreamSynchronize(s));
-          uint32_t run = 0u;
+          uint32_t run = 0u;  // exclusive scan of the height-major table: heights in order, blocks in order
           for (uint32_t h = 0; h < kMaxHeight; ++h) {
             off[h] = run;
-            run += hh[h];
+            for (uint32_t b = 0; b < kHeightBlocks; ++b) {
+              const uint32_t n = bh[(size_t)h * kHeightBlocks + b];
+              bh[(size_t)h * kHeightBlocks + b] = run;
+              run += n;
+            }
+            hh[h] = run - off[h];
           }
-          LB_CHECK(hipMemcpyAsync(hist, off.data(), kMaxHeight * 4, hipMemcpyHostToDevice, s));
-          hipLaunchKernelGGL(k_height_scatter, dim3(blocks_for(nn)), dim3(256), 0, s, nn, lab, hist, order);
+          LB_CHECK(hipMemcpyAsync(hist, bh.data(), bh.size() * 4, hipMemcpyHostToDevice, s));
+          hipLaunchKernelGGL(k_height_scatter, dim3(kHeightBlocks), dim3(256), 0, s, nn, per, lab, hist, order);
           for (uint32_t h = 1; h < kMaxHeight; ++h)
             if (hh[h])
               hipLaunchKernelGGL(k_treelet<SPTR_TREELET>, dim3((hh[h] + kTreeletBlock - 1) / kTreeletBlock),
