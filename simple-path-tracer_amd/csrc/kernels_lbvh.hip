@@ -134,8 +134,24 @@ __global__ void k_prim_bounds(BuildIn in, float4* blo, float4* bhi, uint32_t* cb
   }
 }
 
-__global__ void k_morton(uint32_t N, const float4* blo, const float4* bhi, const uint32_t* cb, uint64_t* keys,
-                         uint32_t* vals) {
+// Embree's precomputed geometric normal Ng = cross(e2, e1) (msub form), as k_leaves stores it
+__device__ __forceinline__ vec3 tri_ng(const BuildIn& in, uint32_t prim) {
+  const uint32_t a = in.idx[3 * prim], b = in.idx[3 * prim + 1], c = in.idx[3 * prim + 2];
+  const vec3 v0 = v3(in.pos[3 * a], in.pos[3 * a + 1], in.pos[3 * a + 2]);
+  const vec3 v1 = v3(in.pos[3 * b], in.pos[3 * b + 1], in.pos[3 * b + 2]);
+  const vec3 v2 = v3(in.pos[3 * c], in.pos[3 * c + 1], in.pos[3 * c + 2]);
+  const vec3 e1 = v0 - v1, e2 = v2 - v0;
+  return v3(__builtin_fmaf(e2.y, e1.z, -(e2.z * e1.y)), __builtin_fmaf(e2.z, e1.x, -(e2.x * e1.z)),
+            __builtin_fmaf(e2.x, e1.y, -(e2.y * e1.x)));
+}
+// Morton code of the centroid; a triangle whose stored Ng is exactly zero (two equal vertices: e.g.
+// the 1250x4000 sphere mesh's north-pole ring, whose vertices are all (+-0, r, +-0)) gets bit 63, so
+// the sort moves it behind every other primitive and the tree is built without it: the Moeller-
+// Trumbore test rejects den = dot(Ng, d) = 0 for every ray (tri_hit4: den != 0), so such a triangle
+// can never be a closest hit or an occluder — excluding it changes no result, and removes boxes that
+// all contain the pole from the fan every polar ray crosses.
+__global__ void k_morton(BuildIn in, uint32_t N, const float4* blo, const float4* bhi, const uint32_t* cb, uint64_t* keys,
+                         uint32_t* vals, uint32_t* ndeg) {
   float lo[3], ext[3];
   for (int k = 0; k < 3; ++k) {
     lo[k] = ord2f(cb[k]);
@@ -150,7 +166,14 @@ __global__ void k_morton(uint32_t N, const float4* blo, const float4* bhi, const
       const float q = fminf(fmaxf(t * 2097152.0f, 0.0f), 2097151.0f);
       code |= expand21((uint32_t)q) << (2 - k);
     }
-    keys[i] = code;
+    bool deg = false;
+    if (i < in.ntri) {
+      const vec3 ng = tri_ng(in, i);
+      deg = ng.x == 0.0f && ng.y == 0.0f && ng.z == 0.0f;
+    }
+    const uint32_t nd = (uint32_t)__popcll(__ballot(deg));
+    if (nd && __lane_id() == (uint32_t)(__ffsll(__ballot(deg)) - 1)) atomicAdd(ndeg, nd);
+    keys[i] = deg ? (code | (1ull << 63)) : code;
     vals[i] = i;
   }
 }
@@ -172,9 +195,7 @@ __global__ void k_leaves(BuildIn in, const uint32_t* vals, const uint32_t* tri_s
       const vec3 v1 = v3(in.pos[3 * b], in.pos[3 * b + 1], in.pos[3 * b + 2]);
       const vec3 v2 = v3(in.pos[3 * c], in.pos[3 * c + 1], in.pos[3 * c + 2]);
       const vec3 e1 = v0 - v1, e2 = v2 - v0;
-      // Ng = cross(e2, e1) with Embree's msub (fma) evaluation
-      const vec3 ng = v3(__builtin_fmaf(e2.y, e1.z, -(e2.z * e1.y)), __builtin_fmaf(e2.z, e1.x, -(e2.x * e1.z)),
-                         __builtin_fmaf(e2.x, e1.y, -(e2.y * e1.x)));
+      const vec3 ng = tri_ng(in, prim);  // Ng = cross(e2, e1) with Embree's msub (fma) evaluation
       tris[3 * slot + 0] = make_float4(v0.x, v0.y, v0.z, e1.x);
       tris[3 * slot + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
       tris[3 * slot + 2] = make_float4(e2.z, ng.x, ng.y, ng.z);
@@ -1045,10 +1066,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
                const float* h_sph, uint32_t nsph, const uint32_t* h_tri_geom, uint32_t sph_geom_base) {
   const auto t0 = std::chrono::steady_clock::now();
   hipStream_t s = c.stream;
-  const uint32_t N = ntris + nsph;
+  const uint32_t NP = ntris + nsph;
   c.num_tris = ntris;
   c.num_sph = nsph;
-  c.num_nodes = N > 1 ? N - 1 : 0;
+  c.num_nodes = NP > 1 ? NP - 1 : 0;
   c.bvh_depth = 0;
   // + 64 B: the unified wide walk (wide_walk_u) reads a node's 56 B from a direct leaf's primitive address
   LB_CHECK(realloc_buf(c.tris, (size_t)ntris * 48 + 64));
@@ -1058,8 +1079,8 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
   LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));
-  LB_CHECK(realloc_buf(c.prim_ref, ((size_t)N + 3) / 4 * 16));
-  if (N == 0) {
+  LB_CHECK(realloc_buf(c.prim_ref, ((size_t)NP + 3) / 4 * 16));
+  if (NP == 0) {
     c.root = kNoHit;
     c.root4 = kNoHit;
     c.num_nodes4 = 0;
@@ -1089,54 +1110,63 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
            *rflags = nullptr, *dmax = nullptr;
   uint2* kids = nullptr;
-  LB_CHECK(tmp.alloc(&blo, N));
-  LB_CHECK(tmp.alloc(&bhi, N));
+  LB_CHECK(tmp.alloc(&blo, NP));
+  LB_CHECK(tmp.alloc(&bhi, NP));
   LB_CHECK(tmp.alloc(&cb, 8));
-  LB_CHECK(tmp.alloc(&keys, N));
-  LB_CHECK(tmp.alloc(&keys_s, N));
-  LB_CHECK(tmp.alloc(&vals, N));
-  LB_CHECK(tmp.alloc(&vals_s, N));
-  LB_CHECK(tmp.alloc(&flag, N));
-  LB_CHECK(tmp.alloc(&slot, N));
-  LB_CHECK(tmp.alloc(&kids, N));
-  LB_CHECK(tmp.alloc(&leaf_parent, N));
-  LB_CHECK(tmp.alloc(&rflags, N));
+  LB_CHECK(tmp.alloc(&keys, NP));
+  LB_CHECK(tmp.alloc(&keys_s, NP));
+  LB_CHECK(tmp.alloc(&vals, NP));
+  LB_CHECK(tmp.alloc(&vals_s, NP));
+  LB_CHECK(tmp.alloc(&flag, NP));
+  LB_CHECK(tmp.alloc(&slot, NP));
+  LB_CHECK(tmp.alloc(&kids, NP));
+  LB_CHECK(tmp.alloc(&leaf_parent, NP));
+  LB_CHECK(tmp.alloc(&rflags, NP));
   LB_CHECK(tmp.alloc(&dmax, 1));
   const uint32_t cb_init[8] = {~0u, ~0u, ~0u, 0u, 0u, 0u, 0u, 0u};
   LB_CHECK(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
   LB_CHECK(hipMemsetAsync(dmax, 0, 4, s));
-  hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(N)), dim3(256), 0, s, in, blo, bhi, cb);
-  hipLaunchKernelGGL(k_morton, dim3(blocks_for(N)), dim3(256), 0, s, N, blo, bhi, cb, keys, vals);
+  hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(NP)), dim3(256), 0, s, in, blo, bhi, cb);
+  hipLaunchKernelGGL(k_morton, dim3(blocks_for(NP)), dim3(256), 0, s, in, NP, blo, bhi, cb, keys, vals, dmax);
   LB_CHECK(hipGetLastError());
   size_t tbytes = 0;
-  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, N, 0, 63, s));
+  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, NP, 0, 64, s));
   void* tstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
-  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, N, 0, 63, s));
+  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, NP, 0, 64, s));
 #if SPTR_EXPERIMENT_HOST_SAH
   std::vector<uint32_t> sah_order;
   std::vector<BvhNode> sah_nodes;
   uint32_t sah_height = 0;
-  const bool use_sah = N > 1 && c.leaf_size != 8 &&
-                       ((uint64_t)(N - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)N + 3) / 4 * 16) >
+  const bool use_sah = NP > 1 && c.leaf_size != 8 &&
+                       ((uint64_t)(NP - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)NP + 3) / 4 * 16) >
                            kLdsSceneBytes;
   if (use_sah) {
     host_sah(h_pos, h_idx, ntris, h_sph, nsph, sah_order, sah_nodes, sah_height);
-    LB_CHECK(hipMemcpyAsync(vals_s, sah_order.data(), (size_t)N * 4, hipMemcpyHostToDevice, s));
+    LB_CHECK(hipMemcpyAsync(vals_s, sah_order.data(), (size_t)NP * 4, hipMemcpyHostToDevice, s));
   }
 #endif
-  hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(N)), dim3(256), 0, s, N, ntris, vals_s, flag);
+  hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(NP)), dim3(256), 0, s, NP, ntris, vals_s, flag);
   size_t sbytes = 0;
-  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, N, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, NP, rocprim::plus<uint32_t>(), s));
   void* sstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&sstore), sbytes));
-  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, N, rocprim::plus<uint32_t>(), s));
-  hipLaunchKernelGGL(k_leaves, dim3(blocks_for(N)), dim3(256), 0, s, in, vals_s, slot,
+  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, NP, rocprim::plus<uint32_t>(), s));
+  hipLaunchKernelGGL(k_leaves, dim3(blocks_for(NP)), dim3(256), 0, s, in, vals_s, slot,
                      static_cast<float4*>(c.tris.p), static_cast<uint32_t*>(c.tri_geom.p),
                      static_cast<uint32_t*>(c.tri_orig.p), static_cast<float4*>(c.sph.p),
                      static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p),
                      static_cast<uint32_t*>(c.prim_ref.p));
   LB_CHECK(hipGetLastError());
+  // the tree covers the first N sorted primitives: all but the exactly degenerate triangles (k_morton),
+  // unless every primitive is one
+  uint32_t ndeg = 0;
+  LB_CHECK(hipMemcpyAsync(&ndeg, dmax, 4, hipMemcpyDeviceToHost, s));
+  LB_CHECK(hipStreamSynchronize(s));
+  LB_CHECK(hipMemsetAsync(dmax, 0, 4, s));
+  const uint32_t N = ndeg < NP ? NP - ndeg : NP;
+  c.excluded_prims = NP - N;
+  c.num_nodes = N > 1 ? N - 1 : 0;
   // automatic leaf size (measured, profiles/r01*, r02g_leaf.txt): ranges of 8 for scenes small enough
   // to be staged in LDS (fewer, divergence-free node steps), single primitives for meshes traversed
   // from L2/HBM (with the greedy wide collapse: C5 14.9 -> 13.9, C3 5.04 -> 4.87 ms/step vs 2)

@@ -346,6 +346,7 @@ struct Context {
   uint32_t treelet_passes = SPTR_TREELET_PASSES;  // SAH treelet passes over L2/HBM scenes' LBVH (kernels_lbvh.hip)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_nodes4 = 0, root4 = 0;
+  uint32_t excluded_prims = 0;  // exactly degenerate triangles left out of the BVH (never hit; k_morton)
   uint32_t num_top4 = 0;  // wide nodes numbered first: the top kTopLevels levels
   uint32_t stack_need2 = 0, stack_need4 = 0;  // traversal stack entries the BVH2 / BVH4 can need
   DevBuf nodes4;
