@@ -571,6 +571,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
     const bool fuse_bounce = fuse && !no_bounce && (uint64_t)fv.P * kk <= kFuseBouncePaths;
+    // larger batches fuse only their late bounces, whose queues are short (SPTR_FUSE_FROM: first fused
+    // bounce of a large batch, for A/B; 0 = none)
+    static const int fuse_from_env = getenv("SPTR_FUSE_FROM") ? atoi(getenv("SPTR_FUSE_FROM")) : 0;
+    const int fuse_from = fuse_bounce ? 1 : ((fuse && !no_bounce && fuse_from_env > 0) ? fuse_from_env : D + 1);
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
@@ -594,7 +598,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
         tmj.end();
         break;
       }
-      if (d >= 1 && fuse_bounce) {  // trace + shade (+ shadow) of this bounce in one launch
+      if (d >= fuse_from) {  // trace + shade (+ shadow) of this bounce in one launch
         WaveView wf = w;
         wf.segN = rays_tab;
         wf.segH = spare_tab;
