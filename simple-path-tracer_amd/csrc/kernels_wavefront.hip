@@ -686,6 +686,9 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
 #ifndef SPTR_WALK_UNIFIED
 #define SPTR_WALK_UNIFIED 1
 #endif
+#ifndef SPTR_PRIMARY_UNIFIED
+#define SPTR_PRIMARY_UNIFIED 1  // camera rays too (k_trace_dyn<primary>); 0: the leaf-inline walk
+#endif
 template <bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
                                             uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
@@ -1657,11 +1660,11 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
       continue;                                       // only invalid (outside-image) items taken
     }
-    // camera rays keep the leaf-inline walk: coherent lanes reach their leaves together, and testing a
-    // node's leaves before descending tightens tfar early (r03x A/B: C5 bounce 0 2.15 ms inline vs 2.37
-    // unified; bounces 1-2 3.06 vs 2.71)
+    // the unified walk for camera rays as well (r03zy, with the pole ring's degenerate triangles out of
+    // the tree and the launches overlapped: C5 8.45 inline vs 8.22 ms/step unified, means of 3; r03x,
+    // before both: 2.15 vs 2.37 ms for the bounce-0 trace)
     if (have && !done)
-      done = walk_steps<false, kCount, kW4, !kPrimary && SPTR_WALK_UNIFIED>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
+      done = walk_steps<false, kCount, kW4, (!kPrimary || SPTR_PRIMARY_UNIFIED) && SPTR_WALK_UNIFIED>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
                                                                           kDynSteps);
 #ifdef SPTR_EXPERIMENT_STEP_CAP
     if (have && !done && ++rounds >= (uint32_t)SPTR_EXPERIMENT_STEP_CAP) done = true;
