@@ -500,6 +500,26 @@ def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
             assert a[1:] == ref[1:], mode
 
 
+def test_many_direct_calls(renderer):
+    """Hundreds of direct-launch calls of an L2-scene frame (each forks k_sky and the shadow launches to
+    the context's second streams and joins them back): the runtime must not accumulate state across
+    calls (a HIP stack overflow was once seen deep into a run of cross-stream calls), and every call
+    must give the same image."""
+    W, H = 96, 64
+    sptr.setup_default(renderer, "sphere_mesh", 60, 120)
+    cam = sptr.camera_lookat(aspect=W / H)
+    try:
+        renderer.set_launch_mode(1)
+        renderer.render(cam, W, H, spp=4, frame_begin=1)
+        ref = renderer.read_accum().copy()
+        for _ in range(400):
+            renderer.render(cam, W, H, spp=4, frame_begin=1, flags=sptr.SPTR_FRAME_ASYNC)
+        renderer.collect_stats()
+        assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32))
+    finally:
+        renderer.set_launch_mode(0)
+
+
 @pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])
 def test_graph_replay_after_camera_switch(renderer, scene, p0, p1):
     """A launch graph captured for camera A must run against A's pixel-cull mask when it is replayed
