@@ -56,7 +56,7 @@ XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 128, "c4": 64, "c5": 64}  # ~1-4 s per run on 16 host threads
 # experiment knobs of the library and the build (timing studies only); a bench line records any that
 # is set, so a stray variable cannot silently change a measured number
-KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU", "SPTR_OVERLAP", "SPTR_LANES", "SPTR_FUSE_FROM")
+KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU", "SPTR_OVERLAP", "SPTR_LANES", "SPTR_FUSE_FROM", "SPTR_SKY_BLOCKS")
 
 
 class _DevArray:

@@ -3455,7 +3455,9 @@ void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint3
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 
 void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
-  const unsigned g = std::min<unsigned>((f.P + kBlock - 1u) / kBlock, 16384u);
+  // SPTR_SKY_BLOCKS (A/B): a smaller grid-stride grid, leaving wave slots to the launches overlapped with it
+  static const unsigned cap = getenv("SPTR_SKY_BLOCKS") ? (unsigned)atoi(getenv("SPTR_SKY_BLOCKS")) : 16384u;
+  const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
   if (sh.env.env != nullptr) hipLaunchKernelGGL(k_sky<true>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
   else hipLaunchKernelGGL(k_sky<false>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
 }
