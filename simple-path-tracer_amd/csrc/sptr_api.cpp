@@ -857,12 +857,6 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
 }  // namespace
 }  // namespace sptr
 
-using namespace sptr;
-
-extern "C" {
-
-int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
-
 namespace sptr {
 namespace {
 std::vector<hipEvent_t*> dep_events(Context& c) {
@@ -878,6 +872,13 @@ bool create_events(Context& c) {
 }
 }  // namespace
 }  // namespace sptr
+
+using namespace sptr;
+
+extern "C" {
+
+int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
+
 
 // SPTR_SEGV_TRACE=1 (diagnostics): a host SIGSEGV prints the native backtrace before the default action
 static void segv_trace(int sig) {
