@@ -86,3 +86,22 @@ def test_no_shadow_launches_no_entry(bench):
     st = _step_stats(1)
     st.shadow_launches = 0
     assert bench.shadow_roofline(CNT, [st], HBM, "no_such_workload", 1) is None
+
+
+@pytest.mark.parametrize("tag,wl", [("r03za", "c2"), ("r03za", "c4"), ("r03zf", "c3"), ("r03zf", "c5")])
+def test_committed_lines_recompute_from_kernel_stats(tag, wl):
+    """Each committed bench line's roofline fraction recomputes from the rocprofv3 kernel statistics of
+    the same session (tools/recompute_roofline.py: the timed-path instantiations pooled over their
+    launches): within 5 % for LDS scenes; within 10 % where the library overlaps launches on a second
+    stream (C3, C5), whose durations depend on what ran beside them in each run."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("recompute_roofline", os.path.join(root, "tools", "recompute_roofline.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = mod.recompute(os.path.join(root, "profiles", f"{tag}_bench_{wl}.json"),
+                        os.path.join(root, "profiles", f"{tag}_kernel_stats_{wl}.csv"))
+    tol = 0.05 if wl in ("c2", "c4") else 0.10
+    assert "roofline" in out
+    for key, r in out.items():
+        assert r["stats_launches"] > 0, key
+        assert r["rel_diff"] <= tol, (key, r)
