@@ -43,6 +43,9 @@ import sptr  # noqa: E402
 import workloads  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# LDS aggregate read bandwidth with every CU streaming ds_read_b64/b128 (MI355X_MICROARCH.md §LDS, ~150 TB/s):
+# the roof §8(d)'s node/primitive bytes are priced against for scenes staged in LDS
+LDS_PEAK_GBS = 150000.0
 # VALU issue peak: a wave issues one VALU instruction per 2 cycles on its SIMD (MI355X_MICROARCH.md),
 # 256 CUs x 4 SIMDs x 0.5 x 2.4 GHz = 1.2288e12 wave-instructions/s
 VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 0.5 * 2.4e9
@@ -56,7 +59,8 @@ XCDS = 8
 CPU_SAMPLE_SPP = {"c1": 4, "c2": 64, "c3": 128, "c4": 64, "c5": 64}  # ~1-4 s per run on 16 host threads
 # experiment knobs of the library and the build (timing studies only); a bench line records any that
 # is set, so a stray variable cannot silently change a measured number
-KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU", "SPTR_OVERLAP", "SPTR_LANES", "SPTR_FUSE_FROM", "SPTR_SKY_BLOCKS")
+KNOB_VARS = ("SPTR_LIB", "SPTR_ABLATE", "SPTR_MAX_BLOCKS_PER_CU", "SPTR_OVERLAP", "SPTR_FUSE_FROM", "SPTR_SKY_BLOCKS",
+             "SPTR_FOLD", "SPTR_NO_FUSE", "SPTR_NO_DYN", "SPTR_DYN_LDS", "SPTR_NO_BOUNCE")
 
 
 class _DevArray:
@@ -131,7 +135,10 @@ def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
       lds  scene staged in LDS (lds_bytes > 0): node/primitive fetches never leave the CU;
       l2   scene fits one XCD's 4 MB L2: one scene copy per XCD per launch;
       hbm  larger scenes (C5, 1.1 GB > the 256 MB MALL): every visit counts, as in SURVEY.md §8(d).
-    frac_s8d: §8(d) taken literally (36 B per traversed ray and every visit charged, whatever the residency).
+    s8d: §8(d) taken literally (36 B per traversed ray and every visit charged, whatever the residency),
+    priced against the roof those bytes actually stream from: HBM for l2/hbm scenes (frac_s8d), the LDS
+    aggregate read bandwidth for LDS-staged scenes (s8d_lds_frac; no HBM fraction is given for them, since
+    their node/primitive reads never reach HBM).
     Beside them: counter_frac / valu_issue_frac / salu_per_valu from the session's rocprofv3 passes."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
@@ -160,9 +167,14 @@ def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
     out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
     out.update(_counter_fracs(wl_name, "trace", avg_launch_s, stream_read / max(1, launches)))
+    if residency == "lds":
+        out["s8d_lds_frac"] = round(s8d / avg_launch_s / 1e9 / LDS_PEAK_GBS, 4) if avg_launch_s else None
+    else:
+        out["frac_s8d"] = round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None
     out.update({
-        "frac_s8d": round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None,
+        "s8d_bytes_per_launch": round(s8d),
         "bytes_per_launch": round(per_launch), "stream_bytes_per_launch": round(stream / max(1, launches)),
+        "scene_hbm_bytes_per_bounce_ray": round(scene_b) if residency == "hbm" else 0,
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches_per_step": round(launches / max(1, steps), 3),
         "traversed_rays_per_launch": round((tp + tb) / max(1, launches)),
@@ -221,6 +233,48 @@ def shadow_roofline(cnt, stats, layout, wl_name, steps):
     if any(hist):
         out["visit_hist_log2"] = [int(x) for x in hist]
     return out
+
+
+# k_shade per shaded hit: hit record (12) + ray origin/direction (32) + throughput (16) read, continuation
+# ray (o, d, thr: 48) written, radiance read-modify-write (32)
+SHADE_BYTES_PER_HIT = 12.0 + 32.0 + 16.0 + 48.0 + 32.0
+SHADOW_TASK_WRITE_BYTES = 32.0  # a shadow task written by k_shade where the shadow ray has a launch of its own
+ACCUM_BYTES_PER_PIXEL = 32.0 + 7.0  # accum read-modify-write; resolved RGBA8 tile + RGB8 image written
+
+
+def step_roofline(cnt, stats, steps, ms_per_step, trace, shadow, pixels, spp, cube_env=False):
+    """Whole-step algorithmic HBM bytes over ms_per_step: every kernel of the step, not one launch.
+      trace   the trace roofline's bytes per launch x its launches per step (traversed rays only)
+      shadow  likewise for k_shadow(_dyn) (scenes whose shadow rays have launches of their own)
+      shade   SHADE_BYTES_PER_HIT per hit of the wavefront trace launches (+ the shadow task written,
+              where shadow rays have launches of their own)
+      tail    k_tail keeps path state in registers: only its closest-hit rays' node/primitive bytes, for
+              HBM scenes (the bounce rays' per-ray scene bytes)
+      sky     culled camera samples: 4 cubemap texels (64 B) each with an HDR environment; the culled
+              pixels' accum read-modify-write (32 B)
+      accum   ACCUM_BYTES_PER_PIXEL per pixel + the 16-B radiance read of every traversed camera path
+    This is a model of the bytes the algorithm must move, priced at the HBM peak; the measured step is
+    latency-bound, so frac is well below 1."""
+    tp = sum(s.traced_primary for s in stats) / steps
+    tb = sum(s.traced_bounce for s in stats) / steps
+    samples = sum(s.samples for s in stats) / steps
+    tail_rays = sum(s.rays_tail for s in stats) / steps
+    hp = getattr(cnt, "hits_primary", 0) / max(1, cnt.traced_primary)
+    hb = getattr(cnt, "hits_bounce", 0) / max(1, cnt.traced_bounce)
+    hits = tp * hp + tb * hb
+    parts = {
+        "trace": trace["bytes_per_launch"] * trace["launches_per_step"],
+        "shadow": shadow["bytes_per_launch"] * shadow["launches_per_step"] if shadow else 0.0,
+        "shade": hits * (SHADE_BYTES_PER_HIT + (SHADOW_TASK_WRITE_BYTES if shadow else 0.0)),
+        "tail": tail_rays * trace.get("scene_hbm_bytes_per_bounce_ray", 0),
+        "sky": (samples - tp) * (ENV_TEXEL_BYTES if cube_env else 0.0) + (samples - tp) / max(1, spp) * 32.0,
+        "accum": pixels * ACCUM_BYTES_PER_PIXEL + tp * RAD_BYTES,
+    }
+    total = sum(parts.values())
+    achieved = total / (ms_per_step * 1e-3) / 1e9 if ms_per_step > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_step": round(total), "ms_per_step": round(ms_per_step, 4),
+            "bytes_by_kernel": {k: round(v) for k, v in parts.items()}}
 
 
 def host_cpus():
@@ -376,8 +430,12 @@ def main():
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
-    ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1],
-                    help="0: replay captured launch graphs (default); 1: direct launches (timing studies)")
+    ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2],
+                    help="0: replay captured launch graphs (default); 1: direct launches; 2: direct launches on one "
+                         "stream, no overlap (timing studies)")
+    ap.add_argument("--no-serial-pass", action="store_true",
+                    help="skip the untimed one-stream pass (launch mode 2) that times the trace / shadow launches "
+                         "alone for scenes whose launches overlap")
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="timing experiment on one GPU: render only shard 0 of G (the per-rank work of a G-GPU run); "
                          "the line is marked emulated and is not a G-GPU measurement")
@@ -432,6 +490,9 @@ def main():
         r.set_tail_depth(args.tail_depth)
     if args.launch_mode:
         r.set_launch_mode(args.launch_mode)
+    # does the library's side stream run beside the render stream on this device (its own hardware
+    # queue)?  Two 200-us one-wave spins, serial vs forked (sptr_overlap_probe)
+    probe = r.overlap_probe()
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
     cam = workloads.camera(wl)
@@ -505,6 +566,24 @@ def main():
     render_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     gather_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
 
+    # untimed one-stream pass (launch mode 2) for scenes whose launches overlap on the side streams: the
+    # trace and shadow launches' own durations, with nothing beside them (roofline_serial)
+    stats_serial = None
+    residency = _residency(layout)[0]
+    if world == 1 and residency != "lds" and not args.no_serial_pass and args.launch_mode == 0 and \
+            args.integrator == "wavefront":
+        r.set_launch_mode(2)
+        step(timing)
+        r.collect_stats()
+        torch.cuda.synchronize()
+        ts0 = time.perf_counter()
+        for i in range(args.steps):
+            step(timing)
+        torch.cuda.synchronize()
+        serial_elapsed = time.perf_counter() - ts0
+        stats_serial = [r.collect_stats()]
+        r.set_launch_mode(0)
+
     rays = sum(s.rays_closest + s.rays_shadow for s in stats)
     samples = sum(s.samples for s in stats)
     traced_p = sum(s.traced_primary for s in stats)
@@ -555,6 +634,7 @@ def main():
                            else "none (1 rank)"),
             "roofline": roofline(cnt, stats, layout, wl.name, args.steps, cube_env=wl.hdr_env),
             "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
+            "overlap_probe": probe,
             "stage_ms_per_step": stage_ms,
             "cull_ms": round(sum(s.ms_cull for s in stats) / args.steps, 4),
             "cull_launches_per_step": sum(s.cull_launches for s in stats) / args.steps,
@@ -573,6 +653,20 @@ def main():
                       "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},
             "cpu_baseline": None,
         }
+        if args.integrator == "wavefront":
+            line["step_roofline"] = step_roofline(cnt, stats, args.steps, elapsed / args.steps * 1e3, line["roofline"],
+                                                  line["shadow_roofline"], samples / max(1, args.steps) / wl.spp / world,
+                                                  wl.spp, cube_env=wl.hdr_env)
+        if stats_serial:
+            rs = roofline(cnt, stats_serial, layout, wl.name, args.steps, cube_env=wl.hdr_env)
+            ss = shadow_roofline(cnt, stats_serial, layout, wl.name, args.steps)
+            line["roofline_serial"] = {
+                "note": "untimed pass with every launch on one stream (launch mode 2): launch durations with nothing "
+                        "beside them; the headline value is the overlapped run's",
+                "ms_per_step": round(serial_elapsed / args.steps * 1e3, 3),
+                "trace": {k: rs[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")},
+                "shadow": {k: ss[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")}
+                if ss else None}
         if knobs:
             line["experiment_knobs"] = knobs
         if args.emulate_shards:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 4
+#define SPTR_ABI_VERSION 5
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -221,11 +221,15 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
  * 1: direct kernel launches for every call; 2: direct launches, all on the render stream (no launch
  * overlapped on the context's second stream).  Results are identical in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
-/* Sample-batch lanes of a wavefront call: 2 runs consecutive batches of the call's samples at the same
- * time on two buffer sets and streams (scenes traversed from L2/HBM only; each lane holds half the
- * batch); 1 keeps one batch at a time; 0 = automatic (the default: 1 — two lanes measured slower on
- * MI355X).  Results are identical either way (tests/test_gpu_configs.py::test_c3_batches_bit_exact). */
-int sptr_set_lanes(sptr_ctx* ctx, uint32_t lanes);
+/* The launch graph the context holds (launch mode 0): valid = 1 once a call shape was captured; its
+ * node count, dependency edges and the nodes on its longest path.  Every captured graph is checked to be
+ * acyclic before it is instantiated (a rejected capture fails the call with SPTR_ERR_HIP). */
+int sptr_graph_info(const sptr_ctx* ctx, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth);
+/* Whether the context's side streams run beside its render stream on this device: ms[0] = two 200-us
+ * one-wave spins on the render stream, ms[1] = one there and one on the shadow side stream, ms[2] = one
+ * there and one on the k_sky side stream (device events).  ms[1], ms[2] near ms[0] / 2: the side
+ * stream has a hardware queue of its own; near ms[0]: its launches serialise with the render stream's. */
+int sptr_overlap_probe(sptr_ctx* ctx, double ms[3]);
 /* Traversal width: 2 (the LBVH as built), 4 (collapsed to 64-B quantised BVH4 nodes), or 0 = automatic (the
  * default: 2 for scenes staged in LDS, 4 otherwise). */
 int sptr_set_bvh_width(sptr_ctx* ctx, uint32_t width);

@@ -3454,9 +3454,20 @@ void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint3
 }
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 
+// sptr_overlap_probe: one wave spinning on the device wall clock (s_memrealtime, a counter read)
+__global__ void k_spin(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+void launch_spin(uint64_t ticks, hipStream_t s) { hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks); }
+
 void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
+#ifdef SPTR_EXPERIMENT_KNOBS
   // SPTR_SKY_BLOCKS (A/B): a smaller grid-stride grid, leaving wave slots to the launches overlapped with it
   static const unsigned cap = getenv("SPTR_SKY_BLOCKS") ? (unsigned)atoi(getenv("SPTR_SKY_BLOCKS")) : 16384u;
+#else
+  constexpr unsigned cap = 16384u;
+#endif
   const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
   if (sh.env.env != nullptr) hipLaunchKernelGGL(k_sky<true>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
   else hipLaunchKernelGGL(k_sky<false>, dim3(g), dim3(kBlock), 0, s, sh.env, f);

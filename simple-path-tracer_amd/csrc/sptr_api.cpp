@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -119,8 +120,8 @@ uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
 // pixel slot it owns, so its segment slack is kMaxSegs * kBlock * k records (k_slack = k); every
 // other producer needs kMaxSegs * kBlock (k_slack = 1).
-int ensure_wave(Context& c, int lane, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
-  WaveBufs& b = c.wb[lane];
+int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
+  WaveBufs& b = c.wb;
   L = L ? L : 1u;
   const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * kHitBytes;
   const bool grow = b.hrec.bytes < hrec_bytes || !(b.cap >= cap && b.L * b.ts >= L * ts && b.rad.p) || !b.seg.p;
@@ -152,8 +153,8 @@ uint32_t task_stride(const Context& c) {
   return 2u;
 }
 
-WaveView wave_view(Context& c, int lane) {
-  const WaveBufs& wb = c.wb[lane];
+WaveView wave_view(Context& c) {
+  const WaveBufs& wb = c.wb;
   WaveView w;
   for (int b = 0; b < 2; ++b) {
     w.rs[b].o = static_cast<float4*>(wb.rs[b][0].p);
@@ -305,12 +306,8 @@ struct StageTimer {
 int collect_pending(Context& c, sptr_stats* stats) {
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (c.pending == 0) return SPTR_OK;
+  // (the side streams' work is joined into pending_stream: complete once it is)
   const hipError_t se = hipStreamSynchronize(c.pending_stream);
-  // the auxiliary streams' work was joined into pending_stream, so it is complete; synchronising them
-  // as well lets the runtime retire their command chains.  (Without it, a long run of direct-launch
-  // calls with cross-stream event waits ended in a stack overflow inside libamdhip64: a recursive walk
-  // over the accumulated fork/join chain, seen in the GPU test suite.)
-  for (hipStream_t st : {c.side_stream, c.lane_stream, c.side2_stream}) (void)hipStreamSynchronize(st);
   double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t trace_launches = 0, shadow_launches = 0;
   for (const StageMark& m : c.marks) {
@@ -448,7 +445,7 @@ constexpr uint32_t kPtFramesPerLaunch = 4;
 uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
-  WaveView w = wave_view(c, 0);
+  WaveView w = wave_view(c);
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool optix = f.integrator == SPTR_INTEGRATOR_OPTIX;
@@ -481,34 +478,45 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
 #endif
 constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 
-// launches overlapped on second streams (SPTR_OVERLAP=0 or launch mode 2: everything on one stream)
+// launches overlapped on the side streams (launch mode 2: everything on one stream)
 bool overlap_enabled(const Context& c) {
-  static const bool env = [] {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static const bool env = [] {  // SPTR_OVERLAP=0: experiment builds only
     const char* e = getenv("SPTR_OVERLAP");
     return !(e && e[0] == '0');
   }();
-  return env && c.launch_mode != 2;
+  if (!env) return false;
+#endif
+  return c.launch_mode != 2;
 }
-// Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s.
+
+// Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s (the
+// caller's stream, or the capture stream inside a graph capture).
 //
-// lanes == 2 (scenes traversed from L2/HBM, path-major bounce 0): consecutive sample batches alternate
-// between two buffer sets ("lanes") and run at the same time, lane 1 on a stream of its own — each
-// launch of these scenes is latency-bound and ends in a long tail, and two independent chains fill
-// each other's idle CUs.  The batches share only the accumulator: the culled pixels' k_sky sums and the
-// k_accum sums must reach accum in sample order, so batch i's k_sky and k_accum wait for batch i-1's.
-// (LDS scenes fold bounce 0 into accum inside the trace kernel, which couples whole batches: 1 lane.)
-uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, int lanes, hipStream_t s, StageTimer& tm) {
+// Side streams, star-shaped: a launch that overlaps the main sequence is forked from s (an event
+// recorded on s, waited on by the side stream) and joined back into s (an event recorded on the side
+// stream, waited on by s); a side stream never waits on an event of the other side stream.  Any
+// other shape breaks the HIP runtime torch ships (ROCm 7.0): a capture in which one forked stream
+// waits on an event recorded by another forked (non-origin) stream — a fork from a fork, or two side
+// streams ordered against each other — ends in an endless recursion inside hipStreamEndCapture, which
+// overflows the host stack (the r03 libamdhip64+0x2d34a8 crash of the two-lane calls;
+// tools/micro/capture_events.hip reproduces it with three streams).  run_call checks every captured
+// graph (check_graph) before instantiating it.
+uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, hipStream_t s, StageTimer& tm) {
   const SceneView sv = scene_view(c);
   const ShadeView sh = shade_view(c);
-  WaveView wl[2] = {wave_view(c, 0), wave_view(c, lanes > 1 ? 1 : 0)};
+  WaveView w = wave_view(c);
   FrameView fv = frame_view(c, f);
   fv.dyn = static_cast<const uint32_t*>(c.dyn.p);
   const bool count = (f.flags & SPTR_FRAME_COUNT_VISITS) != 0;
   const bool fuse = shade_fuses_shadows(sv, sh, count);
 #ifdef SPTR_EXPERIMENT_KNOBS
   static const bool no_bounce = getenv("SPTR_NO_BOUNCE") != nullptr;
+  // SPTR_FUSE_FROM: first fused bounce of a large batch (A/B; 0 = none)
+  static const int fuse_from_env = getenv("SPTR_FUSE_FROM") ? atoi(getenv("SPTR_FUSE_FROM")) : 0;
 #else
   constexpr bool no_bounce = false;
+  constexpr int fuse_from_env = 0;
 #endif
   // bounce-0 pixel-frustum cull mask of this call's camera (every batch of the call shares it): made
   // current by refresh_cull ahead of this launch sequence, or, with SPTR_FRAME_RECULL, computed as the
@@ -526,40 +534,33 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
   }
   uint32_t done = 0, waves = 0;
   const int D = (int)f.max_depth;
-  // launches overlapped on a second stream (SPTR_OVERLAP=0: everything on s, for A/B timing)
   const bool overlap = overlap_enabled(c);
-  const bool cap = s == c.cap_stream;
-  hipStream_t main_s[2] = {s, cap ? c.cap_lane : c.lane_stream};
-  hipStream_t side_s[2] = {cap ? c.cap_side : c.side_stream, cap ? c.cap_side2 : c.side2_stream};
-  // per lane: pending side-stream work (shadow(d): ev_join, k_sky: ev_sky), and whether ev_sky / ev_acc
-  // hold a record the other lane must order after
-  bool join[2] = {false, false}, join_sky[2] = {false, false}, sky_rec[2] = {false, false}, acc_rec[2] = {false, false};
-  auto fork_err = [&](hipError_t e) {
+  const bool cap = tm.capturing;
+  const hipStream_t ss = cap ? c.cap_side : c.side_stream;   // k_shadow_dyn(d)
+  const hipStream_t ks = cap ? c.cap_side2 : c.side2_stream;  // k_sky (apart from the shadow launches it outlasts)
+  const Context::DepEvents& ev = c.dev[cap ? 1 : 0];
+  auto check = [&](hipError_t e) {
     if (e != hipSuccess && tm.err == hipSuccess) tm.err = e;
+  };
+  auto fork_to = [&](hipStream_t side) {  // side's next launches start after everything enqueued on s so far
+    check(hipEventRecord(ev.fork, s));
+    check(hipStreamWaitEvent(side, ev.fork, 0));
+  };
+  // pending side-stream work: shadow(d) (ev.join) and k_sky (ev.sky)
+  bool join = false, join_sky = false;
+  auto join_shadow = [&]() {
+    if (join) check(hipStreamWaitEvent(s, ev.join, 0));
+    join = false;
   };
   // any-hit launches of their own (k_shadow_dyn: scenes traversed from L2/HBM) run on the side stream
   // beside the next bounce's trace: shadow(d) only adds to rad[], which the bounce traces then leave
   // alone (misses deferred to k_shade, WaveView::defer_miss); k_shade(d + 1) overwrites the shadow
-  // tasks and updates rad[], so it, the tail and k_accum wait for shadow(d) (ev_join)
-  const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, wl[0]);
-  wl[0].defer_miss = wl[1].defer_miss = shadow_side ? 1u : 0u;
-  StageTimer tmain1{c, tm.on, tm.trace_only, main_s[1]};
-  StageTimer tside0{c, tm.on, tm.trace_only, side_s[0]}, tside1{c, tm.on, tm.trace_only, side_s[1]};
-  tmain1.capturing = tside0.capturing = tside1.capturing = tm.capturing;
-  StageTimer* tmain[2] = {&tm, &tmain1};
-  StageTimer* tside[2] = {&tside0, &tside1};
-  // lane 1 starts after the call's head on s (k_frame_dyn, k_cull), before lane 0's first batch
-  const bool lane1_forked = lanes > 1 && k < f.spp;
-  if (lane1_forked) {
-    fork_err(hipEventRecord(c.ev_lane, s));
-    fork_err(hipStreamWaitEvent(main_s[1], c.ev_lane, 0));
-  }
-  for (uint32_t batch = 0; done < f.spp; ++batch) {
-    const int j = lanes > 1 ? (int)(batch & 1u) : 0;
-    hipStream_t ms = main_s[j], ss = side_s[j];
-    StageTimer& tmj = *tmain[j];
-    StageTimer& tsj = *tside[j];
-    const WaveView& w = wl[j];
+  // tasks and updates rad[], so it, the tail and k_accum wait for shadow(d) (ev.join)
+  const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, w);
+  w.defer_miss = shadow_side ? 1u : 0u;
+  StageTimer tside{c, tm.on, tm.trace_only, ss};
+  tside.capturing = tm.capturing;
+  while (done < f.spp) {
     const uint32_t kk = std::min<uint32_t>(k, f.spp - done);
     fv.k = kk;
     fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
@@ -571,107 +572,88 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, i
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
     const bool fuse_bounce = fuse && !no_bounce && (uint64_t)fv.P * kk <= kFuseBouncePaths;
-    // larger batches fuse only their late bounces, whose queues are short (SPTR_FUSE_FROM: first fused
-    // bounce of a large batch, for A/B; 0 = none)
-    static const int fuse_from_env = getenv("SPTR_FUSE_FROM") ? atoi(getenv("SPTR_FUSE_FROM")) : 0;
+    // larger batches could fuse only their late bounces, whose queues are short: no gain measured
+    // (r03zx, SPTR_FUSE_FROM 2/3/4 on C2: 3.16-3.25 vs 3.17 ms/step)
     const int fuse_from = fuse_bounce ? 1 : ((fuse && !no_bounce && fuse_from_env > 0) ? fuse_from_env : D + 1);
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
     // fused bounces alternate the ray tables: the table holding the current rays, and the other
     SegTable rays_tab = w.segN, spare_tab = w.segH;
-    auto wait_side = [&]() {
-      if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));
-      if (join_sky[j]) fork_err(hipStreamWaitEvent(ms, c.ev_sky[j], 0));
-      join[j] = join_sky[j] = false;
-    };
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
         // (shadow(d - 1) adds to rad[], which the tail reads; k_sky only to the culled pixels' accum,
         // joined before k_accum, so the tail runs beside it: C3's k_sky outlasts the whole bounce chain)
-        if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));
-        join[j] = false;
+        join_shadow();
         WaveView wt = w;
         wt.segN = rays_tab;
-        tmj.begin(7);
-        launch_tail(sv, sh, fv, wt, d, g_shade, ms);
-        tmj.end();
+        tm.begin(7);
+        launch_tail(sv, sh, fv, wt, d, g_shade, s);
+        tm.end();
         break;
       }
       if (d >= fuse_from) {  // trace + shade (+ shadow) of this bounce in one launch
         WaveView wf = w;
         wf.segN = rays_tab;
         wf.segH = spare_tab;
-        tmj.begin(2);
-        g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, ms);
-        tmj.end();
+        tm.begin(2);
+        g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, s);
+        tm.end();
         std::swap(rays_tab, spare_tab);
         continue;
       }
       const bool sky = d == 0 && fv.sky_fold;  // the culled pixels' environment sums: accumulation, not k_trace
-      const bool sky_side = sky && (overlap || lanes > 1);
+      const bool sky_side = sky && overlap;
       if (sky && !sky_side) {
-        tmj.begin(4);
-        launch_sky(sh, fv, ms);
-        tmj.end();
+        tm.begin(4);
+        launch_sky(sh, fv, s);
+        tm.end();
       }
-      if (sky_side) fork_err(hipEventRecord(c.ev_fork[j], ms));
-      tmj.begin(d == 0 ? 5 : 1);
-      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, ms);
-      tmj.end();
+      // k_sky forks at the same point as the bounce-0 trace (it writes only the culled pixels' accum
+      // words, which nothing reads before this batch's k_accum, the join point): its VALU-bound blocks
+      // fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.  Enqueued
+      // after the trace, so that the trace's grid is dispatched first.
+      if (sky_side) check(hipEventRecord(ev.fork, s));
+      tm.begin(d == 0 ? 5 : 1);
+      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
+      tm.end();
       if (sky_side) {
-        // on the side stream, concurrent with the bounce-0 trace (it writes only the culled pixels'
-        // accum words, which nothing reads before this batch's k_accum, the join point): its VALU-bound
-        // blocks fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.
-        // Submitted after the trace (both wait for the same point), so the trace's grid is dispatched first.
-        // One-lane calls put it on the second side stream, so that the shadow launches queued on the
-        // first one do not wait behind it.
-        const bool after_other = lanes > 1 && sky_rec[1 - j];  // sample order in accum: the previous batch's k_sky first
-        hipStream_t ks = lanes > 1 ? ss : side_s[1];
-        fork_err(hipStreamWaitEvent(ks, c.ev_fork[j], 0));
-        if (after_other) fork_err(hipStreamWaitEvent(ks, c.ev_sky[1 - j], 0));
+        check(hipStreamWaitEvent(ks, ev.fork, 0));
         launch_sky(sh, fv, ks);
-        fork_err(hipEventRecord(c.ev_sky[j], ks));
-        join_sky[j] = sky_rec[j] = true;
+        check(hipEventRecord(ev.sky, ks));
+        join_sky = true;
       }
-      if (join[j]) fork_err(hipStreamWaitEvent(ms, c.ev_join[j], 0));  // shadow(d - 1) before shade(d)
-      join[j] = false;
-      tmj.begin(d == 0 ? 6 : 2);
-      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, ms);
-      tmj.end();
+      join_shadow();  // shadow(d - 1) before shade(d)
+      tm.begin(d == 0 ? 6 : 2);
+      g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
+      tm.end();
       if (!fuse && shadow_side) {
-        fork_err(hipEventRecord(c.ev_fork[j], ms));
-        fork_err(hipStreamWaitEvent(ss, c.ev_fork[j], 0));
-        tsj.begin(3);
+        fork_to(ss);
+        tside.begin(3);
         launch_shadow(sv, sh, w, d, count, g_shade, ss);
-        tsj.end();
-        fork_err(hipEventRecord(c.ev_join[j], ss));
-        join[j] = true;
+        tside.end();
+        check(hipEventRecord(ev.join, ss));
+        join = true;
       } else if (!fuse) {
-        tmj.begin(3);
-        launch_shadow(sv, sh, w, d, count, g_shade, ms);
-        tmj.end();
+        tm.begin(3);
+        launch_shadow(sv, sh, w, d, count, g_shade, s);
+        tm.end();
       }
     }
     // the call's last batch resolves in the same launch (k_accum<true>: each thread resolves the
     // sum it holds, as k_resolve would next)
     const bool resolve = done + kk >= f.spp && !(f.flags & SPTR_FRAME_NO_RESOLVE);
-    wait_side();
-    if (lanes > 1 && acc_rec[1 - j]) fork_err(hipStreamWaitEvent(ms, c.ev_acc[1 - j], 0));  // sample order
-    tmj.begin(4);
+    join_shadow();
+    if (join_sky) check(hipStreamWaitEvent(s, ev.sky, 0));
+    join_sky = false;
+    tm.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
-                      static_cast<uint8_t*>(c.image.p), resolve, ms);
-    tmj.end();
-    if (lanes > 1) {
-      fork_err(hipEventRecord(c.ev_acc[j], ms));
-      acc_rec[j] = true;
-    }
+                      static_cast<uint8_t*>(c.image.p), resolve, s);
+    tm.end();
     done += kk;
     ++waves;
   }
-  if (lane1_forked) fork_err(hipStreamWaitEvent(s, c.ev_acc[1], 0));  // join lane 1 (its last k_accum)
-  for (StageTimer* t : {&tmain1, &tside0, &tside1})
-    if (t->err != hipSuccess && tm.err == hipSuccess) tm.err = t->err;
+  if (tside.err != hipSuccess && tm.err == hipSuccess) tm.err = tside.err;
   tm.end_call();
   return waves;
 }
@@ -686,10 +668,7 @@ int refresh_cull(Context& c, const sptr_frame& f, hipStream_t s, bool timing) {
   if (f.flags & SPTR_FRAME_NO_CULL) return SPTR_OK;
   const uint32_t depth = cull_depth_for(f.spp);
   if (f.flags & SPTR_FRAME_RECULL) {  // the call's own launch sequence computes the mask (enqueue_wavefront)
-    c.cull_epoch = c.epoch;
-    c.cull_cam = f.camera;
-    c.cull_depth = depth;
-    ++c.pending_culls;
+    c.cull_epoch = 0;  // the cached key is set once that sequence is enqueued (sptr_render)
     return SPTR_OK;
   }
   if (!(f.flags & SPTR_FRAME_RECULL) && c.cull_epoch == c.epoch && c.cull_depth == depth &&
@@ -713,6 +692,73 @@ int refresh_cull(Context& c, const sptr_frame& f, hipStream_t s, bool timing) {
 
 bool same_key(const GraphKey& a, const GraphKey& b) { return std::memcmp(&a, &b, sizeof(GraphKey)) == 0; }
 
+// A captured launch graph is accepted only if it is a DAG of bounded depth: nodes, dependency
+// edges and the number of nodes on its longest path (Kahn's algorithm over hipGraphGetEdges).  The
+// fork/join plan of enqueue_wavefront yields ~10-200 nodes whose longest path is the main sequence;
+// a cycle, or a path longer than the node count, means a broken plan.
+struct GraphShape {
+  uint32_t nodes = 0, edges = 0, depth = 0;
+};
+constexpr size_t kMaxGraphNodes = 4096;
+bool check_graph(hipGraph_t g, GraphShape& out, std::string& why) {
+  size_t n = 0, ne = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess || hipGraphGetEdges(g, nullptr, nullptr, &ne) != hipSuccess) {
+    why = "hipGraphGetNodes/Edges failed";
+    return false;
+  }
+  if (n == 0 || n > kMaxGraphNodes) {
+    why = std::to_string(n) + " nodes";
+    return false;
+  }
+  std::vector<hipGraphNode_t> nodes(n), from(ne), to(ne);
+  if (hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess ||
+      (ne && hipGraphGetEdges(g, from.data(), to.data(), &ne) != hipSuccess)) {
+    why = "hipGraphGetNodes/Edges failed";
+    return false;
+  }
+  std::vector<std::pair<hipGraphNode_t, uint32_t>> index(n);
+  for (size_t i = 0; i < n; ++i) index[i] = {nodes[i], (uint32_t)i};
+  std::sort(index.begin(), index.end());
+  auto id_of = [&](hipGraphNode_t x) -> int64_t {
+    const auto it = std::lower_bound(index.begin(), index.end(), std::make_pair(x, 0u));
+    return (it != index.end() && it->first == x) ? (int64_t)it->second : -1;
+  };
+  std::vector<uint32_t> indeg(n, 0), level(n, 1);
+  std::vector<std::vector<uint32_t>> succ(n);
+  for (size_t e = 0; e < ne; ++e) {
+    const int64_t a = id_of(from[e]), b = id_of(to[e]);
+    if (a < 0 || b < 0) {
+      why = "edge to an unknown node";
+      return false;
+    }
+    succ[(size_t)a].push_back((uint32_t)b);
+    ++indeg[(size_t)b];
+  }
+  std::vector<uint32_t> ready;
+  for (uint32_t i = 0; i < n; ++i)
+    if (indeg[i] == 0) ready.push_back(i);
+  size_t seen = 0;
+  uint32_t depth = 0;
+  while (!ready.empty()) {
+    const uint32_t v = ready.back();
+    ready.pop_back();
+    ++seen;
+    depth = std::max(depth, level[v]);
+    for (uint32_t w : succ[v]) {
+      level[w] = std::max(level[w], level[v] + 1);
+      if (--indeg[w] == 0) ready.push_back(w);
+    }
+  }
+  out.nodes = (uint32_t)n;
+  out.edges = (uint32_t)ne;
+  out.depth = depth;
+  if (seen != n) {
+    why = "dependency cycle (" + std::to_string(n - seen) + " of " + std::to_string(n) + " nodes)";
+    return false;
+  }
+  return true;
+}
+
 void drop_graph(Context& c) {
   if (c.graph.exec) (void)hipGraphExecDestroy(c.graph.exec);
   if (c.graph.graph) (void)hipGraphDestroy(c.graph.graph);
@@ -730,10 +776,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
-  // two-lane calls launch directly: their launches are long (L2/HBM scenes, ~20 launches of 0.1-2 ms),
-  // so a graph saves nothing measurable, and capturing the four-stream fork/join sequence repeatedly
-  // ended in a stack overflow inside libamdhip64 (recursion at +0x2d34a8) in the GPU test suite
-  if (c.launch_mode != 0 || key.lanes > 1 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+  if (c.launch_mode != 0 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
     StageTimer tm{c, timing, trace_only, s};
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
@@ -743,6 +786,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   }
   if (!(c.graph.valid && same_key(key, c.graph.key))) {  // capture this shape
     drop_graph(c);
+    GraphShape gshape;
     const size_t m0 = c.marks.size(), e0 = c.events_used;
     // the pool must not grow inside the capture (hipEventCreate is not a capturable call): every
     // span of a call uses two events; 512 covers 255 spans (> 6 batches x 6 bounces x 3 stages)
@@ -760,6 +804,22 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     const std::vector<StageMark> cap_marks(c.marks.begin() + (std::ptrdiff_t)m0, c.marks.end());
     c.marks.resize(m0);  // the capture executed nothing
     c.events_used = e0;
+    // every stream the capture forked must have left capture mode with it (a stream still capturing
+    // would fold the next direct launches into a dead graph)
+    for (hipStream_t st : {c.cap_stream, c.cap_side, c.cap_side2}) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        if (g) (void)hipGraphDestroy(g);
+        return fail(c, SPTR_ERR_HIP, "render: graph capture: a forked stream is still capturing (internal error)");
+      }
+    }
+    if (ec == hipSuccess && tm.err == hipSuccess && g) {
+      std::string why;
+      if (!check_graph(g, gshape, why)) {
+        (void)hipGraphDestroy(g);
+        return fail(c, SPTR_ERR_HIP, "render: captured graph rejected: " + why);
+      }
+    }
     if (ec != hipSuccess || tm.err != hipSuccess || !g) {
       // not capturable (e.g. more stage spans than the pre-grown event pool): direct launches
       if (g) (void)hipGraphDestroy(g);
@@ -775,6 +835,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     gc.graph = g;
     gc.key = key;
     gc.waves = nw;
+    gc.nodes = gshape.nodes + 1;  // + the k_frame_dyn head added below, ahead of every root
+    gc.depth = gshape.depth + 1;
     // the k_frame_dyn node heads the graph: every captured root depends on it
     size_t nr = 0;
     API_HIP(hipGraphGetRootNodes(g, nullptr, &nr));
@@ -793,6 +855,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     kp.extra = nullptr;
     API_HIP(hipGraphAddKernelNode(&gc.dyn_node, g, nullptr, 0, &kp));
     for (hipGraphNode_t r : roots) API_HIP(hipGraphAddDependencies(g, &gc.dyn_node, &r, 1));
+    gc.edges = gshape.edges + (uint32_t)nr;
     gc.dyn_params = kp;
     // event-record nodes of the stage spans, matched through the pool events they recorded
     size_t n = 0;
@@ -860,9 +923,9 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
 namespace sptr {
 namespace {
 std::vector<hipEvent_t*> dep_events(Context& c) {
-  std::vector<hipEvent_t*> v{&c.ev_lane};
-  for (int j = 0; j < 2; ++j)
-    for (hipEvent_t* e : {&c.ev_fork[j], &c.ev_join[j], &c.ev_sky[j], &c.ev_acc[j]}) v.push_back(e);
+  std::vector<hipEvent_t*> v;
+  for (Context::DepEvents& d : c.dev)
+    for (hipEvent_t* e : {&d.fork, &d.join, &d.sky}) v.push_back(e);
   return v;
 }
 bool create_events(Context& c) {
@@ -880,7 +943,10 @@ extern "C" {
 int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
 
 
-// SPTR_SEGV_TRACE=1 (diagnostics): a host SIGSEGV prints the native backtrace before the default action
+// SPTR_SEGV_TRACE=1 (diagnostics only): a host SIGSEGV prints the native backtrace before the default
+// action.  Installed once per process, on the first sptr_create, for the thread that creates the
+// context (its alternate signal stack); the backtrace machinery is primed at install time, so the
+// handler's backtrace() call does not load anything.
 static void segv_trace(int sig) {
   void* fr[64];
   const int n = backtrace(fr, 64);
@@ -890,17 +956,21 @@ static void segv_trace(int sig) {
 }
 
 static void install_segv_trace() {
-  static const bool on = getenv("SPTR_SEGV_TRACE") != nullptr;
-  if (!on) return;
-  static char alt[1 << 16];
-  stack_t ss{};
-  ss.ss_sp = alt;
-  ss.ss_size = sizeof(alt);
-  sigaltstack(&ss, nullptr);
-  struct sigaction sa{};
-  sa.sa_handler = segv_trace;
-  sa.sa_flags = SA_ONSTACK;
-  sigaction(SIGSEGV, &sa, nullptr);
+  static std::once_flag once;
+  std::call_once(once, [] {
+    if (getenv("SPTR_SEGV_TRACE") == nullptr) return;
+    void* prime[2];
+    (void)backtrace(prime, 2);
+    static char alt[1 << 16];
+    stack_t ss{};
+    ss.ss_sp = alt;
+    ss.ss_size = sizeof(alt);
+    sigaltstack(&ss, nullptr);
+    struct sigaction sa{};
+    sa.sa_handler = segv_trace;
+    sa.sa_flags = SA_ONSTACK;
+    sigaction(SIGSEGV, &sa, nullptr);
+  });
 }
 
 int sptr_create(int device, sptr_ctx** out) {
@@ -922,15 +992,12 @@ int sptr_create(int device, sptr_ctx** out) {
       hipStreamCreateWithPriority(&c.cap_side, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side2_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.cap_side2, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
-      // lane 1's main stream at the highest priority: a hardware queue apart from the caller's stream
-      hipStreamCreateWithPriority(&c.lane_stream, hipStreamNonBlocking, c.prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c.cap_lane, hipStreamNonBlocking, c.prio_hi) != hipSuccess ||
       !create_events(c)) {
     delete x;
     return SPTR_ERR_HIP;
   }
-  if (ensure_buf(c.wb[0].seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
-      ensure_buf(c.dyn, 64) != hipSuccess || hipMemset(c.wb[0].seg.p, 0, seg_table_bytes()) != hipSuccess) {
+  if (ensure_buf(c.wb.seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
+      ensure_buf(c.dyn, 64) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess) {
     delete x;
     return SPTR_ERR_OOM;
   }
@@ -948,12 +1015,10 @@ int sptr_destroy(sptr_ctx* x) {
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
                     &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist};
   for (DevBuf* b : bufs) free_buf(*b);
-  for (WaveBufs& wb : c.wb) {
-    for (DevBuf* b : {&wb.hrec, &wb.rad, &wb.stask, &wb.seg}) free_buf(*b);
-    for (auto& r : wb.rs)
-      for (DevBuf& x : r) free_buf(x);
-  }
-  for (hipStream_t st : {c.lane_stream, c.cap_lane, c.side2_stream, c.cap_side2})
+  for (DevBuf* b : {&c.wb.hrec, &c.wb.rad, &c.wb.stask, &c.wb.seg}) free_buf(*b);
+  for (auto& r : c.wb.rs)
+    for (DevBuf& x : r) free_buf(x);
+  for (hipStream_t st : {c.side2_stream, c.cap_side2})
     if (st) (void)hipStreamDestroy(st);
   drop_graph(c);
   free_buf(c.dyn);
@@ -1144,7 +1209,6 @@ int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
 
 int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
   if (!x || !f) return SPTR_ERR_INVALID;
-  install_segv_trace();
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
   if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "render: no scene uploaded");
@@ -1191,11 +1255,10 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     uint64_t wave_paths = c.wave_paths;
     if (!wave_paths) {  // default: 2^29 paths, or what half of the free HBM holds (at least 2^24)
       wave_paths = kDefaultWavePaths;
-      if (c.wb[0].cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
+      if (c.wb.cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
-          uint64_t held = 0;
-          for (const WaveBufs& wb : c.wb) held += wb.cap ? wb.cap * wave_path_bytes(wb.L, wb.ts) : 0ull;
+          const uint64_t held = c.wb.cap ? c.wb.cap * wave_path_bytes(c.wb.L, c.wb.ts) : 0ull;
           const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
           // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
           const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
@@ -1207,35 +1270,18 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     }
     uint32_t k = (uint32_t)std::max<uint64_t>(1, wave_paths / c.P);
     k = std::min<uint32_t>(k, f->spp);
-    int lanes = 1;
     {
-      const SceneView sv = scene_view(c);
-      // two sample-batch lanes (enqueue_wavefront) for scenes traversed from L2/HBM, whose bounce 0 is
-      // path-major: the call's samples in batches of at most half, each lane sized for its batch (so the
-      // two lanes hold what one lane of k samples would)
-      static const int lanes_env = getenv("SPTR_LANES") ? atoi(getenv("SPTR_LANES")) : 0;
-      // default 1: measured slower (r03zj: C5 8.5-8.6 -> 8.9, C3 3.9 -> 4.6-4.8 ms/step): the refilling
-      // kernels' resident grids occupy every CU slot, so two lanes time-slice rather than overlap, and
-      // each launch keeps its tail at half the batch
-      const uint32_t want = c.lanes ? c.lanes : (lanes_env ? (uint32_t)lanes_env : 1u);
-      if (want >= 2 && sv.lds_bytes == 0 && f->spp >= 2 && c.launch_mode != 2) {
-        lanes = 2;
-        k = std::max<uint32_t>(1u, std::min<uint32_t>((f->spp + 1u) / 2u, k >= f->spp ? k : k / 2u));
-      }
       // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
       FrameView probe = frame_view(c, *f);
       probe.k = k;
-      const uint32_t k_slack = bounce0_pixel_major(sv, probe) ? k : 1u;
-      for (int j = 0; j < lanes; ++j) {
-        rc = ensure_wave(c, j, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
-        if (rc != SPTR_OK) return rc;
-      }
+      const uint32_t k_slack = bounce0_pixel_major(scene_view(c), probe) ? k : 1u;
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
+      if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));
     key.epoch = c.epoch;  // ensure_wave may have reallocated
     key.k = k;
     key.tail = (uint32_t)T;
-    key.lanes = (uint32_t)lanes;
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
     rc = refresh_cull(c, *f, s, timing || trace_timing);
     if (rc != SPTR_OK) return rc;
@@ -1243,8 +1289,14 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     uint32_t* clear = ((f->flags & SPTR_FRAME_RECULL) && !(f->flags & SPTR_FRAME_NO_CULL))
                           ? static_cast<uint32_t*>(c.plist.p) + c.P : nullptr;
     rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, clear, timing || trace_timing, !timing, s,
-                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, lanes, cs, tm); }, waves);
+                  [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
+    if (clear) {  // the sequence just enqueued computes this camera's mask (keyed only once enqueued)
+      c.cull_epoch = c.epoch;
+      c.cull_cam = f->camera;
+      c.cull_depth = cull_depth_for(f->spp);
+      ++c.pending_culls;
+    }
     samples = (uint64_t)frame_view(c, *f).valid * f->spp;
   }
   c.last_samples = total;
@@ -1259,10 +1311,59 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   return collect_pending(c, stats);
 }
 
-int sptr_set_lanes(sptr_ctx* x, uint32_t lanes) {
+int sptr_graph_info(const sptr_ctx* x, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth) {
   if (!x) return SPTR_ERR_INVALID;
-  if (lanes > 2) return fail(x->c, SPTR_ERR_INVALID, "lanes must be 0 (automatic), 1 or 2");
-  x->c.lanes = lanes;
+  const GraphCache& g = x->c.graph;
+  if (valid) *valid = g.valid ? 1u : 0u;
+  if (nodes) *nodes = g.valid ? g.nodes : 0u;
+  if (edges) *edges = g.valid ? g.edges : 0u;
+  if (depth) *depth = g.valid ? g.depth : 0u;
+  return SPTR_OK;
+}
+
+int sptr_overlap_probe(sptr_ctx* x, double* ms) {
+  if (!x || !ms) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  API_HIP(hipSetDevice(c.device));
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  int rate_khz = 0;
+  API_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c.device));
+  if (rate_khz <= 0) return fail(c, SPTR_ERR_HIP, "overlap probe: no wall clock rate");
+  const uint64_t ticks = (uint64_t)rate_khz / 5u;  // 200 us per spin
+  hipEvent_t e0 = nullptr, e1 = nullptr, fk = nullptr, jn = nullptr;
+  API_HIP(hipEventCreate(&e0));
+  API_HIP(hipEventCreate(&e1));
+  API_HIP(hipEventCreateWithFlags(&fk, hipEventDisableTiming));
+  API_HIP(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+  hipError_t err = hipSuccess;
+  auto ck = [&](hipError_t e) {
+    if (e != hipSuccess && err == hipSuccess) err = e;
+  };
+  const hipStream_t s = c.stream;
+  launch_spin(ticks / 8u, s);  // warm the kernel
+  ck(hipStreamSynchronize(s));
+  const hipStream_t sides[3] = {nullptr, c.side_stream, c.side2_stream};
+  for (int i = 0; i < 3; ++i) {
+    const hipStream_t side = sides[i] ? sides[i] : s;
+    ck(hipEventRecord(e0, s));
+    if (side != s) {
+      ck(hipEventRecord(fk, s));
+      ck(hipStreamWaitEvent(side, fk, 0));
+    }
+    launch_spin(ticks, s);
+    launch_spin(ticks, side);
+    if (side != s) {
+      ck(hipEventRecord(jn, side));
+      ck(hipStreamWaitEvent(s, jn, 0));
+    }
+    ck(hipEventRecord(e1, s));
+    ck(hipStreamSynchronize(s));
+    float t = 0.0f;
+    ck(hipEventElapsedTime(&t, e0, e1));
+    ms[i] = t;
+  }
+  for (hipEvent_t e : {e0, e1, fk, jn}) (void)hipEventDestroy(e);
+  if (err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("overlap probe: ") + hipGetErrorString(err));
   return SPTR_OK;
 }
 

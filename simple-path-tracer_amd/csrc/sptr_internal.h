@@ -299,7 +299,7 @@ struct StageMark {
 struct GraphKey {
   uint64_t epoch;
   sptr_frame frame;
-  uint32_t k, tail, lanes, pad1;
+  uint32_t k, tail;
 };
 struct GraphMark {
   int stage;
@@ -314,19 +314,25 @@ struct GraphCache {
   hipKernelNodeParams dyn_params{};
   std::vector<GraphMark> marks;  // stage spans in recording order (re-pointed at fresh events per replay)
   uint32_t waves = 0;
+  // shape of the captured graph (check_graph): nodes, dependency edges, nodes on the longest path
+  uint32_t nodes = 0, edges = 0, depth = 0;
 };
 
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t cap_stream = nullptr;  // launch-graph capture
-  // second streams for launches that overlap the main sequence (direct launches / inside a capture),
-  // forked from and joined back into it by ev_fork / ev_join (enqueue_wavefront)
-  hipStream_t side_stream = nullptr, cap_side = nullptr;
-  // lane 1 of a two-lane call: its main stream (a priority of its own) and its side stream
-  hipStream_t lane_stream = nullptr, cap_lane = nullptr, side2_stream = nullptr, cap_side2 = nullptr;
-  // per lane: fork to the side stream, shadow join, k_sky done, k_accum done; lane-1 fork
-  hipEvent_t ev_fork[2] = {}, ev_join[2] = {}, ev_sky[2] = {}, ev_acc[2] = {}, ev_lane = nullptr;
+  // side streams for launches that overlap the main sequence: the shadow launches (side) and k_sky
+  // (side2), for direct launches and inside a capture (cap_*).  Star-shaped fork/join only: a side
+  // stream waits on events of the call's main stream and the main stream on the side streams', never
+  // one side stream on another (enqueue_wavefront, DESIGN.md §3 "Launch graphs").
+  hipStream_t side_stream = nullptr, cap_side = nullptr, side2_stream = nullptr, cap_side2 = nullptr;
+  // fork to a side stream, shadow join, k_sky join.  The direct launches and the captures each have
+  // their own set (dev[0] direct, dev[1] captured), so an event recorded inside a capture is never
+  // waited on by a direct launch.
+  struct DepEvents {
+    hipEvent_t fork = nullptr, join = nullptr, sky = nullptr;
+  } dev[2];
   int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
   uint32_t launch_mode = 0;          // 0: replay a captured graph for repeated call shapes; 1: direct launches
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
@@ -362,10 +368,8 @@ struct Context {
   DevBuf env;
   int32_t env_size = 0;
   float env_intensity = 0.8f, env_clamp = 5.0f;
-  // wavefront buffers: lane 0, and lane 1 when a call runs two sample batches at once (enqueue_wavefront)
-  WaveBufs wb[2];
+  WaveBufs wb;  // wavefront path state
   DevBuf w_tot;
-  uint32_t lanes = 0;  // sample-batch lanes: 1, 2, or 0 = automatic (sptr_set_lanes)
   // pixel buffers
   int32_t W = 0, H = 0, G = 1, R = 0;
   uint32_t P = 0, local_tiles = 0;
@@ -434,5 +438,7 @@ void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
                   bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, uint32_t* stack_overflow, hipStream_t s);
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s);
+// one wave spinning for `ticks` of the device wall clock (sptr_overlap_probe)
+void launch_spin(uint64_t ticks, hipStream_t s);
 
 }  // namespace sptr

@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_lanes", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -138,7 +138,8 @@ def lib() -> C.CDLL:
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_launch_mode": (C.c_int, [vp, u32]),
-        "sptr_set_lanes": (C.c_int, [vp, u32]),
+        "sptr_graph_info": (C.c_int, [vp, up, up, up, up]),
+        "sptr_overlap_probe": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
@@ -399,12 +400,22 @@ class Renderer:
     def set_wave_paths(self, n: int):
         self._check(self._L.sptr_set_wave_paths(self._h, n), "set_wave_paths")
 
-    def set_lanes(self, lanes: int):
-        """sptr_set_lanes: 2 sample-batch lanes at once (L2/HBM scenes), 1, or 0 = automatic."""
-        self._check(self._L.sptr_set_lanes(self._h, lanes), "set_lanes")
+    def graph_info(self) -> dict:
+        """sptr_graph_info: the held launch graph (valid, nodes, edges, longest-path depth)."""
+        v = [C.c_uint32() for _ in range(4)]
+        self._check(self._L.sptr_graph_info(self._h, *[C.byref(x) for x in v]), "graph_info")
+        return dict(zip(("valid", "nodes", "edges", "depth"), (int(x.value) for x in v)))
+
+    def overlap_probe(self) -> dict:
+        """sptr_overlap_probe: ms of two 200-us spins serial, and beside each side stream."""
+        ms = (C.c_double * 3)()
+        self._check(self._L.sptr_overlap_probe(self._h, ms), "overlap_probe")
+        return {"serial_ms": round(ms[0], 4), "side_ms": round(ms[1], 4), "sky_side_ms": round(ms[2], 4),
+                "side_has_own_queue": bool(ms[1] < 0.75 * ms[0]), "sky_side_has_own_queue": bool(ms[2] < 0.75 * ms[0])}
 
     def set_launch_mode(self, mode: int):
-        """0: replay captured launch graphs for repeated call shapes (default); 1: direct launches."""
+        """0: replay captured launch graphs for repeated call shapes (default); 1: direct launches;
+        2: direct launches, all on the render stream (no overlap)."""
         self._check(self._L.sptr_set_launch_mode(self._h, mode), "set_launch_mode")
 
     def set_tail_depth(self, n: int):

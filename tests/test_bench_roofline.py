@@ -39,7 +39,8 @@ LDS = dict(HBM, tri_bytes=48 * 12, prim_ref_bytes=80, node_bytes=64 * 20, num_no
 def test_frac_independent_of_timed_steps(bench, layout):
     a = bench.roofline(CNT, [_step_stats(1)], layout, "no_such_workload", 1)
     b = bench.roofline(CNT, [_step_stats(20)], layout, "no_such_workload", 20)
-    for k in ("frac", "frac_s8d", "bytes_per_launch", "avg_launch_us", "launches_per_step", "traversed_rays_per_launch"):
+    s8d = "frac_s8d" if layout is HBM else "s8d_lds_frac"
+    for k in ("frac", s8d, "bytes_per_launch", "avg_launch_us", "launches_per_step", "traversed_rays_per_launch"):
         assert a[k] == pytest.approx(b[k], rel=1e-9), k
     sa = bench.shadow_roofline(CNT, [_step_stats(1)], layout, "no_such_workload", 1)
     sb = bench.shadow_roofline(CNT, [_step_stats(20)], layout, "no_such_workload", 20)
@@ -75,6 +76,11 @@ def test_culled_rays_not_charged(bench):
 def test_lds_scene_charges_stream_only(bench):
     r = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1)
     assert r["scene_residency"] == "lds"
+    # §8(d)'s node/primitive bytes of an LDS-staged scene are priced against the LDS roof, never HBM
+    assert "frac_s8d" not in r
+    s8d = (36.0 * (CNT.traced_primary + CNT.traced_bounce) + 64.0 * CNT.node_visits + 48.0 * CNT.tri_tests
+           + 16.0 * CNT.sphere_tests) / 6
+    assert r["s8d_lds_frac"] == pytest.approx(s8d / 0.3e-3 / 1e9 / 150000.0, rel=1e-3)
     assert r["bytes_per_launch"] == pytest.approx(_stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25) / 6,
                                                   rel=1e-6)
     c = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1, cube_env=True)
@@ -105,3 +111,36 @@ def test_committed_lines_recompute_from_kernel_stats(tag, wl):
     for key, r in out.items():
         assert r["stats_launches"] > 0, key
         assert r["rel_diff"] <= tol, (key, r)
+
+
+def _full_stats(steps, tail=3_000_000, samples=40_000_000):
+    st = _step_stats(steps)
+    st.rays_tail = tail * steps
+    st.samples = samples * steps
+    return st
+
+
+@pytest.mark.parametrize("layout,cube", [(HBM, False), (LDS, True)], ids=["hbm", "lds-cube"])
+def test_step_roofline_components(bench, layout, cube):
+    """step_roofline: every kernel's modelled bytes per step over the step time; independent of the
+    number of timed steps; components as DESIGN.md §4 states them."""
+    rf = bench.roofline(CNT, [_step_stats(4)], layout, "no_such_workload", 4, cube_env=cube)
+    sh = bench.shadow_roofline(CNT, [_step_stats(4)], layout, "no_such_workload", 4)
+    a = bench.step_roofline(CNT, [_full_stats(4)], 4, 3.0, rf, sh, 2_000_000, 16, cube_env=cube)
+    b = bench.step_roofline(CNT, [_full_stats(1)], 1, 3.0, rf, sh, 2_000_000, 16, cube_env=cube)
+    assert a == b
+    parts = a["bytes_by_kernel"]
+    assert sum(parts.values()) == pytest.approx(a["bytes_per_step"], abs=len(parts))
+    assert parts["trace"] == pytest.approx(rf["bytes_per_launch"] * 6, rel=1e-6)
+    assert parts["shadow"] == pytest.approx(sh["bytes_per_launch"] * 6, rel=1e-6)
+    hits = 10_000_000 * 0.4 + 28_000_000 * 0.25
+    assert parts["shade"] == pytest.approx(hits * (140.0 + 32.0), rel=1e-6)
+    culled = 40_000_000 - 10_000_000
+    assert parts["sky"] == pytest.approx(culled * (64.0 if cube else 0.0) + culled / 16 * 32.0, rel=1e-6)
+    assert parts["accum"] == pytest.approx(2_000_000 * 39.0 + 10_000_000 * 16.0, rel=1e-6)
+    if layout is HBM:
+        assert parts["tail"] == pytest.approx(3_000_000 * rf["scene_hbm_bytes_per_bounce_ray"], rel=1e-6)
+        assert rf["scene_hbm_bytes_per_bounce_ray"] > 0
+    else:
+        assert parts["tail"] == 0
+    assert a["frac"] == pytest.approx(a["bytes_per_step"] / 3e-3 / 1e9 / 8000.0, rel=1e-3)

@@ -376,7 +376,6 @@ def test_wave_fold_bounce0_invariance(renderer, scene, p0, p1, spp):
     W, H = 96, 64
     cam = sptr.camera_lookat(aspect=W / H)
     sptr.setup_default(renderer, scene, p0, p1)
-    renderer.set_lanes(1)  # one batch at a time (the sample-batch lanes are tested in test_c3_batches_bit_exact)
     try:
         st = renderer.render(cam, W, H, spp=spp)
         assert st.waves == 1
@@ -386,7 +385,6 @@ def test_wave_fold_bounce0_invariance(renderer, scene, p0, p1, spp):
         st8 = renderer.render(cam, W, H, spp=spp)
     finally:
         renderer.set_wave_paths(0)
-        renderer.set_lanes(0)
     assert st8.waves == (spp + 7) // 8
     assert np.array_equal(acc.view(np.uint32), renderer.read_accum().view(np.uint32))
     assert np.array_equal(rgb, renderer.read_rgb8())
@@ -500,24 +498,75 @@ def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
             assert a[1:] == ref[1:], mode
 
 
-def test_many_direct_calls(renderer):
-    """Hundreds of direct-launch calls of an L2-scene frame (each forks k_sky and the shadow launches to
-    the context's second streams and joins them back): the runtime must not accumulate state across
-    calls (a HIP stack overflow was once seen deep into a run of cross-stream calls), and every call
-    must give the same image."""
+@pytest.mark.parametrize("mode", [1, 0])
+def test_many_calls_without_collect(renderer, mode):
+    """1500 asynchronous calls of an L2-scene frame with no collection in between, each forking k_sky
+    and the shadow launches to the side streams and joining them back: direct launches (mode 1), and
+    one captured graph replayed (mode 0).  No state may accumulate in the runtime (r03 saw a host stack
+    overflow inside libamdhip64 in this suite — the recursion of hipStreamEndCapture over a cyclic
+    capture-stream list, DESIGN.md §6 "Launch graphs"), and every call must give the same image."""
     W, H = 96, 64
     sptr.setup_default(renderer, "sphere_mesh", 60, 120)
     cam = sptr.camera_lookat(aspect=W / H)
     try:
-        renderer.set_launch_mode(1)
+        renderer.set_launch_mode(mode)
         renderer.render(cam, W, H, spp=4, frame_begin=1)
         ref = renderer.read_accum().copy()
-        for _ in range(400):
+        for _ in range(1500):
             renderer.render(cam, W, H, spp=4, frame_begin=1, flags=sptr.SPTR_FRAME_ASYNC)
         renderer.collect_stats()
         assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32))
+        if mode == 0:
+            assert renderer.graph_info()["valid"] == 1
     finally:
         renderer.set_launch_mode(0)
+
+
+@pytest.mark.parametrize("scene,p0,p1,spp", [("sphere_mesh", 60, 120, 24), ("default_emitter", 0, 0, 24)])
+def test_multibatch_overlapped_graph_replay(renderer, scene, p0, p1, spp):
+    """A call of several sample batches (set_wave_paths: 8 samples per batch -> 3 batches) with the
+    overlapped side-stream launches (k_sky beside each bounce-0 trace, k_shadow_dyn(d) beside the next
+    bounce's trace, on the L2/HBM scene) captured into one graph (launch mode 0, call 2) and replayed
+    (calls 3-4): the graph passes the DAG check, and every call is bit-identical to the serial one-stream
+    direct launches (mode 2)."""
+    W, H = 96, 64
+    sptr.setup_default(renderer, scene, p0, p1)
+    cam = sptr.camera_lookat(aspect=W / H)
+    P = 3 * 2 * 1024  # local pixels: 3 x 2 tiles
+    out = {}
+    try:
+        renderer.set_wave_paths(P * 8)
+        for mode in (2, 0):
+            renderer.set_launch_mode(mode)
+            runs = []
+            for _ in range(4):
+                st = renderer.render(cam, W, H, spp=spp, frame_begin=1)
+                assert st.waves == spp // 8
+                runs.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow))
+            out[mode] = runs
+            if mode == 0:
+                g = renderer.graph_info()
+                assert g["valid"] == 1
+                # a DAG whose longest path runs through every batch's sequence
+                assert 3 * spp // 8 < g["depth"] <= g["nodes"] <= 4096, g
+                assert g["edges"] >= g["nodes"] - 1, g
+    finally:
+        renderer.set_wave_paths(0)
+        renderer.set_launch_mode(0)
+    ref = out[2][0]
+    for mode in (2, 0):
+        for a in out[mode]:
+            assert np.array_equal(a[0].view(np.uint32), ref[0].view(np.uint32)), mode
+            assert a[1:] == ref[1:], mode
+
+
+def test_overlap_probe(renderer):
+    """sptr_overlap_probe runs and reports plausible spin times (the bench line records them)."""
+    p = renderer.overlap_probe()
+    print("overlap_probe", p)
+    assert 0.3 < p["serial_ms"] < 5.0, p
+    assert 0.15 < p["side_ms"] <= p["serial_ms"] * 1.2, p
+    assert 0.15 < p["sky_side_ms"] <= p["serial_ms"] * 1.2, p
 
 
 @pytest.mark.parametrize("scene,p0,p1", [("default_emitter", 0, 0), ("sphere_mesh", 60, 120)])

@@ -3,8 +3,12 @@
 the timed-path instantiations (kCount = false) of the trace kernels (k_trace, k_trace_pm, k_trace_wp,
 k_trace_dyn) pooled over their launches, and of the shadow kernels (k_shadow, k_shadow_dyn).
 achieved = the line's bytes_per_launch / pooled average duration; frac = achieved / peak.
+With a third file (the kernel statistics of a one-stream run, launch mode 2) the line's roofline_serial
+fractions are recomputed the same way.  step_roofline: bytes_per_step = the sum of its per-kernel bytes,
+frac = bytes_per_step / ms_per_step / peak.
 
     usage: tools/recompute_roofline.py profiles/<tag>_bench_<wl>.json profiles/<tag>_kernel_stats_<wl>.csv
+                                       [profiles/<tag>_kernel_stats_<wl>_serial.csv]
 """
 import csv
 import json
@@ -31,21 +35,36 @@ def pooled(rows, family):
     return (total / calls * 1e-3, calls) if calls else (None, 0)
 
 
-def recompute(bench_path, stats_path):
+def _one(r, rows, family, peak):
+    avg_us, calls = pooled(rows, family)
+    achieved = r["bytes_per_launch"] / (avg_us * 1e-6) / 1e9
+    return {"line_frac": r["frac"], "line_avg_launch_us": r["avg_launch_us"], "stats_avg_launch_us": round(avg_us, 2),
+            "stats_launches": calls, "frac": round(achieved / peak, 4),
+            "rel_diff": round(abs(achieved / peak - r["frac"]) / r["frac"], 4)}
+
+
+def recompute(bench_path, stats_path, serial_stats_path=None):
     line = json.loads(open(bench_path).read().splitlines()[-1])
     rows = list(csv.DictReader(open(stats_path)))
     out = {}
     for key, family in (("roofline", "k_trace"), ("shadow_roofline", "k_shadow")):
         r = line.get(key)
-        if not r:
-            continue
-        avg_us, calls = pooled(rows, family)
-        achieved = r["bytes_per_launch"] / (avg_us * 1e-6) / 1e9
-        out[key] = {"line_frac": r["frac"], "line_avg_launch_us": r["avg_launch_us"], "stats_avg_launch_us": round(avg_us, 2),
-                    "stats_launches": calls, "frac": round(achieved / r["peak"], 4),
-                    "rel_diff": round(abs(achieved / r["peak"] - r["frac"]) / r["frac"], 4)}
+        if r:
+            out[key] = _one(r, rows, family, r["peak"])
+    ser = line.get("roofline_serial")
+    if ser and serial_stats_path:
+        srows = list(csv.DictReader(open(serial_stats_path)))
+        for key, family in (("trace", "k_trace"), ("shadow", "k_shadow")):
+            if ser.get(key):
+                out["roofline_serial." + key] = _one(ser[key], srows, family, line["roofline"]["peak"])
+    st = line.get("step_roofline")
+    if st:
+        total = sum(st["bytes_by_kernel"].values())
+        frac = total / (st["ms_per_step"] * 1e-3) / 1e9 / st["peak"]
+        out["step_roofline"] = {"line_frac": st["frac"], "frac": round(frac, 4), "bytes_per_step": total,
+                                "rel_diff": round(abs(frac - st["frac"]) / max(1e-12, st["frac"]), 4)}
     return out
 
 
 if __name__ == "__main__":
-    print(json.dumps(recompute(sys.argv[1], sys.argv[2]), indent=1))
+    print(json.dumps(recompute(*sys.argv[1:4]), indent=1))
