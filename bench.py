@@ -650,7 +650,8 @@ def main():
             "render_ms_per_rank": [round(x, 4) for x in per_rank_render],
             "scene": {"prims": info["prims"], "lbvh_nodes": info["nodes"], "bvh_depth": info["depth"],
                       "lbvh_build_ms": round(info["build_ms"], 3), "leaf_size": layout["leaf_size"],
-                      "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"]},
+                      "bvh_width": layout["bvh_width"], "traversed_nodes": layout["num_nodes"],
+                      "prim_refs": layout["num_prim_refs"]},
             "cpu_baseline": None,
         }
         if args.integrator == "wavefront":

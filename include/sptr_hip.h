@@ -215,6 +215,12 @@ int sptr_set_tail_depth(sptr_ctx* ctx, uint32_t depth);
 /* Maximum primitives per BVH leaf range (1..16; 0 = automatic, the default: 8 for scenes staged in
  * LDS, 1 otherwise); applies to the next sptr_upload_scene. */
 int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
+/* Split references (early split clipping) for scenes traversed from L2/HBM: a triangle whose box is
+ * much larger than the triangle (a sliver lying across the axes) is referenced up to max_pieces times,
+ * each reference bounding one piece of it, so that rays near a fan of slivers stop testing every
+ * sliver's box.  0 = default (16), 1 = no splits, else a power of two up to 32; applies to the next
+ * sptr_upload_scene.  Results do not depend on it (each reference tests the same triangle). */
+int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
  * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument;
@@ -246,7 +252,9 @@ int sptr_scene_info(const sptr_ctx* ctx, uint32_t* num_prims, uint32_t* num_node
 typedef struct sptr_scene_layout {
   uint32_t num_tris, num_spheres, num_nodes, leaf_size, bvh_depth, lds_bytes;
   uint64_t node_bytes, tri_bytes, sphere_bytes, prim_ref_bytes;
-  uint32_t bvh_width, pad; /* num_nodes / node_bytes describe the traversed (BVH2 or BVH4) nodes */
+  uint32_t bvh_width; /* num_nodes / node_bytes describe the traversed (BVH2 or BVH4) nodes */
+  uint32_t num_prim_refs; /* primitive references the BVH is built over: num_tris + num_spheres, plus the
+                             extra references of split triangles (sptr_set_split_refs) */
 } sptr_scene_layout;
 int sptr_scene_layout_info(const sptr_ctx* ctx, sptr_scene_layout* out);
 

@@ -2,11 +2,17 @@
 // (src/backends/EmbreeBackend.cpp:82-181, src/backends/OptixBackend.cpp:916-1308).
 //
 // One flat BVH2 over every world-space triangle and analytic sphere (typed leaf links):
-//   k_prim_bounds : per-primitive AABB + centroid bounds (ordered-int atomics)
-//   k_morton      : 63-bit Morton code (21 bits/axis) of the centroid, value = primitive id
+//   k_prim_bounds : per-primitive AABB
+//   k_split_count + scan + k_split_emit (L2/HBM scenes): split references — a triangle whose box is far
+//                   larger than the triangle (a sliver lying across the axes) gets 2^D references, each
+//                   with the tight box of one piece of the triangle clipped by D recursive midpoint splits
+//                   (early split clipping); every other primitive keeps one reference with its own box
+//   k_ref_bounds  : centroid bounds of the references (ordered-int atomics)
+//   k_morton      : 63-bit Morton code (21 bits/axis) of a reference's box centroid, value = reference id
 //   radix sort    : rocPRIM radix_sort_pairs on the codes
 //   k_leaves      : scatter triangles (v0, e1, e2, Ng precomputed as Embree's TriangleM does) and
-//                   spheres into sorted slots; typed leaf links
+//                   spheres into sorted slots, one slot per reference (a split triangle's references
+//                   each hold a copy); typed leaf links
 //   k_karras      : Karras 2012 binary radix tree over the sorted codes (ties broken by index)
 //   k_refit       : bottom-up box propagation; the second child to arrive at a node finishes it
 //                   (write-through 8-byte box pairs, drained before one agent-scope exchange that
@@ -105,14 +111,147 @@ __device__ __forceinline__ void prim_box(const BuildIn& in, uint32_t i, vec3& lo
   }
 }
 
-__global__ void k_prim_bounds(BuildIn in, float4* blo, float4* bhi, uint32_t* cb) {
+__global__ void k_prim_bounds(BuildIn in, float4* blo, float4* bhi) {
   const uint32_t N = in.ntri + in.nsph;
-  uint32_t mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u};
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
     vec3 lo, hi;
     prim_box(in, i, lo, hi);
     blo[i] = make_float4(lo.x, lo.y, lo.z, 0.0f);
     bhi[i] = make_float4(hi.x, hi.y, hi.z, 0.0f);
+  }
+}
+
+// ------------------------------------------------------------------------------ split references
+// Early split clipping (Ernst & Greiner, "Early Split Clipping for Bounding Volume Hierarchies",
+// RT 2007).  A triangle lying diagonally across the axes has a box far larger than itself: the
+// 1250 x 4000 sphere mesh's rows near the poles (SceneDesc.h:225-279) are slivers ~640 / k times as
+// long as they are wide in row k, all fanning out of the pole, so near the pole the boxes of hundreds of
+// them overlap any point and a ray crossing there visits hundreds of nodes (r03: 256-1023 visits per ray,
+// the rays that set the length of every C5 trace launch).  Such a triangle is referenced 2^D times
+// instead, each reference bounding one piece: the triangle clipped by D recursive splits of its
+// current piece's box at the midpoint of the longest axis.  Pieces are convex polygons (<= 3 + D
+// vertices) clipped in double precision — exact for the float vertices, and each piece box is rounded
+// outwards to float — so the union of a triangle's reference boxes contains the triangle.  Closest-hit
+// and any-hit results are those of the triangle itself (each reference tests the same triangle).
+// D: the smallest depth with box area / (ratio threshold x triangle area) <= 2^D, at most log2 of the
+// context's piece limit (sptr_set_split_refs).
+constexpr float kSplitRatio = 8.0f;  // box half-area / triangle area above which a triangle is split
+constexpr int kMaxSplitDepth = 5;
+
+__device__ __forceinline__ uint32_t split_pieces(const BuildIn& in, uint32_t i, float4 lo, float4 hi, uint32_t max_pieces) {
+  if (i >= in.ntri || max_pieces <= 1u) return 1u;
+  const uint32_t a = in.idx[3 * i], b = in.idx[3 * i + 1], c = in.idx[3 * i + 2];
+  const vec3 p0 = v3(in.pos[3 * a], in.pos[3 * a + 1], in.pos[3 * a + 2]);
+  const vec3 p1 = v3(in.pos[3 * b], in.pos[3 * b + 1], in.pos[3 * b + 2]);
+  const vec3 p2 = v3(in.pos[3 * c], in.pos[3 * c + 1], in.pos[3 * c + 2]);
+  const vec3 n = cross(p1 - p0, p2 - p0);
+  const float area2 = sqrtf(dot(n, n));  // twice the triangle's area
+  const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+  const float box = dx * dy + dy * dz + dz * dx;  // half the box's surface area
+  if (!(area2 > 0.0f) || box <= kSplitRatio * 0.5f * area2) return 1u;
+  uint32_t p = 1u;
+  while (p < max_pieces && box > kSplitRatio * 0.5f * area2 * (float)p) p <<= 1;
+  return p;
+}
+
+__global__ void k_split_count(BuildIn in, const float4* blo, const float4* bhi, uint32_t max_pieces, uint32_t* cnt) {
+  const uint32_t N = in.ntri + in.nsph;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    cnt[i] = split_pieces(in, i, blo[i], bhi[i], max_pieces);
+}
+
+struct Poly {
+  double v[3 + kMaxSplitDepth][3];
+  int n;
+};
+// Sutherland-Hodgman against the half-space x_a <= m (keep_le) or x_a >= m
+__device__ void clip_poly(Poly& p, int a, double m, bool keep_le) {
+  Poly o;
+  o.n = 0;
+  for (int i = 0; i < p.n; ++i) {
+    const double* A = p.v[i];
+    const double* B = p.v[(i + 1) % p.n];
+    const bool ina = keep_le ? A[a] <= m : A[a] >= m;
+    const bool inb = keep_le ? B[a] <= m : B[a] >= m;
+    if (ina && o.n < 3 + kMaxSplitDepth) {
+      for (int k = 0; k < 3; ++k) o.v[o.n][k] = A[k];
+      ++o.n;
+    }
+    if (ina != inb && o.n < 3 + kMaxSplitDepth) {
+      const double t = (m - A[a]) / (B[a] - A[a]);
+      for (int k = 0; k < 3; ++k) o.v[o.n][k] = k == a ? m : A[k] + t * (B[k] - A[k]);
+      ++o.n;
+    }
+  }
+  p = o;
+}
+__device__ __forceinline__ void poly_box(const Poly& p, double lo[3], double hi[3]) {
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = hi[k] = p.v[0][k];
+    for (int i = 1; i < p.n; ++i) {
+      lo[k] = fmin(lo[k], p.v[i][k]);
+      hi[k] = fmax(hi[k], p.v[i][k]);
+    }
+  }
+}
+__device__ __forceinline__ float down_f(double x) {
+  const float f = (float)x;
+  return (double)f > x ? nextafterf(f, -INFINITY) : f;
+}
+__device__ __forceinline__ float up_f(double x) {
+  const float f = (float)x;
+  return (double)f < x ? nextafterf(f, INFINITY) : f;
+}
+
+// references of primitive i at roff[i] ..: rprim = i, the piece boxes (or the primitive's own box)
+__global__ void k_split_emit(BuildIn in, const float4* blo, const float4* bhi, const uint32_t* cnt, const uint32_t* roff,
+                             float4* rlo, float4* rhi, uint32_t* rprim) {
+  const uint32_t N = in.ntri + in.nsph;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    const uint32_t n = cnt[i], r0 = roff[i];
+    const float4 tlo = blo[i], thi = bhi[i];
+    if (n == 1u) {
+      rlo[r0] = tlo;
+      rhi[r0] = thi;
+      rprim[r0] = i;
+      continue;
+    }
+    const uint32_t ia = in.idx[3 * i], ib = in.idx[3 * i + 1], ic = in.idx[3 * i + 2];
+    const uint32_t vid[3] = {ia, ib, ic};
+    const int D = __ffs((int)n) - 1;  // n = 2^D
+    for (uint32_t k = 0; k < n; ++k) {
+      Poly p;
+      p.n = 3;
+      for (int j = 0; j < 3; ++j)
+        for (int a = 0; a < 3; ++a) p.v[j][a] = (double)in.pos[3 * vid[j] + a];
+      for (int lev = 0; lev < D && p.n > 0; ++lev) {
+        double lo[3], hi[3];
+        poly_box(p, lo, hi);
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+          if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        if (!(hi[ax] > lo[ax])) break;  // a point: nothing left to split
+        const double m = 0.5 * (lo[ax] + hi[ax]);
+        clip_poly(p, ax, m, ((k >> (D - 1 - lev)) & 1u) == 0u);
+      }
+      float4 o_lo = tlo, o_hi = thi;
+      if (p.n > 0) {
+        double lo[3], hi[3];
+        poly_box(p, lo, hi);
+        o_lo = make_float4(fmaxf(down_f(lo[0]), tlo.x), fmaxf(down_f(lo[1]), tlo.y), fmaxf(down_f(lo[2]), tlo.z), 0.0f);
+        o_hi = make_float4(fminf(up_f(hi[0]), thi.x), fminf(up_f(hi[1]), thi.y), fminf(up_f(hi[2]), thi.z), 0.0f);
+      }
+      rlo[r0 + k] = o_lo;
+      rhi[r0 + k] = o_hi;
+      rprim[r0 + k] = i;
+    }
+  }
+}
+
+__global__ void k_ref_bounds(uint32_t NR, const float4* blo, const float4* bhi, uint32_t* cb) {
+  uint32_t mn[3] = {~0u, ~0u, ~0u}, mx[3] = {0u, 0u, 0u};
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < NR; i += gridDim.x * blockDim.x) {
+    const float4 lo = blo[i], hi = bhi[i];
     const float c[3] = {0.5f * (lo.x + hi.x), 0.5f * (lo.y + hi.y), 0.5f * (lo.z + hi.z)};
     for (int k = 0; k < 3; ++k) {
       const uint32_t o = f2ord(c[k]);
@@ -150,8 +289,8 @@ __device__ __forceinline__ vec3 tri_ng(const BuildIn& in, uint32_t prim) {
 // Trumbore test rejects den = dot(Ng, d) = 0 for every ray (tri_hit4: den != 0), so such a triangle
 // can never be a closest hit or an occluder — excluding it changes no result, and removes boxes that
 // all contain the pole from the fan every polar ray crosses.
-__global__ void k_morton(BuildIn in, uint32_t N, const float4* blo, const float4* bhi, const uint32_t* cb, uint64_t* keys,
-                         uint32_t* vals, uint32_t* ndeg) {
+__global__ void k_morton(BuildIn in, uint32_t N, const float4* blo, const float4* bhi, const uint32_t* rprim, const uint32_t* cb,
+                         uint64_t* keys, uint32_t* vals, uint32_t* ndeg) {
   float lo[3], ext[3];
   for (int k = 0; k < 3; ++k) {
     lo[k] = ord2f(cb[k]);
@@ -167,8 +306,9 @@ __global__ void k_morton(BuildIn in, uint32_t N, const float4* blo, const float4
       code |= expand21((uint32_t)q) << (2 - k);
     }
     bool deg = false;
-    if (i < in.ntri) {
-      const vec3 ng = tri_ng(in, i);
+    const uint32_t prim = rprim[i];
+    if (prim < in.ntri) {
+      const vec3 ng = tri_ng(in, prim);
       deg = ng.x == 0.0f && ng.y == 0.0f && ng.z == 0.0f;
     }
     const uint32_t nd = (uint32_t)__popcll(__ballot(deg));
@@ -178,16 +318,17 @@ __global__ void k_morton(BuildIn in, uint32_t N, const float4* blo, const float4
   }
 }
 
-__global__ void k_is_tri(uint32_t N, uint32_t ntri, const uint32_t* vals, uint32_t* flag) {
+__global__ void k_is_tri(uint32_t N, uint32_t ntri, const uint32_t* vals, const uint32_t* rprim, uint32_t* flag) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
-    flag[i] = vals[i] < ntri ? 1u : 0u;
+    flag[i] = rprim[vals[i]] < ntri ? 1u : 0u;
 }
 
-__global__ void k_leaves(BuildIn in, const uint32_t* vals, const uint32_t* tri_slot, float4* tris, uint32_t* tri_geom,
-                         uint32_t* tri_orig, float4* sph, uint32_t* sph_geom, uint32_t* sph_orig, uint32_t* prim_ref) {
-  const uint32_t N = in.ntri + in.nsph;
+// sorted reference i -> its slot (triangle slots in reference order, then sphere slots)
+__global__ void k_leaves(BuildIn in, uint32_t N, const uint32_t* vals, const uint32_t* rprim, const uint32_t* tri_slot,
+                         float4* tris, uint32_t* tri_geom, uint32_t* tri_orig, float4* sph, uint32_t* sph_geom,
+                         uint32_t* sph_orig, uint32_t* prim_ref) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
-    const uint32_t prim = vals[i];
+    const uint32_t prim = rprim[vals[i]];
     if (prim < in.ntri) {
       const uint32_t slot = tri_slot[i];
       const uint32_t a = in.idx[3 * prim], b = in.idx[3 * prim + 1], c = in.idx[3 * prim + 2];
@@ -1069,18 +1210,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   const uint32_t NP = ntris + nsph;
   c.num_tris = ntris;
   c.num_sph = nsph;
-  c.num_nodes = NP > 1 ? NP - 1 : 0;
   c.bvh_depth = 0;
-  // + 64 B: the unified wide walk (wide_walk_u) reads a node's 56 B from a direct leaf's primitive address
-  LB_CHECK(realloc_buf(c.tris, (size_t)ntris * 48 + 64));
-  LB_CHECK(realloc_buf(c.tri_geom, (size_t)ntris * 4));
-  LB_CHECK(realloc_buf(c.tri_orig, (size_t)ntris * 4));
-  LB_CHECK(realloc_buf(c.sph, (size_t)nsph * 16 + 64));
-  LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
-  LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
-  LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));
-  LB_CHECK(realloc_buf(c.prim_ref, ((size_t)NP + 3) / 4 * 16));
   if (NP == 0) {
+    c.num_nodes = 0;
+    c.num_tri_refs = 0;
     c.root = kNoHit;
     c.root4 = kNoHit;
     c.num_nodes4 = 0;
@@ -1104,55 +1237,96 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   if (nsph) LB_CHECK(hipMemcpyAsync(d_sph, h_sph, (size_t)nsph * 16, hipMemcpyHostToDevice, s));
   BuildIn in{d_pos, d_idx, d_sph, d_tg, ntris, nsph, sph_geom_base};
 
+  // primitive boxes, then the references: one per primitive, or 2^D pieces of a split triangle.
+  // Scenes small enough to be staged in LDS (C1, C2, C4) are never split (the estimate of their
+  // staged bytes is the automatic leaf-size rule's, below).
+  float4 *pblo = nullptr, *pbhi = nullptr;
+  uint32_t *rcnt = nullptr, *roff = nullptr;
+  LB_CHECK(tmp.alloc(&pblo, NP));
+  LB_CHECK(tmp.alloc(&pbhi, NP));
+  LB_CHECK(tmp.alloc(&rcnt, NP));
+  LB_CHECK(tmp.alloc(&roff, NP));
+  hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi);
+  const bool small = ((uint64_t)(NP - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)NP + 3) / 4 * 16) <=
+                     kLdsSceneBytes;
+  const uint32_t max_pieces = (small || SPTR_EXPERIMENT_HOST_SAH || (c.leaf_size != 0 && c.leaf_size != 1))
+                                  ? 1u : std::min<uint32_t>(c.split_pieces, 1u << kMaxSplitDepth);
+  hipLaunchKernelGGL(k_split_count, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi, max_pieces, rcnt);
+  size_t rbytes = 0;
+  LB_CHECK(rocprim::exclusive_scan(nullptr, rbytes, rcnt, roff, 0u, NP, rocprim::plus<uint32_t>(), s));
+  void* rstore = nullptr;
+  LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&rstore), rbytes));
+  LB_CHECK(rocprim::exclusive_scan(rstore, rbytes, rcnt, roff, 0u, NP, rocprim::plus<uint32_t>(), s));
+  uint32_t last2[2] = {0u, 0u};
+  LB_CHECK(hipMemcpyAsync(&last2[0], rcnt + (NP - 1), 4, hipMemcpyDeviceToHost, s));
+  LB_CHECK(hipMemcpyAsync(&last2[1], roff + (NP - 1), 4, hipMemcpyDeviceToHost, s));
+  LB_CHECK(hipStreamSynchronize(s));
+  const uint64_t NR64 = (uint64_t)last2[0] + last2[1];
+  if (NR64 >= (1ull << (31 - kLeafCountBits)))
+    return (c.err = "lbvh: too many primitive references (" + std::to_string(NR64) + ")", SPTR_ERR_INVALID);
+  const uint32_t NR = (uint32_t)NR64;
+  const uint32_t ntri_refs = NR - nsph;  // spheres keep one reference each
+  c.num_tri_refs = ntri_refs;
+  c.num_nodes = NR > 1 ? NR - 1 : 0;
+  // + 64 B: the unified wide walk (wide_walk_u) reads a node's 56 B from a direct leaf's primitive address
+  LB_CHECK(realloc_buf(c.tris, (size_t)ntri_refs * 48 + 64));
+  LB_CHECK(realloc_buf(c.tri_geom, (size_t)ntri_refs * 4));
+  LB_CHECK(realloc_buf(c.tri_orig, (size_t)ntri_refs * 4));
+  LB_CHECK(realloc_buf(c.sph, (size_t)nsph * 16 + 64));
+  LB_CHECK(realloc_buf(c.sph_geom, (size_t)nsph * 4));
+  LB_CHECK(realloc_buf(c.sph_orig, (size_t)nsph * 4));
+  LB_CHECK(realloc_buf(c.nodes, (size_t)c.num_nodes * sizeof(BvhNode)));
+  LB_CHECK(realloc_buf(c.prim_ref, ((size_t)NR + 3) / 4 * 16));
+
   float4 *blo = nullptr, *bhi = nullptr;
   uint32_t* cb = nullptr;
   uint64_t *keys = nullptr, *keys_s = nullptr;
-  uint32_t *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
+  uint32_t *rprim = nullptr, *vals = nullptr, *vals_s = nullptr, *flag = nullptr, *slot = nullptr, *leaf_parent = nullptr,
            *rflags = nullptr, *dmax = nullptr;
   uint2* kids = nullptr;
-  LB_CHECK(tmp.alloc(&blo, NP));
-  LB_CHECK(tmp.alloc(&bhi, NP));
+  LB_CHECK(tmp.alloc(&blo, NR));
+  LB_CHECK(tmp.alloc(&bhi, NR));
+  LB_CHECK(tmp.alloc(&rprim, NR));
   LB_CHECK(tmp.alloc(&cb, 8));
-  LB_CHECK(tmp.alloc(&keys, NP));
-  LB_CHECK(tmp.alloc(&keys_s, NP));
-  LB_CHECK(tmp.alloc(&vals, NP));
-  LB_CHECK(tmp.alloc(&vals_s, NP));
-  LB_CHECK(tmp.alloc(&flag, NP));
-  LB_CHECK(tmp.alloc(&slot, NP));
-  LB_CHECK(tmp.alloc(&kids, NP));
-  LB_CHECK(tmp.alloc(&leaf_parent, NP));
-  LB_CHECK(tmp.alloc(&rflags, NP));
+  LB_CHECK(tmp.alloc(&keys, NR));
+  LB_CHECK(tmp.alloc(&keys_s, NR));
+  LB_CHECK(tmp.alloc(&vals, NR));
+  LB_CHECK(tmp.alloc(&vals_s, NR));
+  LB_CHECK(tmp.alloc(&flag, NR));
+  LB_CHECK(tmp.alloc(&slot, NR));
+  LB_CHECK(tmp.alloc(&kids, NR));
+  LB_CHECK(tmp.alloc(&leaf_parent, NR));
+  LB_CHECK(tmp.alloc(&rflags, NR));
   LB_CHECK(tmp.alloc(&dmax, 1));
+  hipLaunchKernelGGL(k_split_emit, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi, rcnt, roff, blo, bhi, rprim);
   const uint32_t cb_init[8] = {~0u, ~0u, ~0u, 0u, 0u, 0u, 0u, 0u};
   LB_CHECK(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
   LB_CHECK(hipMemsetAsync(dmax, 0, 4, s));
-  hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(NP)), dim3(256), 0, s, in, blo, bhi, cb);
-  hipLaunchKernelGGL(k_morton, dim3(blocks_for(NP)), dim3(256), 0, s, in, NP, blo, bhi, cb, keys, vals, dmax);
+  hipLaunchKernelGGL(k_ref_bounds, dim3(blocks_for(NR)), dim3(256), 0, s, NR, blo, bhi, cb);
+  hipLaunchKernelGGL(k_morton, dim3(blocks_for(NR)), dim3(256), 0, s, in, NR, blo, bhi, rprim, cb, keys, vals, dmax);
   LB_CHECK(hipGetLastError());
   size_t tbytes = 0;
-  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, NP, 0, 64, s));
+  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, NR, 0, 64, s));
   void* tstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
-  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, NP, 0, 64, s));
+  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, NR, 0, 64, s));
 #if SPTR_EXPERIMENT_HOST_SAH
   std::vector<uint32_t> sah_order;
   std::vector<BvhNode> sah_nodes;
   uint32_t sah_height = 0;
-  const bool use_sah = NP > 1 && c.leaf_size != 8 &&
-                       ((uint64_t)(NP - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)NP + 3) / 4 * 16) >
-                           kLdsSceneBytes;
-  if (use_sah) {
+  const bool use_sah = NP > 1 && c.leaf_size != 8 && !small;
+  if (use_sah) {  // (no split references in this experiment: references = primitives)
     host_sah(h_pos, h_idx, ntris, h_sph, nsph, sah_order, sah_nodes, sah_height);
     LB_CHECK(hipMemcpyAsync(vals_s, sah_order.data(), (size_t)NP * 4, hipMemcpyHostToDevice, s));
   }
 #endif
-  hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(NP)), dim3(256), 0, s, NP, ntris, vals_s, flag);
+  hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(NR)), dim3(256), 0, s, NR, ntris, vals_s, rprim, flag);
   size_t sbytes = 0;
-  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, NP, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, NR, rocprim::plus<uint32_t>(), s));
   void* sstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&sstore), sbytes));
-  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, NP, rocprim::plus<uint32_t>(), s));
-  hipLaunchKernelGGL(k_leaves, dim3(blocks_for(NP)), dim3(256), 0, s, in, vals_s, slot,
+  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, NR, rocprim::plus<uint32_t>(), s));
+  hipLaunchKernelGGL(k_leaves, dim3(blocks_for(NR)), dim3(256), 0, s, in, NR, vals_s, rprim, slot,
                      static_cast<float4*>(c.tris.p), static_cast<uint32_t*>(c.tri_geom.p),
                      static_cast<uint32_t*>(c.tri_orig.p), static_cast<float4*>(c.sph.p),
                      static_cast<uint32_t*>(c.sph_geom.p), static_cast<uint32_t*>(c.sph_orig.p),
@@ -1164,13 +1338,13 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   LB_CHECK(hipMemcpyAsync(&ndeg, dmax, 4, hipMemcpyDeviceToHost, s));
   LB_CHECK(hipStreamSynchronize(s));
   LB_CHECK(hipMemsetAsync(dmax, 0, 4, s));
-  const uint32_t N = ndeg < NP ? NP - ndeg : NP;
-  c.excluded_prims = NP - N;
+  const uint32_t N = ndeg < NR ? NR - ndeg : NR;
+  c.excluded_prims = NR - N;
   c.num_nodes = N > 1 ? N - 1 : 0;
   // automatic leaf size (measured, profiles/r01*, r02g_leaf.txt): ranges of 8 for scenes small enough
   // to be staged in LDS (fewer, divergence-free node steps), single primitives for meshes traversed
   // from L2/HBM (with the greedy wide collapse: C5 14.9 -> 13.9, C3 5.04 -> 4.87 ms/step vs 2)
-  const uint32_t auto_leaf = ((uint64_t)(N > 1 ? N - 1 : 0) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 +
+  const uint32_t auto_leaf = ((uint64_t)(N > 1 ? N - 1 : 0) * 64 + (uint64_t)ntri_refs * 48 + (uint64_t)nsph * 16 +
                               ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : (SPTR_WIDE_GREEDY ? 1u : 2u);
   const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size ? c.leaf_size : auto_leaf, kMaxLeafSize));
   c.leaf_used = leaf_max;

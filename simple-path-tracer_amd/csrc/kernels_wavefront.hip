@@ -3160,23 +3160,23 @@ SceneView scene_view(const Context& c) {
   s.tri_geom = static_cast<const uint32_t*>(c.tri_geom.p);
   s.sph_geom = static_cast<const uint32_t*>(c.sph_geom.p);
   s.num_nodes = c.num_nodes;
-  s.num_tris = c.num_tris;
+  s.num_tris = c.num_tri_refs;  // triangle slots (a split triangle has one per reference)
   s.num_sph = c.num_sph;
   s.root = c.root;
   s.num_nodes4 = c.num_nodes4;
   s.root4 = c.root4;
   // width 0 = automatic: BVH2 for LDS-staged scenes (3-20 nodes: the extra slab tests of a BVH4
   // node cost more than the saved steps), BVH4 for everything traversed from L2/HBM
-  const uint64_t bytes2 = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
-                          ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
+  const uint64_t bytes2 = (uint64_t)c.num_nodes * 64 + (uint64_t)c.num_tri_refs * 48 + (uint64_t)c.num_sph * 16 +
+                          ((uint64_t)c.num_tri_refs + c.num_sph + 3) / 4 * 16;
   s.width = c.bvh_width ? c.bvh_width : (bytes2 <= kLdsSceneBytes ? 2u : (uint32_t)kWide);
   // never a width whose worst-case traversal stack exceeds kStack (build_lbvh rejects trees that
   // even BVH2 cannot traverse)
   if (s.width == (uint32_t)kWide && c.stack_need4 > (uint32_t)kStack) s.width = 2u;
   s.prim_ref = static_cast<const uint32_t*>(c.prim_ref.p);
   const uint64_t node_bytes = s.width == (uint32_t)kWide ? (uint64_t)c.num_nodes4 * sizeof(WideNode) : (uint64_t)c.num_nodes * 64;
-  const uint64_t bytes = node_bytes + (uint64_t)c.num_tris * 48 + (uint64_t)c.num_sph * 16 +
-                         ((uint64_t)c.num_tris + c.num_sph + 3) / 4 * 16;
+  const uint64_t bytes = node_bytes + (uint64_t)c.num_tri_refs * 48 + (uint64_t)c.num_sph * 16 +
+                         ((uint64_t)c.num_tri_refs + c.num_sph + 3) / 4 * 16;
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
   s.scene_bytes = bytes;
   // the refilling wide-BVH kernels of L2/HBM scenes stage the top levels (4-wide nodes only)

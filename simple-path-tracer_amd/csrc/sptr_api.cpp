@@ -1067,6 +1067,16 @@ int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
   return SPTR_OK;
 }
 
+int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (max_pieces == 0u) max_pieces = 16u;
+  if (max_pieces > 32u || (max_pieces & (max_pieces - 1u)))
+    return fail(x->c, SPTR_ERR_INVALID, "split references: 0 (default 16) or a power of two up to 32");
+  x->c.split_pieces = max_pieces;
+  ++x->c.epoch;
+  return SPTR_OK;
+}
+
 int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
   if (!x) return SPTR_ERR_INVALID;
   if (max_paths > (1ull << 30)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^30");
@@ -1130,9 +1140,10 @@ int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
   out->bvh_width = sv.width;
   out->num_nodes = sv.width == (uint32_t)kWide ? c.num_nodes4 : c.num_nodes;
   out->node_bytes = sv.width == (uint32_t)kWide ? (uint64_t)c.num_nodes4 * sizeof(WideNode) : (uint64_t)c.num_nodes * sizeof(BvhNode);
-  out->tri_bytes = (uint64_t)c.num_tris * 48u;
+  out->tri_bytes = (uint64_t)c.num_tri_refs * 48u;
   out->sphere_bytes = (uint64_t)c.num_sph * 16u;
-  out->prim_ref_bytes = ((uint64_t)c.num_tris + c.num_sph) * 4u;
+  out->prim_ref_bytes = ((uint64_t)c.num_tri_refs + c.num_sph) * 4u;
+  out->num_prim_refs = c.num_tri_refs + c.num_sph;
   return SPTR_OK;
 }
 

@@ -351,6 +351,8 @@ struct Context {
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
   uint32_t treelet_passes = SPTR_TREELET_PASSES;  // SAH treelet passes over L2/HBM scenes' LBVH (kernels_lbvh.hip)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
+  uint32_t num_tri_refs = 0;     // triangle references = triangle slots (split references, kernels_lbvh.hip)
+  uint32_t split_pieces = 16;    // most references per split triangle (sptr_set_split_refs; 1 = no splits)
   uint32_t num_nodes4 = 0, root4 = 0;
   uint32_t excluded_prims = 0;  // exactly degenerate triangles left out of the BVH (never hit; k_morton)
   uint32_t num_top4 = 0;  // wide nodes numbered first: the top kTopLevels levels

@@ -98,7 +98,7 @@ class SceneLayout(C.Structure):
     _fields_ = [("num_tris", C.c_uint32), ("num_spheres", C.c_uint32), ("num_nodes", C.c_uint32),
                 ("leaf_size", C.c_uint32), ("bvh_depth", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("node_bytes", C.c_uint64), ("tri_bytes", C.c_uint64), ("sphere_bytes", C.c_uint64),
-                ("prim_ref_bytes", C.c_uint64), ("bvh_width", C.c_uint32), ("pad", C.c_uint32)]
+                ("prim_ref_bytes", C.c_uint64), ("bvh_width", C.c_uint32), ("num_prim_refs", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -142,6 +142,7 @@ def lib() -> C.CDLL:
         "sptr_overlap_probe": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
+        "sptr_set_split_refs": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
         "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
         "sptr_set_materials": (C.c_int, [vp, C.POINTER(Material), u32]),
@@ -423,6 +424,10 @@ class Renderer:
 
     def set_leaf_size(self, n: int):
         self._check(self._L.sptr_set_leaf_size(self._h, n), "set_leaf_size")
+
+    def set_split_refs(self, max_pieces: int):
+        """sptr_set_split_refs: most references per split triangle (0 = default 16, 1 = none); next upload."""
+        self._check(self._L.sptr_set_split_refs(self._h, max_pieces), "set_split_refs")
 
     def set_bvh_width(self, n: int):
         self._check(self._L.sptr_set_bvh_width(self._h, n), "set_bvh_width")

@@ -627,3 +627,41 @@ def test_traced_ray_counts(renderer):
     assert sum(sc.trace_visit_hist) == sc.traced_primary + sc.traced_bounce
     assert sum(sc.shadow_visit_hist) == sc.rays_shadow
     assert sum(sc.nodes_by_depth) == sc.node_visits
+
+
+def test_split_references_change_no_result(renderer):
+    """Split references (early split clipping of sliver triangles, sptr_set_split_refs): the sphere
+    mesh's polar rows are slivers, so with splits on the BVH holds more references than triangles.  First
+    hits (geomID, primID, t bits) on camera and random rays, occlusion, and a render with shadow rays
+    are the same with and without splits (a closest hit can differ only on an exact t tie between two
+    triangles, which the two trees may test in a different order)."""
+    W, H = 96, 64
+    cam = sptr.camera_lookat(aspect=W / H)
+    g = np.random.default_rng(5)
+    d = g.normal(size=(40000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((40000, 8), np.float32)
+    rays[:, 0:3] = g.uniform((-1.2, 0.2, -1.2), (1.2, 2.4, 1.2), size=(40000, 3))  # around the mesh's poles
+    rays[:, 3:6] = d
+    rays[:, 7] = np.inf
+    out = {}
+    try:
+        for pieces in (1, 16):
+            renderer.set_split_refs(pieces)
+            sptr.setup_default(renderer, "sphere_mesh", 60, 120)
+            lay = renderer.scene_layout()
+            st = renderer.render(cam, W, H, spp=8)
+            out[pieces] = (lay, renderer.intersect(rays), renderer.occluded(rays), renderer.read_rgb8().copy(), st)
+    finally:
+        renderer.set_split_refs(0)
+    (l1, h1, o1, rgb1, st1), (l16, h16, o16, rgb16, st16) = out[1], out[16]
+    assert l1["num_prim_refs"] == l1["num_tris"] + l1["num_spheres"]
+    assert l16["num_prim_refs"] > l16["num_tris"] + l16["num_spheres"]
+    same = (h1[0] == h16[0]) & (h1[1] == h16[1])
+    tie = (h1[2].view(np.uint32) == h16[2].view(np.uint32))
+    assert (same | tie).all()
+    assert same.mean() >= 0.9999
+    assert np.array_equal(h1[2][same].view(np.uint32), h16[2][same].view(np.uint32))
+    assert np.array_equal(o1, o16)
+    assert (rgb1 == rgb16).all(axis=2).mean() >= 0.9999
+    assert abs(int(st1.rays_closest) - int(st16.rays_closest)) <= 1e-4 * st1.rays_closest
