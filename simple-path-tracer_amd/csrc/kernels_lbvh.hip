@@ -587,7 +587,7 @@ __global__ void k_height_scatter(uint32_t nn, uint32_t per, const uint32_t* labe
 
 template <int K>
 __global__ void __launch_bounds__(kTreeletBlock) k_treelet(const uint32_t* order, uint32_t count, BvhNode* nodes,
-                                                            float* cost, uint32_t* newh) {
+                                                            float* cost, uint32_t* newh, uint32_t* leaf_parent) {
   constexpr int S = 1 << K;
   __shared__ float s_copt[S][kTreeletBlock];     // least SAH cost of a subset of the treelet's leaves
   __shared__ uint16_t s_part[S][kTreeletBlock];  // its best split (low byte) and height (high byte)
@@ -760,7 +760,9 @@ __global__ void __launch_bounds__(kTreeletBlock) k_treelet(const uint32_t* order
           }
         cnt += c;
         if ((ts & (ts - 1)) == 0) {
-          link[side] = lkj;  // a treelet leaf keeps its link (and its subtree)
+          link[side] = lkj;  // a treelet leaf keeps its link (and its subtree), under a new parent
+          if (!(lkj & kLeafBit)) nodes[lkj].link.z = id;
+          else leaf_parent[(lkj & ~kLeafBit) >> kLeafCountBits] = id;
         } else {
           uint32_t cid = 0u;
 #pragma unroll
@@ -1411,7 +1413,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
           for (uint32_t h = 1; h < kMaxHeight; ++h)
             if (hh[h])
               hipLaunchKernelGGL(k_treelet<SPTR_TREELET>, dim3((hh[h] + kTreeletBlock - 1) / kTreeletBlock),
-                                 dim3(kTreeletBlock), 0, s, order + off[h], hh[h], nodes, cst, nh);
+                                 dim3(kTreeletBlock), 0, s, order + off[h], hh[h], nodes, cst, nh, leaf_parent);
           LB_CHECK(hipGetLastError());
           LB_CHECK(hipMemcpyAsync(&dep, nh, 4, hipMemcpyDeviceToHost, s));  // the root's new height
           LB_CHECK(hipStreamSynchronize(s));
