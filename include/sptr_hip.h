@@ -228,9 +228,12 @@ int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
  * overlapped on the context's second stream).  Results are identical in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
 /* The launch graph the context holds (launch mode 0): valid = 1 once a call shape was captured; its
- * node count, dependency edges and the nodes on its longest path.  Every captured graph is checked to be
- * acyclic before it is instantiated (a rejected capture fails the call with SPTR_ERR_HIP). */
-int sptr_graph_info(const sptr_ctx* ctx, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth);
+ * node count, dependency edges and the nodes on its longest path; captures = graphs captured so far;
+ * capture_status = the hipError_t of the last capture attempt that fell back to direct launches (0:
+ * none).  Every captured graph is checked to be acyclic before it is instantiated (a rejected capture
+ * fails the call with SPTR_ERR_HIP).  Any pointer may be NULL. */
+int sptr_graph_info(const sptr_ctx* ctx, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth,
+                    uint32_t* captures, int32_t* capture_status);
 /* Whether the context's side streams run beside its render stream on this device: ms[0] = two 200-us
  * one-wave spins on the render stream, ms[1] = one there and one on the shadow side stream, ms[2] = one
  * there and one on the k_sky side stream (device events).  ms[1], ms[2] near ms[0] / 2: the side

@@ -275,14 +275,20 @@ __device__ __forceinline__ FrameView frame_dyn(FrameView f) {
   }
   return f;
 }
-// clear (may be null): a counter the call's launch sequence accumulates from zero (the unculled-pixel
-// count of an in-sequence k_cull), zeroed here instead of by a memset node of its own.
+// clear (may be null): the two counters an in-sequence k_cull accumulates from zero (its unculled and
+// culled pixel counts), zeroed here instead of by a memset node of their own.  dyn[kDynPmQueue]: the
+// work queue of the pixel-major bounce 0 (k_trace_pm), zeroed here and by every k_accum, so each batch's
+// k_trace_pm starts from zero.
 __global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear) {
   if (threadIdx.x == 0) {
     dyn[0] = frame_begin;
     dyn[1] = reset;
     dyn[2] = total;
-    if (clear) *clear = 0u;
+    dyn[kDynPmQueue] = 0u;
+    if (clear) {
+      clear[0] = 0u;
+      clear[1] = 0u;
+    }
   }
 }
 
@@ -1031,17 +1037,19 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   }
   return true;
 }
-// bit l of mask: pixel l is culled (see above).  plist: the valid pixels that are not culled (count at
-// plist[P], zeroed before).  One block per local tile: thread (qx, qy) tests the 2x2 pixel quad at
-// (2qx, 2qy) of the tile and sets the quad's bits in the tile's 32 LDS row words; then each thread
-// lists the unculled valid pixels of 4 consecutive local indices, the tile's list in pixel order at a
-// range one atomic per tile reserves.  (r02: a pyramid per pixel and one atomic per wave, C2 108 us;
-// per pixel and per tile 65-75 us.)
+// bit l of mask: pixel l is culled (see above).  plist: the valid pixels that are not culled, from
+// plist[0] (count at plist[P]), and every other local pixel — culled, or a tile slot outside the image —
+// from plist[P - 1] downwards (count at plist[P + 1]); both counts zeroed before.  So plist[0..P) is a
+// permutation of the local pixels, the expensive ones first (the order of the pixel-major bounce 0,
+// k_trace_pm).  One block per local tile: thread (qx, qy) tests the 2x2 pixel quad at (2qx, 2qy) of the
+// tile and sets the quad's bits in the tile's 32 LDS row words; then each thread lists the pixels of 4
+// consecutive local indices, the tile's runs at ranges one atomic per tile and list reserves.  (r02: a
+// pyramid per pixel and one atomic per wave, C2 108 us; per pixel and per tile 65-75 us.)
 __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
   static_assert(kTile == 32 && kBlock == 256, "16 x 16 quads per 32 x 32 tile");
   __shared__ uint32_t s_row[kTile];
-  __shared__ uint32_t s_cnt[kBlock / 64u];
-  __shared__ uint32_t s_base;
+  __shared__ uint32_t s_cnt[kBlock / 64u], s_ccnt[kBlock / 64u];
+  __shared__ uint32_t s_base, s_cbase;
   const uint32_t t0 = blockIdx.x * kTilePixels;  // the tile's first local pixel
   if (threadIdx.x < (uint32_t)kTile) s_row[threadIdx.x] = 0u;
   __syncthreads();
@@ -1079,29 +1087,43 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
   uint32_t w = mbits << col;
   for (int off = 1; off < 8; off <<= 1) w |= __shfl_xor(w, off);
   if ((threadIdx.x & 7u) == 0u) mask[(t0 >> 5) + row] = w;
-  // list the kept pixels: per-thread counts, wave scan, block offsets, one atomic per tile
-  const uint32_t n = (uint32_t)__popc(keep), lane = lane_id();
-  uint32_t incl = n;
+  // list the kept pixels (and the others from the top): per-thread counts, wave scans, block offsets,
+  // one atomic per tile and list
+  const uint32_t drop = ~keep & 0xFu;
+  const uint32_t n = (uint32_t)__popc(keep), nd = (uint32_t)__popc(drop), lane = lane_id();
+  uint32_t incl = n, incd = nd;
   for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t v = __shfl_up(incl, off);
-    if (lane >= (uint32_t)off) incl += v;
+    const uint32_t v = __shfl_up(incl, off), vd = __shfl_up(incd, off);
+    if (lane >= (uint32_t)off) {
+      incl += v;
+      incd += vd;
+    }
   }
-  if (lane == 63u) s_cnt[threadIdx.x >> 6] = incl;
+  if (lane == 63u) {
+    s_cnt[threadIdx.x >> 6] = incl;
+    s_ccnt[threadIdx.x >> 6] = incd;
+  }
   __syncthreads();
   if (threadIdx.x == 0u) {
-    uint32_t run = 0u;
+    uint32_t run = 0u, runc = 0u;
     for (uint32_t i = 0; i < kBlock / 64u; ++i) {
-      const uint32_t c = s_cnt[i];
+      const uint32_t c = s_cnt[i], cd = s_ccnt[i];
       s_cnt[i] = run;
+      s_ccnt[i] = runc;
       run += c;
+      runc += cd;
     }
     s_base = run ? atomicAdd(&plist[f.P], run) : 0u;
+    s_cbase = runc ? atomicAdd(&plist[f.P + 1u], runc) : 0u;
   }
   __syncthreads();
   uint32_t o = s_base + s_cnt[threadIdx.x >> 6] + incl - n;
+  uint32_t od = s_cbase + s_ccnt[threadIdx.x >> 6] + incd - nd;
 #pragma unroll
-  for (uint32_t j = 0; j < 4u; ++j)
+  for (uint32_t j = 0; j < 4u; ++j) {
     if ((keep >> j) & 1u) plist[o++] = t0 + 4u * threadIdx.x + j;
+    if ((drop >> j) & 1u) plist[f.P - 1u - od++] = t0 + 4u * threadIdx.x + j;
+  }
 }
 // Path-major bounce 0 over the unculled pixel list (f.plist: nlist pixels x k samples): compacted
 // item i -> path p.  Items run in groups of kPrimaryGroup listed pixels — neighbours, since k_cull lists
@@ -1253,15 +1275,26 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // radiance at all and k_accum skips it; from the first hit on, misses go to rad[p] and k_accum
 // resumes there (accum.w = resume slot).  A kernel of its own (not a branch of k_trace), so that
 // its registers are allocated for this loop alone.
+//
+// Work distribution (r04): a thread's unit of work is one pixel's whole sample loop (its misses fold in
+// sample order), so a statically dealt schedule — 256-pixel chunks round-robin, 4.5 per block on C2 —
+// left the kernel waiting for the blocks that drew a fifth chunk or the costly pixels, with the average
+// wave alive for ~55 % of the launch (r03 SQ_WAVE_CYCLES).  Now every wave takes 64 pixels at a time
+// from a global queue (FrameView::dyn[kDynPmQueue], zeroed by k_frame_dyn and k_accum), in the order of
+// k_cull's list: the unculled pixels (traversals) first, the culled ones (raygen + sky only) after them,
+// so the launch ends on the cheap chunks.  A block's hit records stay in its own segment, sized for twice
+// its static share: a wave takes pixels only while its block has room (s_taken), and since all
+// segments together hold twice the frame, some block always has room while pixels remain.  The pixel
+// order changes no result: each pixel's samples are summed in sample order by the thread that owns it.
 template <bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_PM_WAVES)
     k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_cnt, s_taken;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
-  if (threadIdx.x == 0) s_cnt = 0u;
+  if (threadIdx.x == 0) s_cnt = s_taken = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<true>(sv, lds);
   __syncthreads();
@@ -1273,10 +1306,23 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   const ImageDiv idiv = image_div(f);
   Visits vc;
   const Sched sd = block_sched(f.P);
-  const uint32_t per = sd.per * f.k;  // hit-record segment stride: all samples of the block's pixels
-  const uint32_t seg0 = sd.seg0 * f.k;
-  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
-    const uint32_t l = base + threadIdx.x;
+  const uint32_t cap = 2u * sd.per;  // pixels this block may take: its hit-record segment holds cap * k records
+  const uint32_t per = cap * f.k;    // hit-record segment stride
+  const uint32_t seg0 = logical_block() * per;
+  const uint32_t* order = f.pm_order;  // k_cull's list (null without a cull mask: local pixel order)
+  const uint32_t n_unc = order ? order[f.P] : f.P;
+  uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
+  const uint32_t lane = lane_id();
+  for (;;) {
+    uint32_t base = kNoHit;
+    if (lane == 0u) {
+      const uint32_t t = atomicAdd(&s_taken, 64u);
+      if (t + 64u <= cap) base = atomicAdd(queue, 64u);
+    }
+    base = __shfl(base, 0);
+    if (base >= f.P) break;  // the frame is taken (or this block's segment is full)
+    const uint32_t i = base + lane;
+    const uint32_t l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
@@ -2514,6 +2560,8 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
                                                   uint8_t* image) {
   const FrameView f = frame_dyn(fin);
   const uint32_t n_total = f.dyn ? f.dyn[2] : 0u;  // total frames of the accumulation (kResolve)
+  // the next batch's k_trace_pm takes its pixels from a fresh queue
+  if (f.dyn && blockIdx.x == 0 && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     uint32_t s0 = 0u;
     vec3 a = v3(0.0f, 0.0f, 0.0f);

@@ -118,12 +118,13 @@ uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
-// pixel slot it owns, so its segment slack is kMaxSegs * kBlock * k records (k_slack = k); every
-// other producer needs kMaxSegs * kBlock (k_slack = 1).
-int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack) {
+// pixel slot it may take, twice its static share (k_trace_pm's work queue), so the hit records span
+// 2 (cap + kMaxSegs * kBlock * k) (k_slack = k); every other producer needs cap + kMaxSegs * kBlock
+// (k_slack = 1).
+int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack, uint32_t hrec_mult) {
   WaveBufs& b = c.wb;
   L = L ? L : 1u;
-  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * kHitBytes;
+  const size_t hrec_bytes = ((size_t)cap + (size_t)kMaxSegs * kBlock * k_slack) * kHitBytes * hrec_mult;
   const bool grow = b.hrec.bytes < hrec_bytes || !(b.cap >= cap && b.L * b.ts >= L * ts && b.rad.p) || !b.seg.p;
   if (grow && sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // pending renders may still use the old streams
   if (grow) ++c.epoch;
@@ -231,6 +232,7 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.sky_fold = 0u;
   v.plist = nullptr;
   v.unculled = nullptr;
+  v.pm_order = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -394,7 +396,7 @@ int ensure_pixels(Context& c, int W, int H, int G, int R, hipStream_t s, bool& r
   API_HIP(ensure_buf(c.tiles, (size_t)c.P * 4));
   API_HIP(ensure_buf(c.image, (size_t)W * H * 3));
   API_HIP(ensure_buf(c.cull, (size_t)c.P / 32u * 4u + 4u));
-  API_HIP(ensure_buf(c.plist, ((size_t)c.P + 1u) * 4u));
+  API_HIP(ensure_buf(c.plist, ((size_t)c.P + 2u) * 4u));
   ++c.epoch;
   API_HIP(hipMemsetAsync(c.accum.p, 0, (size_t)c.P * 16, s));
   API_HIP(hipMemsetAsync(c.tiles.p, 0, (size_t)c.P * 4, s));
@@ -568,6 +570,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.pixel_major = bounce0_pixel_major(sv, fv);
     fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
     fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
+    fv.pm_order = (fv.cull != nullptr && fv.pixel_major == kFoldThread) ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
@@ -678,7 +681,7 @@ int refresh_cull(Context& c, const sptr_frame& f, hipStream_t s, bool timing) {
   fv.cull_depth = depth;
   StageTimer tm{c, timing, true, s};
   tm.begin(8);
-  API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 4, s));
+  API_HIP(hipMemsetAsync(static_cast<uint32_t*>(c.plist.p) + c.P, 0, 8, s));
   launch_cull(scene_view(c), fv, static_cast<uint32_t*>(c.cull.p), static_cast<uint32_t*>(c.plist.p), s);
   tm.end();
   API_HIP(hipGetLastError());
@@ -822,6 +825,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     }
     if (ec != hipSuccess || tm.err != hipSuccess || !g) {
       // not capturable (e.g. more stage spans than the pre-grown event pool): direct launches
+      c.capture_status = (int32_t)(ec != hipSuccess ? ec : (tm.err != hipSuccess ? tm.err : hipErrorUnknown));
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
       StageTimer td{c, timing, trace_only, s};
@@ -892,6 +896,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     }
     gc.valid = true;
     c.graph = gc;
+    ++c.captures;
   }
   // replay: the call's values into the k_frame_dyn node, fresh pool events into the event nodes
   GraphCache& gc = c.graph;
@@ -1285,8 +1290,12 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       // hit-record slack: k records per pixel slot only when some batch runs bounce 0 pixel-major
       FrameView probe = frame_view(c, *f);
       probe.k = k;
-      const uint32_t k_slack = bounce0_pixel_major(scene_view(c), probe) ? k : 1u;
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), k_slack);
+      bool pm = bounce0_pixel_major(scene_view(c), probe) != 0u;
+      if (f->spp % k) {  // the call's last, partial batch
+        probe.k = f->spp % k;
+        pm = pm || bounce0_pixel_major(scene_view(c), probe) != 0u;
+      }
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, pm ? 2u : 1u);
       if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));
@@ -1322,9 +1331,12 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   return collect_pending(c, stats);
 }
 
-int sptr_graph_info(const sptr_ctx* x, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth) {
+int sptr_graph_info(const sptr_ctx* x, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth,
+                    uint32_t* captures, int32_t* capture_status) {
   if (!x) return SPTR_ERR_INVALID;
   const GraphCache& g = x->c.graph;
+  if (captures) *captures = x->c.captures;
+  if (capture_status) *capture_status = x->c.capture_status;
   if (valid) *valid = g.valid ? 1u : 0u;
   if (nodes) *nodes = g.valid ? g.nodes : 0u;
   if (edges) *edges = g.valid ? g.edges : 0u;

@@ -169,7 +169,11 @@ struct FrameView {
   uint32_t cull_depth;   // BVH2 levels k_cull tests (<= kCullDepthMax)
   const uint32_t* plist; // with sky_fold: the unculled local pixels (count at plist[P]), bounce 0's paths
   const uint32_t* unculled;  // with cull: the number of unculled valid local pixels (k_cull's plist[P])
+  const uint32_t* pm_order;  // pixel-major bounce 0 with a cull mask: k_cull's list (unculled first), else null
 };
+// FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
+// the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
+constexpr uint32_t kDynPmQueue = 8;
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
 // rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each
@@ -338,6 +342,8 @@ struct Context {
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
   GraphCache graph;
+  int32_t capture_status = 0;        // hipError_t of the last capture that fell back to direct launches (0: none)
+  uint32_t captures = 0;             // graphs captured and instantiated
   GraphKey last_key{};               // the previous call's shape: a graph is captured when it repeats
   bool have_last_key = false;
   std::string err;

@@ -138,7 +138,7 @@ def lib() -> C.CDLL:
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_launch_mode": (C.c_int, [vp, u32]),
-        "sptr_graph_info": (C.c_int, [vp, up, up, up, up]),
+        "sptr_graph_info": (C.c_int, [vp, up, up, up, up, up, C.POINTER(C.c_int32)]),
         "sptr_overlap_probe": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
@@ -403,9 +403,9 @@ class Renderer:
 
     def graph_info(self) -> dict:
         """sptr_graph_info: the held launch graph (valid, nodes, edges, longest-path depth)."""
-        v = [C.c_uint32() for _ in range(4)]
+        v = [C.c_uint32() for _ in range(5)] + [C.c_int32()]
         self._check(self._L.sptr_graph_info(self._h, *[C.byref(x) for x in v]), "graph_info")
-        return dict(zip(("valid", "nodes", "edges", "depth"), (int(x.value) for x in v)))
+        return dict(zip(("valid", "nodes", "edges", "depth", "captures", "capture_status"), (int(x.value) for x in v)))
 
     def overlap_probe(self) -> dict:
         """sptr_overlap_probe: ms of two 200-us spins serial, and beside each side stream."""

@@ -302,7 +302,8 @@ def _render_as_bench(renderer, cam, W, H, S):
         assert np.array_equal(rgb, runs[0][1])
         assert np.array_equal(acc.view(np.uint32), runs[0][2].view(np.uint32))
         assert (st.rays_closest, st.rays_shadow) == (runs[0][0].rays_closest, runs[0][0].rays_shadow)
-    assert renderer.graph_info()["valid"] == 1
+    g = renderer.graph_info()
+    assert g["valid"] == 1, g
     return runs[-1]
 
 

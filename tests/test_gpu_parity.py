@@ -517,7 +517,8 @@ def test_many_calls_without_collect(renderer, mode):
         renderer.collect_stats()
         assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32))
         if mode == 0:
-            assert renderer.graph_info()["valid"] == 1
+            g = renderer.graph_info()
+            assert g["valid"] == 1, g
     finally:
         renderer.set_launch_mode(0)
 
@@ -546,7 +547,7 @@ def test_multibatch_overlapped_graph_replay(renderer, scene, p0, p1, spp):
             out[mode] = runs
             if mode == 0:
                 g = renderer.graph_info()
-                assert g["valid"] == 1
+                assert g["valid"] == 1, g
                 # a DAG whose longest path runs through every batch's sequence
                 assert 3 * spp // 8 < g["depth"] <= g["nodes"] <= 4096, g
                 assert g["edges"] >= g["nodes"] - 1, g
