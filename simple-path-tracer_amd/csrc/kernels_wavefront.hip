@@ -1386,9 +1386,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // sample r*8 + q of round r), so a wave's rays come from 8 neighbouring pixels.  A pixel's leading
 // misses (the samples before its first hit) are summed into the accumulator in sample order — an
 // 8-step shuffle loop per round, the same adds in the same order as k_accum; later misses go to
-// rad[p] and accum.w records where k_accum resumes.  Blocks take 32-pixel chunks round-robin.
-// (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts 289 us, 8 lanes
-// 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
+// rad[p] and accum.w records where k_accum resumes.  Waves take 8 pixels at a time from the global
+// queue in k_cull's order (unculled pixels first), as k_trace_pm does (r04; r03 dealt 32-pixel block
+// chunks round-robin).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
+// 289 us, 8 lanes 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 template <bool kLds, bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WP_WAVES)
@@ -1396,9 +1397,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_cnt, s_taken;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
-  if (threadIdx.x == 0) s_cnt = 0u;
+  if (threadIdx.x == 0) s_cnt = s_taken = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   __syncthreads();
@@ -1409,16 +1410,28 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
-  constexpr uint32_t kPix = kBlock / kFoldLanes;  // pixels per block chunk
+  constexpr uint32_t kPix = kBlock / kFoldLanes;   // pixels per block round of the static share
+  constexpr uint32_t kWavePix = 64u / kFoldLanes;  // pixels per wave grab
   const uint32_t lane = lane_id(), q = lane & (kFoldLanes - 1u), g0 = lane & ~(kFoldLanes - 1u);
   const uint32_t lb = logical_block();
-  const uint32_t first = lb * kPix, step = gridDim.x * kPix;
-  const uint32_t per_pix = (f.P + step - 1u) / step * kPix;  // pixels per block at most
-  const uint32_t per = per_pix * f.k;                         // hit-record segment stride
+  const uint32_t step = gridDim.x * kPix;
+  const uint32_t cap = 2u * ((f.P + step - 1u) / step * kPix);  // pixels per block at most: twice its static share
+  const uint32_t per = cap * f.k;                                // hit-record segment stride
   const uint32_t seg0 = lb * per;
   const uint32_t rounds = (f.k + kFoldLanes - 1u) / kFoldLanes;
-  for (uint32_t base = first; base < f.P; base += step) {
-    const uint32_t l = base + threadIdx.x / kFoldLanes;
+  const uint32_t* order = f.pm_order;
+  const uint32_t n_unc = order ? order[f.P] : f.P;
+  uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
+  for (;;) {
+    uint32_t base = kNoHit;
+    if (lane == 0u) {
+      const uint32_t t = atomicAdd(&s_taken, kWavePix);
+      if (t + kWavePix <= cap) base = atomicAdd(queue, kWavePix);
+    }
+    base = __shfl(base, 0);
+    if (base >= f.P) break;
+    const uint32_t i = base + lane / kFoldLanes;
+    const uint32_t l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;

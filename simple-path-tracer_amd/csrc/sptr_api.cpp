@@ -570,7 +570,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.pixel_major = bounce0_pixel_major(sv, fv);
     fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
     fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
-    fv.pm_order = (fv.cull != nullptr && fv.pixel_major == kFoldThread) ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
+    fv.pm_order = (fv.cull != nullptr && fv.pixel_major != kFoldNone) ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
