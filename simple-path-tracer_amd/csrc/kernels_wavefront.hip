@@ -1636,16 +1636,85 @@ __device__ __forceinline__ uint32_t block_item(const Sched& sd, uint32_t k) {
   return sd.first + (k / kBlock) * sd.step + (k % kBlock);
 }
 
-template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
+// Per-XCD work queues (k_shadow_dyn and k_trace_dyn of scenes larger than an XCD's L2): one counter
+// per XCD (128 B apart) hands out that XCD's 256-item chunks of the static round-robin schedule in
+// order, a 64-item quarter at a time to a wave whose quarter is used up.  The schedule's L2 locality
+// stays (an XCD works through its own chunks in order), each counter sees an eighth of the grabs, and
+// no wave idles while its XCD holds unstarted items.  A producer with an output segment per block
+// (k_trace_dyn) reserves room for a quarter in its block's segment (s_taken, cap items) before taking
+// it; the segments hold twice the static shares, so while items remain some block of the XCD has room.
+constexpr uint32_t kQueueChunk = 64u;
+struct XcdQueue {
+  uint32_t* counter;
+  uint32_t xcd, per_xcd, n;
+  uint32_t cbase, cend;  // the wave's current quarter [cbase, cend) (wave-uniform)
+  bool drained;          // no unstarted item is left for this wave
+};
+__device__ __forceinline__ XcdQueue xcd_queue(uint32_t* counters, uint32_t n) {
+  XcdQueue q;
+  const bool xm = (gridDim.x % kXcds) == 0u;
+  q.xcd = xm ? blockIdx.x % kXcds : 0u;
+  q.per_xcd = xm ? gridDim.x / kXcds : gridDim.x;  // logical blocks per XCD
+  q.counter = counters + q.xcd * 32u;
+  q.n = n;
+  q.cbase = q.cend = 0u;
+  q.drained = false;
+  return q;
+}
+// The next item for each lane with `need` (kNoHit for the others, or when nothing is left); every lane
+// of the wave calls it together.
+__device__ __forceinline__ uint32_t xcd_take(XcdQueue& q, bool need, uint32_t* s_taken, uint32_t cap) {
+  const uint32_t lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const unsigned long long m = __ballot(need);
+  uint32_t item = kNoHit;
+  if (m == 0ull || q.drained) return item;
+  const uint32_t cnt = (uint32_t)__popcll(m), rank = (uint32_t)__popcll(m & below);
+  const uint32_t t1 = min(cnt, q.cend - q.cbase);
+  if (need && rank < t1) item = q.cbase + rank;
+  q.cbase += t1;
+  if (cnt > t1) {  // the quarter ran out: the next one from the queue
+    uint32_t u = kNoHit;
+    if (lane == 0u) {
+      const bool room = s_taken == nullptr || atomicAdd(s_taken, kQueueChunk) + kQueueChunk <= cap;
+      if (room) u = atomicAdd(q.counter, 1u);
+    }
+    u = __shfl(u, 0);
+    if (u == kNoHit) {  // this block's output segment is full: the XCD's other blocks take the rest
+      q.drained = true;
+      return item;
+    }
+    // unit u: quarter u % 4 of this XCD's (u / 4)-th chunk c = j * G + xcd * per_xcd + rr
+    const uint32_t kq = u >> 2, j = kq / q.per_xcd, rr = kq - j * q.per_xcd;
+    const uint64_t c = (uint64_t)j * gridDim.x + (uint64_t)q.xcd * q.per_xcd + rr;
+    const uint64_t b0 = c * kBlock + (u & 3u) * kQueueChunk;
+    if (b0 >= q.n) {
+      q.drained = true;
+    } else {
+      q.cbase = (uint32_t)b0;
+      q.cend = min((uint32_t)b0 + kQueueChunk, q.n);
+      const uint32_t t2 = min(cnt - t1, q.cend - q.cbase);
+      if (need && rank >= t1 && rank - t1 < t2) item = q.cbase + (rank - t1);
+      q.cbase += t2;
+    }
+  }
+  return item;
+}
+
+// kQueue (scenes larger than an XCD's L2, r04): items come from the per-XCD work queues (xcd_take,
+// counters zeroed by k_shade and k_accum) instead of the block's static share, so the launch does not
+// wait for the blocks that drew the costly rays; hit records stay in the block's segment, sized for
+// twice its static share.
+template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube, bool kQueue>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace_dyn(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt, s_next, s_hits;
+  __shared__ uint32_t s_cnt, s_next, s_hits, s_taken;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + (kLds ? sv.lds_bytes / 16u : 0u));
-  if (threadIdx.x == 0) s_cnt = s_next = s_hits = 0u;
+  if (threadIdx.x == 0) s_cnt = s_next = s_hits = s_taken = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   const uint32_t ntop = (kW4 && !kLds) ? sv.num_top4 : 0u;
@@ -1669,6 +1738,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   Visits vc;
   const Sched sd = block_sched(n);
   const uint32_t nb = block_items(sd, n);
+  const uint32_t cap = kQueue ? 2u * sd.per : sd.per;  // records of the block's hit-record segment
+  const uint32_t seg0 = logical_block() * cap;
+  XcdQueue xq = xcd_queue(w.work + kWorkTraceQueue, n);
   TravStack<kLds ? kLdsStack : kLdsStackG> stack;
   stack.lds = &s_stack.e[0][threadIdx.x];
   bool have = false, done = false;
@@ -1681,9 +1753,18 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   Ray r;
   WideWalk wk;
   for (;;) {
-    const uint32_t k = block_take(&s_next, !have);
-    if (!have && k < nb) {
-      const uint32_t i = block_item(sd, k);
+    uint32_t item = kNoHit;
+    bool more;  // unstarted items may remain for this wave
+    if constexpr (kQueue) {
+      item = xcd_take(xq, !have, &s_taken, cap);
+      more = !xq.drained;
+    } else {
+      const uint32_t k = block_take(&s_next, !have);
+      if (!have && k < nb) item = block_item(sd, k);
+      more = __ballot(!have && k < nb) != 0ull;
+    }
+    if (item != kNoHit) {
+      const uint32_t i = item;
       bool valid = true, culled = false;
       vec3 o, d;
       if (kPrimary) {
@@ -1716,8 +1797,8 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       }
     }
     if (__ballot(have) == 0ull) {
-      if (__ballot(!have && k < nb) == 0ull) break;  // nothing left for this wave
-      continue;                                       // only invalid (outside-image) items taken
+      if (!more) break;  // nothing left for this wave
+      continue;          // only invalid (outside-image) items taken
     }
     // the unified walk for camera rays as well (r03zy, with the pole ring's degenerate triangles out of
     // the tree and the launches overlapped: C5 8.45 inline vs 8.22 ms/step unified, means of 3; r03x,
@@ -1751,12 +1832,12 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
       if (nh && lane_id() == 0u) atomicAdd(&s_hits, nh);
     }
     if (rec) {
-      if (sd.seg0 + j < w.hrec_cap) w.hrec.put(sd.seg0 + j, id, wk.hit ? __float_as_uint(tfar) : pid, wk.hit ? ref : kNoHit);
+      if (seg0 + j < w.hrec_cap) w.hrec.put(seg0 + j, id, wk.hit ? __float_as_uint(tfar) : pid, wk.hit ? ref : kNoHit);
       else w.tot[kTotOverflow] = 1ull;
     }
     if (fin) have = false;
   }
-  seg_publish(w.segH, &s_cnt, sd.per);
+  seg_publish(w.segH, &s_cnt, cap);
   if (kCount && threadIdx.x == 0) atomicAdd(&w.tot[kPrimary ? kTotHitP : kTotHitB], (unsigned long long)s_hits);
   report_stack(vc, w.tot);
   if (kCount) {
@@ -1942,8 +2023,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 #endif
   const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x == 0) s_cnt_n = s_cnt_s = s_rays = 0u;
-  if (blockIdx.x == 0 && threadIdx.x < kXcds)  // k_shadow_dyn's per-XCD queues of this bounce
-    w.work[((uint32_t)depth % (kWorkWords / 256u)) * 256u + threadIdx.x * 32u] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < kXcds) {
+    w.work[((uint32_t)depth % 2u) * 256u + threadIdx.x * 32u] = 0u;  // k_shadow_dyn's queues of this bounce
+    w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;                 // k_trace_dyn's, for the next bounce
+  }
   const Staged sc = stage_scene<kFuse>(sv, lds);
   Visits vc;
   uint32_t rays = 0u;
@@ -2274,50 +2357,15 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   vec3 contrib;
   Ray r;
   WideWalk wk;
-  // kQueue: one queue per XCD (counter at a 128-B stride, zeroed by k_shade) hands out that XCD's
-  // 256-task chunks of the static round-robin schedule in order, 64 tasks at a time to a wave whose
-  // chunk is used up, so the schedule's L2 locality stays, each counter sees an eighth of the grabs,
-  // and no wave idles while its XCD still holds unstarted tasks.  Any block may trace any of its
-  // XCD's tasks: they only add to rad[p], there is no output stream.
-  constexpr uint32_t kQueueChunk = 64u;
-  const bool xm = (gridDim.x % kXcds) == 0u;
-  const uint32_t xcd = xm ? blockIdx.x % kXcds : 0u;
-  const uint32_t per_xcd = xm ? gridDim.x / kXcds : gridDim.x;  // logical blocks per XCD
-  uint32_t* queue = w.work + ((uint32_t)depth % (kWorkWords / 256u)) * 256u + xcd * 32u;
-  const uint32_t lane = lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t cbase = 0u, cend = 0u;  // the wave's current chunk [cbase, cend) (wave-uniform)
-  bool drained = false;            // the queue has no unstarted task left for this wave
+  // kQueue: the per-XCD work queues (xcd_take; counters zeroed by k_shade).  Any block may trace any
+  // of its XCD's tasks: they only add to rad[p], there is no output stream.
+  XcdQueue xq = xcd_queue(w.work + ((uint32_t)depth % 2u) * 256u, n);
   for (;;) {
     uint32_t item = kNoHit;
     bool more;  // unstarted tasks may remain for this wave
     if constexpr (kQueue) {
-      const unsigned long long need = __ballot(!have);
-      if (need != 0ull && !drained) {
-        const uint32_t cnt = (uint32_t)__popcll(need), rank = (uint32_t)__popcll(need & below);
-        const uint32_t t1 = min(cnt, cend - cbase);
-        if (!have && rank < t1) item = cbase + rank;
-        cbase += t1;
-        if (cnt > t1) {  // the chunk ran out: the next one from the queue
-          uint32_t u = 0u;
-          if (lane == 0u) u = atomicAdd(queue, 1u);
-          u = __shfl(u, 0);
-          // unit u: 64-task quarter u % 4 of this XCD's (u / 4)-th chunk c = j * G + xcd * per + rr
-          const uint32_t kq = u >> 2, j = kq / per_xcd, rr = kq - j * per_xcd;
-          const uint64_t c = (uint64_t)j * gridDim.x + (uint64_t)xcd * per_xcd + rr;
-          const uint64_t b0 = c * kBlock + (u & 3u) * kQueueChunk;
-          if (b0 >= n) {
-            drained = true;
-          } else {
-            cbase = (uint32_t)b0;
-            cend = min((uint32_t)b0 + kQueueChunk, n);
-            const uint32_t t2 = min(cnt - t1, cend - cbase);
-            if (!have && rank >= t1 && rank - t1 < t2) item = cbase + (rank - t1);
-            cbase += t2;
-          }
-        }
-      }
-      more = !drained;
+      item = xcd_take(xq, !have, nullptr, 0u);
+      more = !xq.drained;
     } else {
       const uint32_t k = block_take(&s_next, !have);
       if (!have && k < nb) item = block_item(sd, k);
@@ -2573,8 +2621,11 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
                                                   uint8_t* image) {
   const FrameView f = frame_dyn(fin);
   const uint32_t n_total = f.dyn ? f.dyn[2] : 0u;  // total frames of the accumulation (kResolve)
-  // the next batch's k_trace_pm takes its pixels from a fresh queue
-  if (f.dyn && blockIdx.x == 0 && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
+  // the next batch's bounce-0 trace (k_trace_pm, k_trace_wp, k_trace_dyn) takes its work from fresh queues
+  if (blockIdx.x == 0) {
+    if (f.dyn && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
+    if (threadIdx.x < kXcds) w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;
+  }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     uint32_t s0 = 0u;
     vec3 a = v3(0.0f, 0.0f, 0.0f);
@@ -3310,6 +3361,15 @@ static bool dyn_lds() {
   return kDynLds;
 #endif
 }
+// experiment knob SPTR_TRACE_QUEUE=0: k_trace_dyn keeps the block's static share (A/B)
+static bool trace_queue() {
+#ifdef SPTR_EXPERIMENT_KNOBS
+  static const bool v = !(getenv("SPTR_TRACE_QUEUE") && getenv("SPTR_TRACE_QUEUE")[0] == '0');
+  return v;
+#else
+  return true;
+#endif
+}
 static bool no_dyn() {
 #ifdef SPTR_EXPERIMENT_KNOBS
   static const bool v = getenv("SPTR_NO_DYN") != nullptr;
@@ -3352,19 +3412,21 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   }
   if (((!L && W) || (L && !W && !P && dyn_lds())) && !no_dyn()) {  // refilling lanes
     const unsigned lbd = lb + (!L && W ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
+    // per-XCD work queues for scenes larger than an XCD's L2 (as k_shadow_dyn)
+    const bool queue = !L && W && sv.scene_bytes > kL2BytesPerXcd && trace_queue();
     return dispatch(
         [&](auto fl) -> unsigned {
-          return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube>(Flags<Lc, C, Pc, Wc, Cube>) {
-            if constexpr (Lc == Wc) {
+          return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube, bool Q>(Flags<Lc, C, Pc, Wc, Cube, Q>) {
+            if constexpr (Lc == Wc || (Q && Lc)) {
               return 0u;  // not instantiated: LDS scenes traverse BVH2, L2/HBM scenes the wide BVH
             } else {
-              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube>, lbd);
-              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
+              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube, Q>, lbd);
+              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
               return g;
             }
           }(fl);
         },
-        Flags<>{}, L, count, P, W, cube);
+        Flags<>{}, L, count, P, W, cube, queue);
   }
   return dispatch(
       [&](auto fl) -> unsigned {

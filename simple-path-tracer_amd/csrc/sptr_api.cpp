@@ -110,11 +110,11 @@ size_t seg_table_bytes() { return 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kW
 
 // device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
 // L shadow tasks of ts float4s
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + kHitBytes + 16 + (uint64_t)L * ts * 16; }
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 2 * kHitBytes + 16 + (uint64_t)L * ts * 16; }
 // fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
 uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
   const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
-  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + recs * k_slack * kHitBytes;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + 2 * recs * k_slack * kHitBytes;
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
@@ -1002,7 +1002,7 @@ int sptr_create(int device, sptr_ctx** out) {
     return SPTR_ERR_HIP;
   }
   if (ensure_buf(c.wb.seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
-      ensure_buf(c.dyn, 64) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess) {
+      ensure_buf(c.dyn, kDynBytes) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess) {
     delete x;
     return SPTR_ERR_OOM;
   }
@@ -1295,7 +1295,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
         probe.k = f->spp % k;
         pm = pm || bounce0_pixel_major(scene_view(c), probe) != 0u;
       }
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, pm ? 2u : 1u);
+      // hit-record segments hold twice the static shares (the bounce-0 work queues, k_trace_dyn's per-XCD queues)
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, 2u);
       if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));

@@ -173,14 +173,18 @@ struct FrameView {
 };
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
 // the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
-constexpr uint32_t kDynPmQueue = 8;
+constexpr uint32_t kDynPmQueue = 32;  // a 128-B line of its own
+constexpr size_t kDynBytes = 256;
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
 // rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each
 // pixel's leading misses into accum and record the resume slot for k_accum.
 enum : uint32_t { kFoldNone = 0, kFoldThread = 1, kFoldWave = 2 };
 
-constexpr uint32_t kWorkWords = 512;  // work-queue counters (WaveView::work): 2 bounce slots x 8 XCDs, 128-B apart
+// work-queue counters (WaveView::work), 8 XCDs 128 B apart per slot: k_shadow_dyn's two bounce slots
+// (words 0 and 256), k_trace_dyn's (kWorkTraceQueue)
+constexpr uint32_t kWorkWords = 768;
+constexpr uint32_t kWorkTraceQueue = 512;
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 
 // 64-bit totals block
