@@ -285,6 +285,7 @@ __global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset,
     dyn[1] = reset;
     dyn[2] = total;
     dyn[kDynPmQueue] = 0u;
+    dyn[kDynSkyQueue] = 0u;
     if (clear) {
       clear[0] = 0u;
       clear[1] = 0u;
@@ -2537,14 +2538,59 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
 __device__ __forceinline__ bool sky_pixel(const FrameView& f, uint32_t l, int& x, int& y) {
   return pixel_culled(f, l) && local_pixel(f, l, x, y);
 }
-template <bool kCube>
+//
+// Work distribution (r04): a pixel's samples are one serial sum, so with a thread per pixel the
+// launch is made of units k samples long (C3: 256), dealt in blocks that also held the unculled pixels
+// (idle lanes) — and it ended on the last blocks' whole sample loops.  kLanes = 8: a lane group per
+// culled pixel, taken 8 pixels per wave from k_cull's list of culled pixels (plist[P - 1 - j]) through
+// a queue (FrameView::dyn[kDynSkyQueue], zeroed by k_frame_dyn and k_accum); lane q computes sample
+// r * 8 + q of round r, and the group adds the 8 radiances into the pixel's sum in sample order (the
+// fold of k_trace_wp), so every lane works and a unit is k / 8 samples long.  kLanes = 1 (batches of
+// fewer than 8 samples, or no list): a thread per pixel over the local pixels, the r03 kernel.
+template <bool kCube, uint32_t kLanes>
 __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
   const FrameView f = frame_dyn(fin);
   const ImageDiv idiv = image_div(f);
+  if constexpr (kLanes > 1u) {
+    const uint32_t n_cull = f.plist[f.P + 1u];  // k_cull's other list: culled pixels and tile slots outside the image
+    uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynSkyQueue;
+    const uint32_t lane = lane_id(), q = lane & (kLanes - 1u), g0 = lane & ~(kLanes - 1u);
+    constexpr uint32_t kWavePix = 64u / kLanes;
+    const uint32_t rounds = (f.k + kLanes - 1u) / kLanes;
+    for (;;) {
+      uint32_t base = 0u;
+      if (lane == 0u) base = atomicAdd(queue, kWavePix);
+      base = __shfl(base, 0);
+      if (base >= n_cull) break;
+      const uint32_t j = base + lane / kLanes;
+      const uint32_t l = j < n_cull ? f.plist[f.P - 1u - j] : kNoHit;
+      int x = 0, y = 0;
+      const bool valid = l < f.P && sky_pixel(f, l, x, y);
+      vec3 a = v3(0.0f, 0.0f, 0.0f);
+      if (valid && !f.reset) a = xyz(f.accum[l]);
+      const uint32_t ps = (uint32_t)(y * f.W + x);
+      for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t smp = r * kLanes + q;
+        vec3 rv = v3(0.0f, 0.0f, 0.0f);
+        if (valid && smp < f.k && sh.debug_mode != 1) {
+          Primary pr;
+          primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
+          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+        }
+        const uint32_t nact = min(kLanes, f.k - r * kLanes);
+#pragma unroll
+        for (uint32_t s = 0; s < kLanes; ++s) {
+          const float vx = __shfl(rv.x, (int)(g0 + s)), vy = __shfl(rv.y, (int)(g0 + s)), vz = __shfl(rv.z, (int)(g0 + s));
+          if (s < nact) a = v3(a.x + vx, a.y + vy, a.z + vz);
+        }
+      }
+      if (valid && q == 0u) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(f.k));
+    }
+    return;
+  }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     int x, y;
-    // only the culled pixels' words: k_accum sums the others (sky_pixel), so a batch's k_sky may run
-    // beside the previous batch's k_accum (two-lane calls, enqueue_wavefront)
+    // only the culled pixels' words: k_accum sums the others (sky_pixel)
     if (sky_pixel(f, l, x, y)) {
       vec3 a = v3(0.0f, 0.0f, 0.0f);
       if (!f.reset) a = xyz(f.accum[l]);
@@ -2621,9 +2667,11 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
                                                   uint8_t* image) {
   const FrameView f = frame_dyn(fin);
   const uint32_t n_total = f.dyn ? f.dyn[2] : 0u;  // total frames of the accumulation (kResolve)
-  // the next batch's bounce-0 trace (k_trace_pm, k_trace_wp, k_trace_dyn) takes its work from fresh queues
+  // the next batch's bounce-0 trace (k_trace_pm, k_trace_wp, k_trace_dyn) and k_sky take their work
+  // from fresh queues
   if (blockIdx.x == 0) {
     if (f.dyn && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
+    if (f.dyn && threadIdx.x == 64) const_cast<uint32_t*>(f.dyn)[kDynSkyQueue] = 0u;
     if (threadIdx.x < kXcds) w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;
   }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
@@ -3592,8 +3640,16 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
   constexpr unsigned cap = 16384u;
 #endif
   const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
-  if (sh.env.env != nullptr) hipLaunchKernelGGL(k_sky<true>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
-  else hipLaunchKernelGGL(k_sky<false>, dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  if (f.plist && f.dyn && f.k >= 8u) {  // lane groups over k_cull's culled-pixel list, resident grid
+    const bool cube = sh.env.env != nullptr;
+    const void* fn = cube ? (const void*)&k_sky<true, 8u> : (const void*)&k_sky<false, 8u>;
+    const unsigned gr = std::min<unsigned>(resident_grid(fn, 0u), std::max(1u, g));
+    if (cube) hipLaunchKernelGGL((k_sky<true, 8u>), dim3(gr), dim3(kBlock), 0, s, sh.env, f);
+    else hipLaunchKernelGGL((k_sky<false, 8u>), dim3(gr), dim3(kBlock), 0, s, sh.env, f);
+    return;
+  }
+  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_sky<true, 1u>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  else hipLaunchKernelGGL((k_sky<false, 1u>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
 }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,

@@ -173,7 +173,8 @@ struct FrameView {
 };
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
 // the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
-constexpr uint32_t kDynPmQueue = 32;  // a 128-B line of its own
+constexpr uint32_t kDynPmQueue = 32;   // a 128-B line of its own
+constexpr uint32_t kDynSkyQueue = 64;  // k_sky's work queue, likewise
 constexpr size_t kDynBytes = 256;
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
