@@ -27,6 +27,11 @@ for wl in "$@"; do
   echo "[$(date +%T)] rocprof kernel trace + stats $wl"
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_$wl" -o run -- \
     python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive > "$out/stats_$wl.log" 2>&1
+  if [ "$wl" = c3 ] || [ "$wl" = c5 ]; then  # the launches alone: one stream, nothing overlapped (roofline_serial)
+    echo "[$(date +%T)] rocprof kernel trace + stats $wl, launch mode 2"
+    timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_${wl}_serial" -o run -- \
+      python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive --launch-mode 2 > "$out/stats_${wl}_serial.log" 2>&1
+  fi
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "[$(date +%T)] pmc $c $wl"
     timeout -s KILL 300 rocprofv3 --pmc "$c" --output-format csv -d "$out/pmc_${c}_$wl" -o run -- \
