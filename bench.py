@@ -429,6 +429,7 @@ def main():
     ap.add_argument("--wave-paths", type=int, default=0)
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
+    ap.add_argument("--split-refs", type=int, default=0, help="most references per split triangle (0 = library default, 1 = none)")
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
     ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2],
                     help="0: replay captured launch graphs (default); 1: direct launches; 2: direct launches on one "
@@ -486,6 +487,8 @@ def main():
         r.set_leaf_size(args.leaf_size)
     if args.bvh_width:
         r.set_bvh_width(args.bvh_width)
+    if args.split_refs:
+        r.set_split_refs(args.split_refs)
     if args.tail_depth:
         r.set_tail_depth(args.tail_depth)
     if args.launch_mode:
@@ -611,6 +614,8 @@ def main():
         knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
         if args.launch_mode:
             knobs["launch_mode"] = args.launch_mode
+        if args.split_refs:
+            knobs["split_refs"] = args.split_refs
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),
