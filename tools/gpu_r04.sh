@@ -18,3 +18,6 @@ for wl in c5 c3 c2; do
   timeout -k 10 300 python3 bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-interactive > $out/bench_$wl.json 2> $out/bench_$wl.err || exit 3
   python3 -c "import json;d=json.loads(open('$out/bench_$wl.json').read().splitlines()[-1]);r=d['roofline'];print('$wl',d['ms_per_step'],d['value'],'trace',r['avg_launch_us'],r['frac'],'hist',r.get('visit_hist_log2'),'serial',json.dumps(d.get('roofline_serial')),'step',d.get('step_roofline',{}).get('frac'),'probe',d['overlap_probe'],'refs',d['scene'].get('prim_refs'),'stages',d['stage_ms_per_step'])"
 done
+# A/B: C5 without split references
+timeout -k 10 300 python3 bench.py --workload c5 --steps 10 --warmup 2 --no-cpu-baseline --no-interactive --no-serial-pass --split-refs 1 > $out/bench_c5_nosplit.json 2> $out/bench_c5_nosplit.err || exit 4
+python3 -c "import json;d=json.loads(open('$out/bench_c5_nosplit.json').read().splitlines()[-1]);r=d['roofline'];print('c5 nosplit',d['ms_per_step'],d['value'],'trace',r['avg_launch_us'],'stages',d['stage_ms_per_step'],'build',d['scene']['lbvh_build_ms'])"
