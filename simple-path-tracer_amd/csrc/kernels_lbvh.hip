@@ -9,7 +9,7 @@
 //                   (early split clipping); every other primitive keeps one reference with its own box
 //   k_ref_bounds  : centroid bounds of the references (ordered-int atomics)
 //   k_morton      : 63-bit Morton code (21 bits/axis) of a reference's box centroid, value = reference id
-//   radix sort    : rocPRIM radix_sort_pairs on the codes
+//   radix sort    : radix_sort_pairs_u64 on the codes (kernels_sort.hip, hand-written LSD, stable)
 //   k_leaves      : scatter triangles (v0, e1, e2, Ng precomputed as Embree's TriangleM does) and
 //                   spheres into sorted slots, one slot per reference (a split triangle's references
 //                   each hold a copy); typed leaf links
@@ -34,7 +34,6 @@
 #include <chrono>
 #include <cstring>
 #include <vector>
-#include <rocprim/rocprim.hpp>
 
 #include "sptr_internal.h"
 
@@ -1255,10 +1254,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
                                   ? 1u : std::min<uint32_t>(c.split_pieces, 1u << kMaxSplitDepth);
   hipLaunchKernelGGL(k_split_count, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi, max_pieces, rcnt);
   size_t rbytes = 0;
-  LB_CHECK(rocprim::exclusive_scan(nullptr, rbytes, rcnt, roff, 0u, NP, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(scan_u32(nullptr, rbytes, rcnt, roff, NP, s));
   void* rstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&rstore), rbytes));
-  LB_CHECK(rocprim::exclusive_scan(rstore, rbytes, rcnt, roff, 0u, NP, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(scan_u32(rstore, rbytes, rcnt, roff, NP, s));
   uint32_t last2[2] = {0u, 0u};
   LB_CHECK(hipMemcpyAsync(&last2[0], rcnt + (NP - 1), 4, hipMemcpyDeviceToHost, s));
   LB_CHECK(hipMemcpyAsync(&last2[1], roff + (NP - 1), 4, hipMemcpyDeviceToHost, s));
@@ -1308,10 +1307,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   hipLaunchKernelGGL(k_morton, dim3(blocks_for(NR)), dim3(256), 0, s, in, NR, blo, bhi, rprim, cb, keys, vals, dmax);
   LB_CHECK(hipGetLastError());
   size_t tbytes = 0;
-  LB_CHECK(rocprim::radix_sort_pairs(nullptr, tbytes, keys, keys_s, vals, vals_s, NR, 0, 64, s));
+  LB_CHECK(radix_sort_pairs_u64(nullptr, tbytes, keys, keys_s, vals, vals_s, NR, s));
   void* tstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
-  LB_CHECK(rocprim::radix_sort_pairs(tstore, tbytes, keys, keys_s, vals, vals_s, NR, 0, 64, s));
+  LB_CHECK(radix_sort_pairs_u64(tstore, tbytes, keys, keys_s, vals, vals_s, NR, s));
 #if SPTR_EXPERIMENT_HOST_SAH
   std::vector<uint32_t> sah_order;
   std::vector<BvhNode> sah_nodes;
@@ -1324,10 +1323,10 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
 #endif
   hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(NR)), dim3(256), 0, s, NR, ntris, vals_s, rprim, flag);
   size_t sbytes = 0;
-  LB_CHECK(rocprim::exclusive_scan(nullptr, sbytes, flag, slot, 0u, NR, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(scan_u32(nullptr, sbytes, flag, slot, NR, s));
   void* sstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&sstore), sbytes));
-  LB_CHECK(rocprim::exclusive_scan(sstore, sbytes, flag, slot, 0u, NR, rocprim::plus<uint32_t>(), s));
+  LB_CHECK(scan_u32(sstore, sbytes, flag, slot, NR, s));
   hipLaunchKernelGGL(k_leaves, dim3(blocks_for(NR)), dim3(256), 0, s, in, NR, vals_s, rprim, slot,
                      static_cast<float4*>(c.tris.p), static_cast<uint32_t*>(c.tri_geom.p),
                      static_cast<uint32_t*>(c.tri_orig.p), static_cast<float4*>(c.sph.p),
@@ -1447,7 +1446,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       LB_CHECK(tmp.alloc(&nxt, N));
       LB_CHECK(tmp.alloc(&off, N));
       size_t sw = 0;
-      LB_CHECK(rocprim::exclusive_scan(nullptr, sw, flag, off, 0u, N, rocprim::plus<uint32_t>(), s));
+      LB_CHECK(scan_u32(nullptr, sw, flag, off, N, s));
       void* stw = nullptr;
       LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&stw), sw));
       LB_CHECK(realloc_buf(c.nodes4, (size_t)(N - 1) * sizeof(WideNode)));  // <= one wide node per BVH2 node
@@ -1458,7 +1457,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       while (ncur > 0u) {
         hipLaunchKernelGGL(k_wide_count, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, nodes, flag);
         LB_CHECK(hipGetLastError());
-        LB_CHECK(rocprim::exclusive_scan(stw, sw, flag, off, 0u, ncur, rocprim::plus<uint32_t>(), s));
+        LB_CHECK(scan_u32(stw, sw, flag, off, ncur, s));
         hipLaunchKernelGGL(k_wide_emit, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, base, nodes, off, nxt,
                            static_cast<WideNode*>(c.nodes4.p), static_cast<const uint32_t*>(c.prim_ref.p),
                            (uint32_t)SPTR_WIDE_DIRECT);
@@ -1485,11 +1484,11 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       hipLaunchKernelGGL(k_depth_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag, topf);
       LB_CHECK(hipGetLastError());
       size_t s4 = 0;
-      LB_CHECK(rocprim::exclusive_scan(nullptr, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
+      LB_CHECK(scan_u32(nullptr, s4, flag, slot, N - 1, s));
       void* st4 = nullptr;
       LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&st4), s4));
-      LB_CHECK(rocprim::exclusive_scan(st4, s4, flag, slot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
-      LB_CHECK(rocprim::exclusive_scan(st4, s4, topf, tslot, 0u, N - 1, rocprim::plus<uint32_t>(), s));
+      LB_CHECK(scan_u32(st4, s4, flag, slot, N - 1, s));
+      LB_CHECK(scan_u32(st4, s4, topf, tslot, N - 1, s));
       uint32_t last[4] = {0u, 0u, 0u, 0u};  // keep, slot, top, tslot of node N - 2
       LB_CHECK(hipMemcpyAsync(&last[0], flag + (N - 2), 4, hipMemcpyDeviceToHost, s));
       LB_CHECK(hipMemcpyAsync(&last[1], slot + (N - 2), 4, hipMemcpyDeviceToHost, s));

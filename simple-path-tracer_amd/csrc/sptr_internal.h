@@ -410,6 +410,11 @@ struct Context {
 int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* h_idx, uint32_t ntris,
                const float* h_sph, uint32_t nsph, const uint32_t* h_tri_geom, uint32_t sph_geom_base);
 
+// kernels_sort.hip: the build's device primitives (temp == nullptr: set temp_bytes only)
+hipError_t scan_u32(void* temp, size_t& temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s);
+hipError_t radix_sort_pairs_u64(void* temp, size_t& temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                                const uint32_t* vals_in, uint32_t* vals_out, uint32_t n, hipStream_t s);
+
 // kernels_wavefront.hip
 SceneView scene_view(const Context& c);
 // Stage launchers return their (resident) grid size: the segment count their consumer scans.
