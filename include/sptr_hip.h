@@ -234,6 +234,8 @@ int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
  * fails the call with SPTR_ERR_HIP).  Any pointer may be NULL. */
 int sptr_graph_info(const sptr_ctx* ctx, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth,
                     uint32_t* captures, int32_t* capture_status);
+/* The call that made the last capture attempt fall back to direct launches, with its error text ("" if none). */
+const char* sptr_capture_error(const sptr_ctx* ctx);
 /* Whether the context's side streams run beside its render stream on this device: ms[0] = two 200-us
  * one-wave spins on the render stream, ms[1] = one there and one on the shadow side stream, ms[2] = one
  * there and one on the k_sky side stream (device events).  ms[1], ms[2] near ms[0] / 2: the side

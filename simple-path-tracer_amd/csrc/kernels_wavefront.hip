@@ -24,6 +24,17 @@
 #include "sptr_internal.h"
 
 // Occupancy hints (min waves per SIMD); 1 = let the register allocator decide.
+// r04 work distribution (A/B builds): bounce-0 pixel-major work queue; k_sky lane groups over the
+// culled list; k_trace_dyn per-XCD queues (DESIGN.md §3 "Work queues")
+#ifndef SPTR_PM_QUEUE
+#define SPTR_PM_QUEUE 1
+#endif
+#ifndef SPTR_SKY_LANES
+#define SPTR_SKY_LANES 1
+#endif
+#ifndef SPTR_TRACE_QUEUE
+#define SPTR_TRACE_QUEUE 1
+#endif
 #ifndef SPTR_TRACE_WAVES
 #define SPTR_TRACE_WAVES 7  // measured: 7 -> +6% on C2 (SGPR-limited to 6 otherwise)
 #endif
@@ -285,7 +296,9 @@ __global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset,
     dyn[1] = reset;
     dyn[2] = total;
     dyn[kDynPmQueue] = 0u;
-    dyn[kDynSkyQueue] = 0u;
+  }
+  if (threadIdx.x < kXcds) dyn[kDynSkyQueue + 32u * threadIdx.x] = 0u;
+  if (threadIdx.x == 0) {
     if (clear) {
       clear[0] = 0u;
       clear[1] = 0u;
@@ -1307,23 +1320,31 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   const ImageDiv idiv = image_div(f);
   Visits vc;
   const Sched sd = block_sched(f.P);
-  const uint32_t cap = 2u * sd.per;  // pixels this block may take: its hit-record segment holds cap * k records
-  const uint32_t per = cap * f.k;    // hit-record segment stride
+  constexpr bool kQ = SPTR_PM_QUEUE != 0;
+  const uint32_t cap = kQ ? 2u * sd.per : sd.per;  // pixels this block may take: its hit-record segment holds cap * k records
+  const uint32_t per = cap * f.k;                  // hit-record segment stride
   const uint32_t seg0 = logical_block() * per;
   const uint32_t* order = f.pm_order;  // k_cull's list (null without a cull mask: local pixel order)
   const uint32_t n_unc = order ? order[f.P] : f.P;
   uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
   const uint32_t lane = lane_id();
-  for (;;) {
-    uint32_t base = kNoHit;
-    if (lane == 0u) {
-      const uint32_t t = atomicAdd(&s_taken, 64u);
-      if (t + 64u <= cap) base = atomicAdd(queue, 64u);
+  for (uint32_t it = 0;; ++it) {
+    uint32_t l;
+    if constexpr (kQ) {
+      uint32_t base = kNoHit;
+      if (lane == 0u) {
+        const uint32_t t = atomicAdd(&s_taken, 64u);
+        if (t + 64u <= cap) base = atomicAdd(queue, 64u);
+      }
+      base = __shfl(base, 0);
+      if (base >= f.P) break;  // the frame is taken (or this block's segment is full)
+      const uint32_t i = base + lane;
+      l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
+    } else {  // the static share: 256-pixel chunks dealt round-robin
+      const uint32_t base = sd.first + it * sd.step;
+      if (base >= sd.end) break;
+      l = base + threadIdx.x;
     }
-    base = __shfl(base, 0);
-    if (base >= f.P) break;  // the frame is taken (or this block's segment is full)
-    const uint32_t i = base + lane;
-    const uint32_t l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
@@ -1416,23 +1437,31 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
   const uint32_t lane = lane_id(), q = lane & (kFoldLanes - 1u), g0 = lane & ~(kFoldLanes - 1u);
   const uint32_t lb = logical_block();
   const uint32_t step = gridDim.x * kPix;
-  const uint32_t cap = 2u * ((f.P + step - 1u) / step * kPix);  // pixels per block at most: twice its static share
-  const uint32_t per = cap * f.k;                                // hit-record segment stride
+  constexpr bool kQ = SPTR_PM_QUEUE != 0;
+  const uint32_t cap = (kQ ? 2u : 1u) * ((f.P + step - 1u) / step * kPix);  // pixels per block at most
+  const uint32_t per = cap * f.k;                                           // hit-record segment stride
   const uint32_t seg0 = lb * per;
   const uint32_t rounds = (f.k + kFoldLanes - 1u) / kFoldLanes;
   const uint32_t* order = f.pm_order;
   const uint32_t n_unc = order ? order[f.P] : f.P;
   uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
-  for (;;) {
-    uint32_t base = kNoHit;
-    if (lane == 0u) {
-      const uint32_t t = atomicAdd(&s_taken, kWavePix);
-      if (t + kWavePix <= cap) base = atomicAdd(queue, kWavePix);
+  for (uint32_t it = 0;; ++it) {
+    uint32_t l;
+    if constexpr (kQ) {
+      uint32_t base = kNoHit;
+      if (lane == 0u) {
+        const uint32_t t = atomicAdd(&s_taken, kWavePix);
+        if (t + kWavePix <= cap) base = atomicAdd(queue, kWavePix);
+      }
+      base = __shfl(base, 0);
+      if (base >= f.P) break;
+      const uint32_t i = base + lane / kFoldLanes;
+      l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
+    } else {  // the static share: 32-pixel block chunks dealt round-robin
+      const uint32_t base = lb * kPix + it * step;
+      if (base >= f.P) break;
+      l = base + threadIdx.x / kFoldLanes;
     }
-    base = __shfl(base, 0);
-    if (base >= f.P) break;
-    const uint32_t i = base + lane / kFoldLanes;
-    const uint32_t l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
@@ -2553,17 +2582,28 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
   const ImageDiv idiv = image_div(f);
   if constexpr (kLanes > 1u) {
     const uint32_t n_cull = f.plist[f.P + 1u];  // k_cull's other list: culled pixels and tile slots outside the image
-    uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynSkyQueue;
+    // per-XCD counters (128 B apart): counter x hands out the 64-pixel chunks c = 8 u + x, a wave works
+    // through a chunk 8 pixels at a time (grids of fewer than 8 blocks use counter 0 for every chunk)
+    const uint32_t nq = gridDim.x >= kXcds ? kXcds : 1u, qx = blockIdx.x % nq;
+    uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynSkyQueue + 32u * qx;
     const uint32_t lane = lane_id(), q = lane & (kLanes - 1u), g0 = lane & ~(kLanes - 1u);
-    constexpr uint32_t kWavePix = 64u / kLanes;
+    constexpr uint32_t kWavePix = 64u / kLanes;  // pixels per wave round
+    constexpr uint32_t kChunkPix = 64u;          // pixels per queue grab
     const uint32_t rounds = (f.k + kLanes - 1u) / kLanes;
+    uint32_t cbase = 0u, cend = 0u;
     for (;;) {
-      uint32_t base = 0u;
-      if (lane == 0u) base = atomicAdd(queue, kWavePix);
-      base = __shfl(base, 0);
-      if (base >= n_cull) break;
+      if (cbase >= cend) {
+        uint32_t u = 0u;
+        if (lane == 0u) u = atomicAdd(queue, 1u);
+        u = __shfl(u, 0);
+        cbase = (u * nq + qx) * kChunkPix;
+        if (cbase >= n_cull) break;
+        cend = min(cbase + kChunkPix, n_cull);
+      }
+      const uint32_t base = cbase;
+      cbase += kWavePix;
       const uint32_t j = base + lane / kLanes;
-      const uint32_t l = j < n_cull ? f.plist[f.P - 1u - j] : kNoHit;
+      const uint32_t l = j < cend ? f.plist[f.P - 1u - j] : kNoHit;
       int x = 0, y = 0;
       const bool valid = l < f.P && sky_pixel(f, l, x, y);
       vec3 a = v3(0.0f, 0.0f, 0.0f);
@@ -2671,7 +2711,7 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
   // from fresh queues
   if (blockIdx.x == 0) {
     if (f.dyn && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
-    if (f.dyn && threadIdx.x == 64) const_cast<uint32_t*>(f.dyn)[kDynSkyQueue] = 0u;
+    if (f.dyn && threadIdx.x >= 64 && threadIdx.x < 64 + kXcds) const_cast<uint32_t*>(f.dyn)[kDynSkyQueue + 32u * (threadIdx.x - 64)] = 0u;
     if (threadIdx.x < kXcds) w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;
   }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
@@ -3409,15 +3449,8 @@ static bool dyn_lds() {
   return kDynLds;
 #endif
 }
-// experiment knob SPTR_TRACE_QUEUE=0: k_trace_dyn keeps the block's static share (A/B)
-static bool trace_queue() {
-#ifdef SPTR_EXPERIMENT_KNOBS
-  static const bool v = !(getenv("SPTR_TRACE_QUEUE") && getenv("SPTR_TRACE_QUEUE")[0] == '0');
-  return v;
-#else
-  return true;
-#endif
-}
+// SPTR_TRACE_QUEUE=0 (A/B builds): k_trace_dyn keeps the block's static share
+static bool trace_queue() { return SPTR_TRACE_QUEUE != 0; }
 static bool no_dyn() {
 #ifdef SPTR_EXPERIMENT_KNOBS
   static const bool v = getenv("SPTR_NO_DYN") != nullptr;
@@ -3640,7 +3673,7 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
   constexpr unsigned cap = 16384u;
 #endif
   const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
-  if (f.plist && f.dyn && f.k >= 8u) {  // lane groups over k_cull's culled-pixel list, resident grid
+  if (SPTR_SKY_LANES && f.plist && f.dyn && f.k >= 8u) {  // lane groups over k_cull's culled-pixel list, resident grid
     const bool cube = sh.env.env != nullptr;
     const void* fn = cube ? (const void*)&k_sky<true, 8u> : (const void*)&k_sky<false, 8u>;
     const unsigned gr = std::min<unsigned>(resident_grid(fn, 0u), std::max(1u, g));

@@ -265,6 +265,7 @@ struct StageTimer {
   bool trace_only;          // SPTR_FRAME_TIMING_TRACE alone: stages 1 and 5 only
   hipStream_t s;
   hipError_t err = hipSuccess;
+  const char* what = "";    // the call that set err
   size_t open = SIZE_MAX;   // index in c.marks of the stage being recorded
   size_t call = SIZE_MAX;   // index in c.marks of this call's stage-0 span
   size_t alloc() {  // a pool event for this call (not recorded)
@@ -283,7 +284,10 @@ struct StageTimer {
   size_t next() {
     const size_t i = alloc();
     if (i != SIZE_MAX && err == hipSuccess)
+    {
       err = capturing ? hipEventRecordWithFlags(c.events[i], s, hipEventRecordExternal) : hipEventRecord(c.events[i], s);
+      if (err != hipSuccess) what = capturing ? "stage event record (external)" : "stage event record";
+    }
     return i;
   }
   void begin(int stage) {
@@ -541,17 +545,20 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   const hipStream_t ss = cap ? c.cap_side : c.side_stream;   // k_shadow_dyn(d)
   const hipStream_t ks = cap ? c.cap_side2 : c.side2_stream;  // k_sky (apart from the shadow launches it outlasts)
   const Context::DepEvents& ev = c.dev[cap ? 1 : 0];
-  auto check = [&](hipError_t e) {
-    if (e != hipSuccess && tm.err == hipSuccess) tm.err = e;
+  auto check = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && tm.err == hipSuccess) {
+      tm.err = e;
+      tm.what = what;
+    }
   };
   auto fork_to = [&](hipStream_t side) {  // side's next launches start after everything enqueued on s so far
-    check(hipEventRecord(ev.fork, s));
-    check(hipStreamWaitEvent(side, ev.fork, 0));
+    check(hipEventRecord(ev.fork, s), "shadow fork record");
+    check(hipStreamWaitEvent(side, ev.fork, 0), "shadow fork wait");
   };
   // pending side-stream work: shadow(d) (ev.join) and k_sky (ev.sky)
   bool join = false, join_sky = false;
   auto join_shadow = [&]() {
-    if (join) check(hipStreamWaitEvent(s, ev.join, 0));
+    if (join) check(hipStreamWaitEvent(s, ev.join, 0), "shadow join wait");
     join = false;
   };
   // any-hit launches of their own (k_shadow_dyn: scenes traversed from L2/HBM) run on the side stream
@@ -616,14 +623,14 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       // words, which nothing reads before this batch's k_accum, the join point): its VALU-bound blocks
       // fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.  Enqueued
       // after the trace, so that the trace's grid is dispatched first.
-      if (sky_side) check(hipEventRecord(ev.fork, s));
+      if (sky_side) check(hipEventRecord(ev.fork, s), "sky fork record");
       tm.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
       if (sky_side) {
-        check(hipStreamWaitEvent(ks, ev.fork, 0));
+        check(hipStreamWaitEvent(ks, ev.fork, 0), "sky fork wait");
         launch_sky(sh, fv, ks);
-        check(hipEventRecord(ev.sky, ks));
+        check(hipEventRecord(ev.sky, ks), "sky join record");
         join_sky = true;
       }
       join_shadow();  // shadow(d - 1) before shade(d)
@@ -635,7 +642,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         tside.begin(3);
         launch_shadow(sv, sh, w, d, count, g_shade, ss);
         tside.end();
-        check(hipEventRecord(ev.join, ss));
+        check(hipEventRecord(ev.join, ss), "shadow join record");
         join = true;
       } else if (!fuse) {
         tm.begin(3);
@@ -647,7 +654,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     // sum it holds, as k_resolve would next)
     const bool resolve = done + kk >= f.spp && !(f.flags & SPTR_FRAME_NO_RESOLVE);
     join_shadow();
-    if (join_sky) check(hipStreamWaitEvent(s, ev.sky, 0));
+    if (join_sky) check(hipStreamWaitEvent(s, ev.sky, 0), "sky join wait");
     join_sky = false;
     tm.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
@@ -656,7 +663,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     done += kk;
     ++waves;
   }
-  if (tside.err != hipSuccess && tm.err == hipSuccess) tm.err = tside.err;
+  if (tside.err != hipSuccess && tm.err == hipSuccess) {
+    tm.err = tside.err;
+    tm.what = tside.what;
+  }
   tm.end_call();
   return waves;
 }
@@ -826,6 +836,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     if (ec != hipSuccess || tm.err != hipSuccess || !g) {
       // not capturable (e.g. more stage spans than the pre-grown event pool): direct launches
       c.capture_status = (int32_t)(ec != hipSuccess ? ec : (tm.err != hipSuccess ? tm.err : hipErrorUnknown));
+      c.capture_error = ec != hipSuccess ? std::string("hipStreamEndCapture: ") + hipGetErrorString(ec)
+                                         : std::string(tm.what) + ": " + hipGetErrorString(tm.err);
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
       StageTimer td{c, timing, trace_only, s};
@@ -1331,6 +1343,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   }
   return collect_pending(c, stats);
 }
+
+const char* sptr_capture_error(const sptr_ctx* x) { return x ? x->c.capture_error.c_str() : "null context"; }
 
 int sptr_graph_info(const sptr_ctx* x, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth,
                     uint32_t* captures, int32_t* capture_status) {

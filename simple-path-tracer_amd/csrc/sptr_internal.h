@@ -174,8 +174,8 @@ struct FrameView {
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
 // the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
 constexpr uint32_t kDynPmQueue = 32;   // a 128-B line of its own
-constexpr uint32_t kDynSkyQueue = 64;  // k_sky's work queue, likewise
-constexpr size_t kDynBytes = 256;
+constexpr uint32_t kDynSkyQueue = 64;  // k_sky's per-XCD work queues, 32 words (128 B) apart
+constexpr size_t kDynBytes = 2048;
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
 // rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each
@@ -348,6 +348,7 @@ struct Context {
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
   GraphCache graph;
   int32_t capture_status = 0;        // hipError_t of the last capture that fell back to direct launches (0: none)
+  std::string capture_error;         // ... and the call that returned it
   uint32_t captures = 0;             // graphs captured and instantiated
   GraphKey last_key{};               // the previous call's shape: a graph is captured when it repeats
   bool have_last_key = false;

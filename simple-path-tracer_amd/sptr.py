@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_launch_mode": (C.c_int, [vp, u32]),
         "sptr_graph_info": (C.c_int, [vp, up, up, up, up, up, C.POINTER(C.c_int32)]),
+        "sptr_capture_error": (C.c_char_p, [vp]),
         "sptr_overlap_probe": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
@@ -405,7 +406,9 @@ class Renderer:
         """sptr_graph_info: the held launch graph (valid, nodes, edges, longest-path depth)."""
         v = [C.c_uint32() for _ in range(5)] + [C.c_int32()]
         self._check(self._L.sptr_graph_info(self._h, *[C.byref(x) for x in v]), "graph_info")
-        return dict(zip(("valid", "nodes", "edges", "depth", "captures", "capture_status"), (int(x.value) for x in v)))
+        d = dict(zip(("valid", "nodes", "edges", "depth", "captures", "capture_status"), (int(x.value) for x in v)))
+        d["capture_error"] = self._L.sptr_capture_error(self._h).decode()
+        return d
 
     def overlap_probe(self) -> dict:
         """sptr_overlap_probe: ms of two 200-us spins serial, and beside each side stream."""
