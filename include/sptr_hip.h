@@ -218,8 +218,9 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 /* Split references (early split clipping) for scenes traversed from L2/HBM: a triangle whose box is
  * much larger than the triangle (a sliver lying across the axes) is referenced up to max_pieces times,
  * each reference bounding one piece of it, so that rays near a fan of slivers stop testing every
- * sliver's box.  0 = default (16), 1 = no splits, else a power of two up to 32; applies to the next
- * sptr_upload_scene.  Results do not depend on it (each reference tests the same triangle). */
+ * sliver's box.  0 = default (1: no splits — measured no faster on the 10M-triangle mesh),
+ * else a power of two up to 32; applies to the next sptr_upload_scene.  Results do not depend on it
+ * (each reference tests the same triangle). */
 int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call

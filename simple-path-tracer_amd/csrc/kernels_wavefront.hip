@@ -24,17 +24,6 @@
 #include "sptr_internal.h"
 
 // Occupancy hints (min waves per SIMD); 1 = let the register allocator decide.
-// r04 work distribution (A/B builds): bounce-0 pixel-major work queue; k_sky lane groups over the
-// culled list; k_trace_dyn per-XCD queues (DESIGN.md §3 "Work queues")
-#ifndef SPTR_PM_QUEUE
-#define SPTR_PM_QUEUE 1
-#endif
-#ifndef SPTR_SKY_LANES
-#define SPTR_SKY_LANES 1
-#endif
-#ifndef SPTR_TRACE_QUEUE
-#define SPTR_TRACE_QUEUE 1
-#endif
 #ifndef SPTR_TRACE_WAVES
 #define SPTR_TRACE_WAVES 7  // measured: 7 -> +6% on C2 (SGPR-limited to 6 otherwise)
 #endif
@@ -1059,6 +1048,8 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
 // tile and sets the quad's bits in the tile's 32 LDS row words; then each thread lists the pixels of 4
 // consecutive local indices, the tile's runs at ranges one atomic per tile and list reserves.  (r02: a
 // pyramid per pixel and one atomic per wave, C2 108 us; per pixel and per tile 65-75 us.)
+// the list of the other pixels is written only when a work queue reads it (SPTR_PM_QUEUE, SPTR_SKY_LANES)
+constexpr bool kCullListBoth = SPTR_PM_QUEUE != 0 || SPTR_SKY_LANES != 0;
 __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
   static_assert(kTile == 32 && kBlock == 256, "16 x 16 quads per 32 x 32 tile");
   __shared__ uint32_t s_row[kTile];
@@ -1128,7 +1119,7 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
       runc += cd;
     }
     s_base = run ? atomicAdd(&plist[f.P], run) : 0u;
-    s_cbase = runc ? atomicAdd(&plist[f.P + 1u], runc) : 0u;
+    s_cbase = (kCullListBoth && runc) ? atomicAdd(&plist[f.P + 1u], runc) : 0u;
   }
   __syncthreads();
   uint32_t o = s_base + s_cnt[threadIdx.x >> 6] + incl - n;
@@ -1136,7 +1127,7 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
 #pragma unroll
   for (uint32_t j = 0; j < 4u; ++j) {
     if ((keep >> j) & 1u) plist[o++] = t0 + 4u * threadIdx.x + j;
-    if ((drop >> j) & 1u) plist[f.P - 1u - od++] = t0 + 4u * threadIdx.x + j;
+    if (kCullListBoth && ((drop >> j) & 1u)) plist[f.P - 1u - od++] = t0 + 4u * threadIdx.x + j;
   }
 }
 // Path-major bounce 0 over the unculled pixel list (f.plist: nlist pixels x k samples): compacted

@@ -110,11 +110,11 @@ size_t seg_table_bytes() { return 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kW
 
 // device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
 // L shadow tasks of ts float4s
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + 2 * kHitBytes + 16 + (uint64_t)L * ts * 16; }
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + kHrecQueueMult * kHitBytes + 16 + (uint64_t)L * ts * 16; }
 // fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
 uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
   const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
-  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + 2 * recs * k_slack * kHitBytes;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + kHrecQueueMult * recs * k_slack * kHitBytes;
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
@@ -1086,7 +1086,7 @@ int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
 
 int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
   if (!x) return SPTR_ERR_INVALID;
-  if (max_pieces == 0u) max_pieces = 16u;
+  if (max_pieces == 0u) max_pieces = 1u;
   if (max_pieces > 32u || (max_pieces & (max_pieces - 1u)))
     return fail(x->c, SPTR_ERR_INVALID, "split references: 0 (default 16) or a power of two up to 32");
   x->c.split_pieces = max_pieces;
@@ -1308,7 +1308,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
         pm = pm || bounce0_pixel_major(scene_view(c), probe) != 0u;
       }
       // hit-record segments hold twice the static shares (the bounce-0 work queues, k_trace_dyn's per-XCD queues)
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, 2u);
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, kHrecQueueMult);
       if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));

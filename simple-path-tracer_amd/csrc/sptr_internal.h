@@ -173,6 +173,21 @@ struct FrameView {
 };
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
 // the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
+// r04 work distribution (A/B builds; measured r04f, DESIGN.md §8: each slower or within noise, so off):
+// SPTR_PM_QUEUE, the pixel-major bounce 0 takes 64-pixel chunks from a queue in k_cull's order;
+// SPTR_SKY_LANES, k_sky runs lane groups over k_cull's culled list through per-XCD queues;
+// SPTR_TRACE_QUEUE, k_trace_dyn of scenes beyond an XCD's L2 takes work from per-XCD queues
+#ifndef SPTR_PM_QUEUE
+#define SPTR_PM_QUEUE 0
+#endif
+#ifndef SPTR_SKY_LANES
+#define SPTR_SKY_LANES 0
+#endif
+#ifndef SPTR_TRACE_QUEUE
+#define SPTR_TRACE_QUEUE 0
+#endif
+// hit-record segments hold twice the static shares when a producer takes work from a queue
+constexpr uint32_t kHrecQueueMult = (SPTR_PM_QUEUE || SPTR_TRACE_QUEUE) ? 2u : 1u;
 constexpr uint32_t kDynPmQueue = 32;   // a 128-B line of its own
 constexpr uint32_t kDynSkyQueue = 64;  // k_sky's per-XCD work queues, 32 words (128 B) apart
 constexpr size_t kDynBytes = 2048;
@@ -364,7 +379,7 @@ struct Context {
   uint32_t treelet_passes = SPTR_TREELET_PASSES;  // SAH treelet passes over L2/HBM scenes' LBVH (kernels_lbvh.hip)
   uint32_t num_nodes = 0, num_tris = 0, num_sph = 0, root = 0, bvh_depth = 0;
   uint32_t num_tri_refs = 0;     // triangle references = triangle slots (split references, kernels_lbvh.hip)
-  uint32_t split_pieces = 16;    // most references per split triangle (sptr_set_split_refs; 1 = no splits)
+  uint32_t split_pieces = 1;     // most references per split triangle (sptr_set_split_refs; 1 = no splits, the default)
   uint32_t num_nodes4 = 0, root4 = 0;
   uint32_t excluded_prims = 0;  // exactly degenerate triangles left out of the BVH (never hit; k_morton)
   uint32_t num_top4 = 0;  // wide nodes numbered first: the top kTopLevels levels
