@@ -265,7 +265,7 @@ struct StageTimer {
   bool trace_only;          // SPTR_FRAME_TIMING_TRACE alone: stages 1 and 5 only
   hipStream_t s;
   hipError_t err = hipSuccess;
-  const char* what = "";    // the call that set err
+  std::string what;         // the call that set err
   size_t open = SIZE_MAX;   // index in c.marks of the stage being recorded
   size_t call = SIZE_MAX;   // index in c.marks of this call's stage-0 span
   size_t alloc() {  // a pool event for this call (not recorded)
@@ -273,25 +273,27 @@ struct StageTimer {
       hipEvent_t e = nullptr;
       const hipError_t r = hipEventCreate(&e);
       if (r != hipSuccess) {
-        if (err == hipSuccess) err = r;
+        if (err == hipSuccess) {
+          err = r;
+          what = "stage event create";
+        }
         return SIZE_MAX;
       }
       c.events.push_back(e);
     }
     return c.events_used++;
   }
-  bool capturing = false;  // inside a graph capture: record as external event nodes (run_call)
+  bool capturing = false;  // inside a graph capture: no stage events (run_call), the streams are the cap_* ones
   size_t next() {
     const size_t i = alloc();
-    if (i != SIZE_MAX && err == hipSuccess)
-    {
-      err = capturing ? hipEventRecordWithFlags(c.events[i], s, hipEventRecordExternal) : hipEventRecord(c.events[i], s);
-      if (err != hipSuccess) what = capturing ? "stage event record (external)" : "stage event record";
+    if (i != SIZE_MAX && err == hipSuccess) {
+      err = hipEventRecord(c.events[i], s);
+      if (err != hipSuccess) what = "stage event record";
     }
     return i;
   }
   void begin(int stage) {
-    if (!on || (trace_only && stage != 1 && stage != 5 && stage != 3 && stage != 8)) return;
+    if (!on || capturing || (trace_only && stage != 1 && stage != 5 && stage != 3 && stage != 8)) return;
     open = c.marks.size();
     c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
@@ -300,11 +302,14 @@ struct StageTimer {
     c.marks[open].e = next();
     open = SIZE_MAX;
   }
-  void begin_call() {
+  void begin_call() {  // (a replayed graph's call span is recorded around its launch: run_call)
+    if (capturing) return;
     call = c.marks.size();
     c.marks.push_back(StageMark{0, next(), SIZE_MAX});
   }
-  void end_call() { c.marks[call].e = next(); }
+  void end_call() {
+    if (call != SIZE_MAX) c.marks[call].e = next();
+  }
 };
 
 // Wait for the pending render calls, fold their device counters and stage events into *stats
@@ -781,42 +786,34 @@ void drop_graph(Context& c) {
 // Enqueue one render call's launch sequence on s.  A call shape seen twice in a row is captured
 // once into a hipGraph (on the context's capture stream) and replayed from then on: one graph
 // launch instead of ~20 kernel launches, with the per-call values (frame_begin, reset, total) passed
-// as the arguments of the graph's k_frame_dyn node and the timing events re-pointed at fresh pool
-// events per replay.  The launch sequence itself is the same code either way.
+// as the arguments of the graph's k_frame_dyn node.  The launch sequence itself is the same code
+// either way.  A replay's call span (stage 0) is recorded around its hipGraphLaunch; calls with stage
+// timing (SPTR_FRAME_TIMING*) always run as direct launches: a stage span inside a graph would need
+// external event-record nodes, which torch's HIP 7.0 runtime (the one bench.py and any process that
+// imports torch first binds libsptr_hip to) refuses inside a capture (hipErrorInvalidValue, r04g).
 template <class Enqueue>
 int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
              bool timing, bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
-  if (c.launch_mode != 0 || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+  if (c.launch_mode != 0 || timing || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
     StageTimer tm{c, timing, trace_only, s};
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
-    if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
+    if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + tm.what + ": " + hipGetErrorString(tm.err));
     return SPTR_OK;
   }
   if (!(c.graph.valid && same_key(key, c.graph.key))) {  // capture this shape
     drop_graph(c);
     GraphShape gshape;
-    const size_t m0 = c.marks.size(), e0 = c.events_used;
-    // the pool must not grow inside the capture (hipEventCreate is not a capturable call): every
-    // span of a call uses two events; 512 covers 255 spans (> 6 batches x 6 bounces x 3 stages)
-    while (c.events.size() < c.events_used + 512) {
-      hipEvent_t e = nullptr;
-      API_HIP(hipEventCreate(&e));
-      c.events.push_back(e);
-    }
     API_HIP(hipStreamBeginCapture(c.cap_stream, hipStreamCaptureModeThreadLocal));
-    StageTimer tm{c, timing, trace_only, c.cap_stream};
+    StageTimer tm{c, false, false, c.cap_stream};
     tm.capturing = true;
     const uint32_t nw = enqueue(c.cap_stream, tm);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(c.cap_stream, &g);
-    const std::vector<StageMark> cap_marks(c.marks.begin() + (std::ptrdiff_t)m0, c.marks.end());
-    c.marks.resize(m0);  // the capture executed nothing
-    c.events_used = e0;
     // every stream the capture forked must have left capture mode with it (a stream still capturing
     // would fold the next direct launches into a dead graph)
     for (hipStream_t st : {c.cap_stream, c.cap_side, c.cap_side2}) {
@@ -834,17 +831,17 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
       }
     }
     if (ec != hipSuccess || tm.err != hipSuccess || !g) {
-      // not capturable (e.g. more stage spans than the pre-grown event pool): direct launches
+      // not capturable: direct launches (graph_info reports why)
       c.capture_status = (int32_t)(ec != hipSuccess ? ec : (tm.err != hipSuccess ? tm.err : hipErrorUnknown));
       c.capture_error = ec != hipSuccess ? std::string("hipStreamEndCapture: ") + hipGetErrorString(ec)
-                                         : std::string(tm.what) + ": " + hipGetErrorString(tm.err);
+                                         : tm.what + ": " + hipGetErrorString(tm.err);
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
       StageTimer td{c, timing, trace_only, s};
       launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
       waves = enqueue(s, td);
       API_HIP(hipGetLastError());
-      if (td.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(td.err));
+      if (td.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + td.what + ": " + hipGetErrorString(td.err));
       return SPTR_OK;
     }
     GraphCache gc;
@@ -873,34 +870,6 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     for (hipGraphNode_t r : roots) API_HIP(hipGraphAddDependencies(g, &gc.dyn_node, &r, 1));
     gc.edges = gshape.edges + (uint32_t)nr;
     gc.dyn_params = kp;
-    // event-record nodes of the stage spans, matched through the pool events they recorded
-    size_t n = 0;
-    API_HIP(hipGraphGetNodes(g, nullptr, &n));
-    std::vector<hipGraphNode_t> nodes(n);
-    API_HIP(hipGraphGetNodes(g, nodes.data(), &n));
-    std::vector<std::pair<hipEvent_t, hipGraphNode_t>> ev_nodes;
-    for (hipGraphNode_t nd : nodes) {
-      hipGraphNodeType t;
-      API_HIP(hipGraphNodeGetType(nd, &t));
-      if (t != hipGraphNodeTypeEventRecord) continue;
-      hipEvent_t e = nullptr;
-      API_HIP(hipGraphEventRecordNodeGetEvent(nd, &e));
-      ev_nodes.emplace_back(e, nd);
-    }
-    auto node_of = [&](size_t ei) -> hipGraphNode_t {
-      for (auto& pr : ev_nodes)
-        if (ei < c.events.size() && pr.first == c.events[ei]) return pr.second;
-      return nullptr;
-    };
-    for (const StageMark& m : cap_marks) {
-      const GraphMark gm{m.stage, node_of(m.b), node_of(m.e)};
-      if (!gm.b || !gm.e) {
-        (void)hipGraphDestroy(g);
-        return fail(c, SPTR_ERR_HIP, "render: graph capture: stage event node not found (" +
-                                         std::to_string(ev_nodes.size()) + " event nodes)");
-      }
-      gc.marks.push_back(gm);
-    }
     const hipError_t ei = hipGraphInstantiate(&gc.exec, g, nullptr, nullptr, 0);
     if (ei != hipSuccess) {
       (void)hipGraphDestroy(g);
@@ -910,7 +879,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     c.graph = gc;
     ++c.captures;
   }
-  // replay: the call's values into the k_frame_dyn node, fresh pool events into the event nodes
+  // replay: the call's values into the k_frame_dyn node, the call span around the launch
   GraphCache& gc = c.graph;
   void* dyn_ptr = c.dyn.p;
   uint32_t a0 = frame_begin, a1 = reset, a2 = total;
@@ -920,16 +889,11 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   p.kernelParams = args;
   p.extra = nullptr;
   API_HIP(hipGraphExecKernelNodeSetParams(gc.exec, gc.dyn_node, &p));
-  StageTimer tm{c, true, false, s};
-  for (const GraphMark& m : gc.marks) {
-    const size_t b = tm.alloc(), e = tm.alloc();
-    if (b == SIZE_MAX || e == SIZE_MAX) break;
-    API_HIP(hipGraphExecEventRecordNodeSetEvent(gc.exec, m.b, c.events[b]));
-    API_HIP(hipGraphExecEventRecordNodeSetEvent(gc.exec, m.e, c.events[e]));
-    c.marks.push_back(StageMark{m.stage, b, e});
-  }
-  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("render: events: ") + hipGetErrorString(tm.err));
+  StageTimer tm{c, false, false, s};
+  tm.begin_call();
   API_HIP(hipGraphLaunch(gc.exec, s));
+  tm.end_call();
+  if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + tm.what + ": " + hipGetErrorString(tm.err));
   waves = gc.waves;
   return SPTR_OK;
 }

@@ -325,10 +325,6 @@ struct GraphKey {
   sptr_frame frame;
   uint32_t k, tail;
 };
-struct GraphMark {
-  int stage;
-  hipGraphNode_t b, e;  // event-record nodes of the stage span
-};
 struct GraphCache {
   bool valid = false;
   GraphKey key{};
@@ -336,7 +332,6 @@ struct GraphCache {
   hipGraphExec_t exec = nullptr;
   hipGraphNode_t dyn_node = nullptr;  // k_frame_dyn: its arguments are the per-call values
   hipKernelNodeParams dyn_params{};
-  std::vector<GraphMark> marks;  // stage spans in recording order (re-pointed at fresh events per replay)
   uint32_t waves = 0;
   // shape of the captured graph (check_graph): nodes, dependency edges, nodes on the longest path
   uint32_t nodes = 0, edges = 0, depth = 0;

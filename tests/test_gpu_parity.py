@@ -405,9 +405,10 @@ def test_wave_fold_vs_oracle(renderer):
 @pytest.mark.parametrize("integrator", [0, 1, 2])
 def test_launch_graph_replay_equals_direct(renderer, integrator):
     """Repeated call shapes are captured into a hipGraph and replayed (sptr_set_launch_mode 0): the
-    accumulation, the stats and the stage timings must match direct launches call for call —
-    including progressive continuation (the per-call frame index is a graph-node argument), a
-    camera change (new shape: direct launches again) and asynchronous calls."""
+    accumulation and the stats must match direct launches call for call — including progressive
+    continuation (the per-call frame index is a graph-node argument), a camera change (new shape:
+    direct launches again, then a second capture) and asynchronous calls.  Calls with stage timing run
+    as direct launches in every mode (no capture)."""
     W, H = 96, 64
     sptr.setup_default(renderer, "default_emitter")
     cams = [sptr.camera_lookat(aspect=W / H), sptr.camera_lookat(pos=(0.5, 3.0, 8.0), aspect=W / H)]
@@ -415,11 +416,11 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
     try:
         for mode in (1, 0):
             renderer.set_launch_mode(mode)
+            g0 = renderer.graph_info()
             seq = []
             for cam in (cams[0], cams[0], cams[0], cams[1], cams[1], cams[1]):
                 fb = 1 if not seq or seq[-1][3] is not cam else seq[-1][4] + 2
-                st = renderer.render(cam, W, H, spp=2, frame_begin=fb, integrator=integrator,
-                                     flags=sptr.SPTR_FRAME_TIMING_TRACE)
+                st = renderer.render(cam, W, H, spp=2, frame_begin=fb, integrator=integrator)
                 seq.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, cam, fb, st.ms_total))
             for fb in (1, 3, 5):  # asynchronous replays, one collection
                 renderer.render(cams[0], W, H, spp=2, frame_begin=fb, integrator=integrator,
@@ -427,6 +428,17 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
             st = renderer.collect_stats()
             seq.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, None, 0, st.ms_total))
             out[mode] = seq
+            g = renderer.graph_info()
+            if mode == 0:  # one capture per camera, the asynchronous calls replay the first camera's again
+                assert g["valid"] == 1 and g["captures"] == g0["captures"] + 3, (g0, g)
+            else:
+                assert g["captures"] == g0["captures"], (g0, g)
+        # stage timing: direct launches however often the shape repeats
+        g0 = renderer.graph_info()
+        for _ in range(3):
+            st = renderer.render(cams[0], W, H, spp=2, integrator=integrator, flags=sptr.SPTR_FRAME_TIMING_TRACE)
+            assert st.ms_trace + st.ms_trace0 > 0.0
+        assert renderer.graph_info()["captures"] == g0["captures"]
     finally:
         renderer.set_launch_mode(0)
     for a, b in zip(out[1], out[0]):
