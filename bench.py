@@ -431,9 +431,9 @@ def main():
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
     ap.add_argument("--split-refs", type=int, default=0, help="most references per split triangle (0 = library default, 1 = none)")
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
-    ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2],
-                    help="0: replay captured launch graphs (default); 1: direct launches; 2: direct launches on one "
-                         "stream, no overlap (timing studies)")
+    ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="0: replay captured launch graphs where they pay (default); 1: direct launches; 2: direct "
+                         "launches on one stream, no overlap (timing studies); 3: graphs for every repeated shape")
     ap.add_argument("--no-serial-pass", action="store_true",
                     help="skip the untimed one-stream pass (launch mode 2) that times the trace / shadow launches "
                          "alone for scenes whose launches overlap")
@@ -587,12 +587,13 @@ def main():
         stats_serial = [r.collect_stats()]
         r.set_launch_mode(0)
 
-    # untimed pass of the same steps without stage events: the call shape is captured into a launch
-    # graph on its second call and replayed from then on (stage spans inside a graph would need
+    # untimed pass of the same steps without stage events, launch mode 3: the call shape is captured
+    # into a launch graph on its second call and replayed from then on (stage spans inside a graph would need
     # external event-record nodes, which torch's HIP 7.0 runtime refuses inside a capture: calls with
     # stage timing, like the timed steps above, run as direct launches)
     graph_replay = None
     if world == 1 and args.launch_mode == 0 and args.integrator == "wavefront" and not args.no_serial_pass:
+        r.set_launch_mode(3)  # (mode 0 launches a large call with side-stream launches directly)
         for _ in range(2):
             step(sptr.SPTR_FRAME_RECULL)
         r.collect_stats()
@@ -604,6 +605,7 @@ def main():
         graph_elapsed = time.perf_counter() - tg0
         gst = r.collect_stats()
         g = r.graph_info()
+        r.set_launch_mode(0)
         graph_replay = {"ms_per_step": round(graph_elapsed / args.steps * 1e3, 3),
                         "mrays_per_s": round((gst.rays_closest + gst.rays_shadow) / graph_elapsed / 1e6, 2),
                         "graph": {k: g[k] for k in ("valid", "nodes", "edges", "depth", "captures")},

@@ -224,9 +224,13 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
- * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument;
+ * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument —
+ * except a call of more than 2^22 samples whose launches fork to the side streams (the graph executor
+ * runs a graph's branches one after another: such calls launch directly);
  * 1: direct kernel launches for every call; 2: direct launches, all on the render stream (no launch
- * overlapped on the context's second stream).  Results are identical in every mode. */
+ * overlapped on the context's second stream); 3: as 0 for every repeated shape, whatever its size.
+ * Calls with stage timing (SPTR_FRAME_TIMING*) launch directly in every mode.  Results are identical
+ * in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
 /* The launch graph the context holds (launch mode 0): valid = 1 once a call shape was captured; its
  * node count, dependency edges and the nodes on its longest path; captures = graphs captured so far;

@@ -557,6 +557,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     }
   };
   auto fork_to = [&](hipStream_t side) {  // side's next launches start after everything enqueued on s so far
+    if (!cap) c.last_forked = true;
     check(hipEventRecord(ev.fork, s), "shadow fork record");
     check(hipStreamWaitEvent(side, ev.fork, 0), "shadow fork wait");
   };
@@ -628,7 +629,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       // words, which nothing reads before this batch's k_accum, the join point): its VALU-bound blocks
       // fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.  Enqueued
       // after the trace, so that the trace's grid is dispatched first.
-      if (sky_side) check(hipEventRecord(ev.fork, s), "sky fork record");
+      if (sky_side) {
+        if (!cap) c.last_forked = true;
+        check(hipEventRecord(ev.fork, s), "sky fork record");
+      }
       tm.begin(d == 0 ? 5 : 1);
       const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
       tm.end();
@@ -792,12 +796,18 @@ void drop_graph(Context& c) {
 // external event-record nodes, which torch's HIP 7.0 runtime (the one bench.py and any process that
 // imports torch first binds libsptr_hip to) refuses inside a capture (hipErrorInvalidValue, r04g).
 template <class Enqueue>
-int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
+int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, uint64_t samples, uint32_t* clear,
              bool timing, bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
-  if (c.launch_mode != 0 || timing || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+  // mode 0 captures a call whose direct launches forked nothing, or a small one (launch-bound): the
+  // runtime's graph executor does not run a graph's parallel branches concurrently, so a large call
+  // with side-stream launches replays slower than it launches directly (r04h: C5 8.70 vs 8.18 ms,
+  // C3 3.80 vs 3.75; C2, which forks nothing, 3.07 vs 3.10).  Mode 3 captures every repeated shape.
+  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && (!c.last_forked || samples <= kGraphForkedMaxSamples));
+  if (!graphable || timing || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+    c.last_forked = false;  // (set by the launch sequence if it forks)
     StageTimer tm{c, timing, trace_only, s};
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
@@ -1239,7 +1249,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   if (f->integrator != SPTR_INTEGRATOR_WAVEFRONT) {
     if (c.pending == 0) API_HIP(hipMemsetAsync(c.w_tot.p, 0, kTotWords * 8, s));
     const uint32_t spf = f->integrator == SPTR_INTEGRATOR_PATHTRACER ? (f->samples_per_frame ? f->samples_per_frame : 4u) : 1u;
-    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, nullptr, timing || trace_timing, false, s,
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, (uint64_t)frame_view(c, *f).valid * f->spp, nullptr,
+                  timing || trace_timing, false, s,
                   [&](hipStream_t cs, StageTimer& tm) { return enqueue_path_per_thread(c, *f, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
     samples = (uint64_t)frame_view(c, *f).valid * f->spp * spf;
@@ -1285,7 +1296,8 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     // an in-sequence cull (SPTR_FRAME_RECULL) counts its unculled pixels from zero: k_frame_dyn clears it
     uint32_t* clear = ((f->flags & SPTR_FRAME_RECULL) && !(f->flags & SPTR_FRAME_NO_CULL))
                           ? static_cast<uint32_t*>(c.plist.p) + c.P : nullptr;
-    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, clear, timing || trace_timing, !timing, s,
+    rc = run_call(c, key, f->frame_begin, reset ? 1u : 0u, total, (uint64_t)frame_view(c, *f).valid * f->spp, clear,
+                  timing || trace_timing, !timing, s,
                   [&](hipStream_t cs, StageTimer& tm) { return enqueue_wavefront(c, *f, k, T, cs, tm); }, waves);
     if (rc != SPTR_OK) return rc;
     if (clear) {  // the sequence just enqueued computes this camera's mask (keyed only once enqueued)
@@ -1371,7 +1383,9 @@ int sptr_overlap_probe(sptr_ctx* x, double* ms) {
 
 int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
   if (!x) return SPTR_ERR_INVALID;
-  if (mode > 2) return fail(x->c, SPTR_ERR_INVALID, "launch mode must be 0 (graphs), 1 (direct) or 2 (direct, one stream)");
+  if (mode > 3)
+    return fail(x->c, SPTR_ERR_INVALID,
+                "launch mode must be 0 (graphs where they pay), 1 (direct), 2 (direct, one stream) or 3 (graphs)");
   x->c.launch_mode = mode;
   return SPTR_OK;
 }

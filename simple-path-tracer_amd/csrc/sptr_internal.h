@@ -191,6 +191,7 @@ constexpr uint32_t kHrecQueueMult = (SPTR_PM_QUEUE || SPTR_TRACE_QUEUE) ? 2u : 1
 constexpr uint32_t kDynPmQueue = 32;   // a 128-B line of its own
 constexpr uint32_t kDynSkyQueue = 64;  // k_sky's per-XCD work queues, 32 words (128 B) apart
 constexpr size_t kDynBytes = 2048;
+constexpr uint64_t kGraphForkedMaxSamples = 1ull << 22;  // run_call: graphs for forked calls up to this size
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
 // rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each
@@ -353,7 +354,10 @@ struct Context {
     hipEvent_t fork = nullptr, join = nullptr, sky = nullptr;
   } dev[2];
   int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
-  uint32_t launch_mode = 0;          // 0: replay a captured graph for repeated call shapes; 1: direct launches
+  // 0: replay a captured graph for repeated call shapes (large calls with side-stream launches
+  // excepted, run_call); 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
+  uint32_t launch_mode = 0;
+  bool last_forked = false;          // the last direct launch sequence forked launches to a side stream
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
   GraphCache graph;

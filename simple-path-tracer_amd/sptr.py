@@ -418,8 +418,9 @@ class Renderer:
                 "side_has_own_queue": bool(ms[1] < 0.75 * ms[0]), "sky_side_has_own_queue": bool(ms[2] < 0.75 * ms[0])}
 
     def set_launch_mode(self, mode: int):
-        """0: replay captured launch graphs for repeated call shapes (default); 1: direct launches;
-        2: direct launches, all on the render stream (no overlap)."""
+        """0: replay captured launch graphs for repeated call shapes (default; large calls with
+        side-stream launches excepted); 1: direct launches; 2: direct launches, all on the render
+        stream (no overlap); 3: launch graphs for every repeated shape."""
         self._check(self._L.sptr_set_launch_mode(self._h, mode), "set_launch_mode")
 
     def set_tail_depth(self, n: int):

@@ -292,17 +292,21 @@ def test_c5_render_vs_oracle(renderer, c5_scene):
 # ------------------------------------------------------------------- full-size timed configurations
 def _render_as_bench(renderer, cam, W, H, S):
     """The timed call shape of bench.py (in-step cull, SPTR_FRAME_RECULL) three times: direct launches,
-    then the captured graph (second call of the shape), then its replay.  All three must be identical;
+    then the captured graph (second call of the shape, launch mode 3), then its replay.  All three must be identical;
     the replay's image is returned."""
     runs = []
-    for _ in range(3):
-        st = renderer.render(cam, W, H, spp=S, flags=sptr.SPTR_FRAME_RECULL)
-        runs.append((st, renderer.read_rgb8().copy(), renderer.read_accum().copy()))
+    try:
+        renderer.set_launch_mode(3)  # (mode 0 launches a large call with side-stream launches directly)
+        for _ in range(3):
+            st = renderer.render(cam, W, H, spp=S, flags=sptr.SPTR_FRAME_RECULL)
+            runs.append((st, renderer.read_rgb8().copy(), renderer.read_accum().copy()))
+        g = renderer.graph_info()
+    finally:
+        renderer.set_launch_mode(0)
     for st, rgb, acc in runs[1:]:
         assert np.array_equal(rgb, runs[0][1])
         assert np.array_equal(acc.view(np.uint32), runs[0][2].view(np.uint32))
         assert (st.rays_closest, st.rays_shadow) == (runs[0][0].rays_closest, runs[0][0].rays_shadow)
-    g = renderer.graph_info()
     assert g["valid"] == 1, g
     return runs[-1]
 
