@@ -115,7 +115,14 @@ def _counter_fracs(wl_name, kernel, avg_launch_s, stream_read_per_launch):
             "salu_per_valu": round(salu / valu, 3) if salu and valu else None, "valu_source": sq_src}
 
 
-def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
+def env_hbm_bytes(lookups, env_bytes, launches):
+    """HBM bytes of cubemap lookups (4 texels, ENV_TEXEL_BYTES each): the faces (6 x size^2 float4, 25 MB
+    at 512^2) stay in the 256 MB MALL, so a launch reads them from HBM at most once per XCD, as an
+    L2-resident scene (_residency)."""
+    return min(ENV_TEXEL_BYTES * lookups, XCDS * env_bytes * launches) if env_bytes else 0.0
+
+
+def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     """Roofline of the dominant kernel, k_trace (all its launches: bounce 0 and the wavefront bounces
     before the path-per-thread tail; one template).
 
@@ -154,9 +161,9 @@ def roofline(cnt, stats, layout, wl_name, steps, cube_env=False):
     node_b = layout["node_bytes"] / max(1, layout["num_nodes"]) if layout["num_nodes"] else 64.0
     scene_p = node_b * pp[0] + 48.0 * pp[1] + 16.0 * pp[2]
     scene_b = node_b * pb[0] + 48.0 * pb[1] + 16.0 * pb[2]
-    env = ENV_TEXEL_BYTES if cube_env else 0.0
-    stream = (tp * (hp * HIT_RECORD_BYTES + (1.0 - hp) * (RAD_BYTES + env))
-              + tb * (RAY_READ_BYTES + hb * HIT_RECORD_BYTES + (1.0 - hb) * (THR_READ_BYTES + 2 * RAD_BYTES + env)))
+    stream = (tp * (hp * HIT_RECORD_BYTES + (1.0 - hp) * RAD_BYTES)
+              + tb * (RAY_READ_BYTES + hb * HIT_RECORD_BYTES + (1.0 - hb) * (THR_READ_BYTES + 2 * RAD_BYTES)))
+    stream += env_hbm_bytes(tp * (1.0 - hp) + tb * (1.0 - hb), env_bytes, launches)
     stream_read = tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))  # coalesced reads
     residency, footprint = _residency(layout)
     scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * tb}[residency]
@@ -242,7 +249,7 @@ SHADOW_TASK_WRITE_BYTES = 32.0  # a shadow task written by k_shade where the sha
 ACCUM_BYTES_PER_PIXEL = 32.0 + 7.0  # accum read-modify-write; resolved RGBA8 tile + RGB8 image written
 
 
-def step_roofline(cnt, stats, steps, ms_per_step, trace, shadow, pixels, spp, cube_env=False):
+def step_roofline(cnt, stats, steps, ms_per_step, trace, shadow, pixels, spp, env_bytes=0):
     """Whole-step algorithmic HBM bytes over ms_per_step: every kernel of the step, not one launch.
       trace   the trace roofline's bytes per launch x its launches per step (traversed rays only)
       shadow  likewise for k_shadow(_dyn) (scenes whose shadow rays have launches of their own)
@@ -250,8 +257,9 @@ def step_roofline(cnt, stats, steps, ms_per_step, trace, shadow, pixels, spp, cu
               where shadow rays have launches of their own)
       tail    k_tail keeps path state in registers: only its closest-hit rays' node/primitive bytes, for
               HBM scenes (the bounce rays' per-ray scene bytes)
-      sky     culled camera samples: 4 cubemap texels (64 B) each with an HDR environment; the culled
-              pixels' accum read-modify-write (32 B)
+      sky     culled camera samples: 4 cubemap texels (64 B) each with an HDR environment, up to one
+              copy of the faces per XCD per k_sky launch (one per sample batch); the culled pixels'
+              accum read-modify-write (32 B)
       accum   ACCUM_BYTES_PER_PIXEL per pixel + the 16-B radiance read of every traversed camera path
     This is a model of the bytes the algorithm must move, priced at the HBM peak; the measured step is
     latency-bound, so frac is well below 1."""
@@ -267,7 +275,8 @@ def step_roofline(cnt, stats, steps, ms_per_step, trace, shadow, pixels, spp, cu
         "shadow": shadow["bytes_per_launch"] * shadow["launches_per_step"] if shadow else 0.0,
         "shade": hits * (SHADE_BYTES_PER_HIT + (SHADOW_TASK_WRITE_BYTES if shadow else 0.0)),
         "tail": tail_rays * trace.get("scene_hbm_bytes_per_bounce_ray", 0),
-        "sky": (samples - tp) * (ENV_TEXEL_BYTES if cube_env else 0.0) + (samples - tp) / max(1, spp) * 32.0,
+        "sky": env_hbm_bytes(samples - tp, env_bytes, sum(getattr(s, "waves", 1) for s in stats) / steps)
+               + (samples - tp) / max(1, spp) * 32.0,
         "accum": pixels * ACCUM_BYTES_PER_PIXEL + tp * RAD_BYTES,
     }
     total = sum(parts.values())
@@ -498,6 +507,7 @@ def main():
     probe = r.overlap_probe()
     flat = workloads.setup(r, wl)
     layout, info = r.scene_layout(), r.scene_info()
+    env_bytes = 6 * 512 * 512 * 16 if wl.hdr_env else 0  # workloads.hdr_env_faces(): 512^2 faces, float4 on the device
     cam = workloads.camera(wl)
     shards = args.emulate_shards if args.emulate_shards else world
     shard = 0 if args.emulate_shards else rank
@@ -661,7 +671,7 @@ def main():
             "world_size": world,
             "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
-            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, cube_env=wl.hdr_env),
+            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, env_bytes=env_bytes),
             "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
             "overlap_probe": probe,
             "stage_ms_per_step": stage_ms,
@@ -686,9 +696,9 @@ def main():
         if args.integrator == "wavefront":
             line["step_roofline"] = step_roofline(cnt, stats, args.steps, elapsed / args.steps * 1e3, line["roofline"],
                                                   line["shadow_roofline"], samples / max(1, args.steps) / wl.spp / world,
-                                                  wl.spp, cube_env=wl.hdr_env)
+                                                  wl.spp, env_bytes=env_bytes)
         if stats_serial:
-            rs = roofline(cnt, stats_serial, layout, wl.name, args.steps, cube_env=wl.hdr_env)
+            rs = roofline(cnt, stats_serial, layout, wl.name, args.steps, env_bytes=env_bytes)
             ss = shadow_roofline(cnt, stats_serial, layout, wl.name, args.steps)
             line["roofline_serial"] = {
                 "note": "untimed pass with every launch on one stream (launch mode 2): launch durations with nothing "

@@ -83,9 +83,13 @@ def test_lds_scene_charges_stream_only(bench):
     assert r["s8d_lds_frac"] == pytest.approx(s8d / 0.3e-3 / 1e9 / 150000.0, rel=1e-3)
     assert r["bytes_per_launch"] == pytest.approx(_stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25) / 6,
                                                   rel=1e-6)
-    c = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1, cube_env=True)
+    # a cubemap environment: 64 B per miss, up to one copy of the faces per XCD per launch
+    c = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1, env_bytes=1 << 30)
     assert c["bytes_per_launch"] == pytest.approx(
         _stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25, env=64.0) / 6, rel=1e-6)
+    d = bench.roofline(CNT, [_step_stats(1)], LDS, "no_such_workload", 1, env_bytes=1000)
+    assert d["bytes_per_launch"] == pytest.approx(
+        _stream(CNT.traced_primary, CNT.traced_bounce, 0.4, 0.25) / 6 + 8 * 1000, rel=1e-6)
 
 
 def test_no_shadow_launches_no_entry(bench):
@@ -94,22 +98,31 @@ def test_no_shadow_launches_no_entry(bench):
     assert bench.shadow_roofline(CNT, [st], HBM, "no_such_workload", 1) is None
 
 
-@pytest.mark.parametrize("tag,wl", [("r03za", "c2"), ("r03za", "c4"), ("r03zf", "c3"), ("r03zf", "c5")])
+@pytest.mark.parametrize("tag,wl", [("r03za", "c2"), ("r03za", "c4"), ("r03zf", "c3"), ("r03zf", "c5"),
+                                    ("r04p", "c2"), ("r04p", "c4"), ("r04p", "c5")])
 def test_committed_lines_recompute_from_kernel_stats(tag, wl):
     """Each committed bench line's roofline fraction recomputes from the rocprofv3 kernel statistics of
     the same session (tools/recompute_roofline.py: the timed-path instantiations pooled over their
     launches): within 5 % for LDS scenes; within 10 % where the library overlaps launches on a second
-    stream (C3, C5), whose durations depend on what ran beside them in each run."""
+    stream (C3, C5), whose durations depend on what ran beside them in each run.  From r04 on, the
+    overlapped lines carry roofline_serial (the one-stream pass, recomputed from its own kernel
+    statistics), and the overlapped shadow span, which includes the time its launch waits for CUs the
+    trace holds, is not compared."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     spec = importlib.util.spec_from_file_location("recompute_roofline", os.path.join(root, "tools", "recompute_roofline.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    serial = os.path.join(root, "profiles", f"{tag}_kernel_stats_{wl}_serial.csv")
     out = mod.recompute(os.path.join(root, "profiles", f"{tag}_bench_{wl}.json"),
-                        os.path.join(root, "profiles", f"{tag}_kernel_stats_{wl}.csv"))
+                        os.path.join(root, "profiles", f"{tag}_kernel_stats_{wl}.csv"),
+                        serial if os.path.exists(serial) else None)
     tol = 0.05 if wl in ("c2", "c4") else 0.10
     assert "roofline" in out
+    if tag >= "r04" and wl in ("c3", "c5"):
+        assert "roofline_serial.trace" in out and "roofline_serial.shadow" in out
+        out.pop("shadow_roofline")
     for key, r in out.items():
-        assert r["stats_launches"] > 0, key
+        assert key == "step_roofline" or r["stats_launches"] > 0, key
         assert r["rel_diff"] <= tol, (key, r)
 
 
@@ -117,17 +130,18 @@ def _full_stats(steps, tail=3_000_000, samples=40_000_000):
     st = _step_stats(steps)
     st.rays_tail = tail * steps
     st.samples = samples * steps
+    st.waves = 2 * steps
     return st
 
 
-@pytest.mark.parametrize("layout,cube", [(HBM, False), (LDS, True)], ids=["hbm", "lds-cube"])
-def test_step_roofline_components(bench, layout, cube):
+@pytest.mark.parametrize("layout,env", [(HBM, 0), (LDS, 1 << 30), (LDS, 25 << 20)], ids=["hbm", "lds-cube", "lds-cube-mall"])
+def test_step_roofline_components(bench, layout, env):
     """step_roofline: every kernel's modelled bytes per step over the step time; independent of the
     number of timed steps; components as DESIGN.md §4 states them."""
-    rf = bench.roofline(CNT, [_step_stats(4)], layout, "no_such_workload", 4, cube_env=cube)
+    rf = bench.roofline(CNT, [_step_stats(4)], layout, "no_such_workload", 4, env_bytes=env)
     sh = bench.shadow_roofline(CNT, [_step_stats(4)], layout, "no_such_workload", 4)
-    a = bench.step_roofline(CNT, [_full_stats(4)], 4, 3.0, rf, sh, 2_000_000, 16, cube_env=cube)
-    b = bench.step_roofline(CNT, [_full_stats(1)], 1, 3.0, rf, sh, 2_000_000, 16, cube_env=cube)
+    a = bench.step_roofline(CNT, [_full_stats(4)], 4, 3.0, rf, sh, 2_000_000, 16, env_bytes=env)
+    b = bench.step_roofline(CNT, [_full_stats(1)], 1, 3.0, rf, sh, 2_000_000, 16, env_bytes=env)
     assert a == b
     parts = a["bytes_by_kernel"]
     assert sum(parts.values()) == pytest.approx(a["bytes_per_step"], abs=len(parts))
@@ -136,7 +150,8 @@ def test_step_roofline_components(bench, layout, cube):
     hits = 10_000_000 * 0.4 + 28_000_000 * 0.25
     assert parts["shade"] == pytest.approx(hits * (140.0 + 32.0), rel=1e-6)
     culled = 40_000_000 - 10_000_000
-    assert parts["sky"] == pytest.approx(culled * (64.0 if cube else 0.0) + culled / 16 * 32.0, rel=1e-6)
+    texels = min(64.0 * culled, 8 * env * 2)  # two k_sky launches (sample batches) per step
+    assert parts["sky"] == pytest.approx(texels + culled / 16 * 32.0, rel=1e-6)
     assert parts["accum"] == pytest.approx(2_000_000 * 39.0 + 10_000_000 * 16.0, rel=1e-6)
     if layout is HBM:
         assert parts["tail"] == pytest.approx(3_000_000 * rf["scene_hbm_bytes_per_bounce_ray"], rel=1e-6)
