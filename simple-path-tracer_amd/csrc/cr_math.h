@@ -62,11 +62,19 @@ __device__ __forceinline__ float inv_len_nrm(float l2) { return rcp_nrm(sqrt_nrm
 // 1 + ceil(j/2) 2^-23.  The neglected second-order terms stay below a quarter ulp for |d| < 2900;
 // checked against 1.0f / sqrtf over the whole window on the CPU (tests/test_cr_math_cpu.py) and on
 // the GPU (tests/hip/crmath_check.hip).  Other l2 take the general sequence.
+// inv_len_unit_cf: the closed form alone, both signs of d evaluated and selected (no divergent
+// branch), for l2 of a vector that came out of a normalization (|d| a few ulps), where inv_len_unit's
+// range test cannot fail.  On the bits b of l2 (0x3F800000 is even): d >= 0 gives 0x7F000000 -
+// (b & ~1); d < 0 gives 0x3F800000 + ceil(-d / 4) = 0x3F800000 + ((0x3F800003 - b) >> 2).
+__device__ __forceinline__ float inv_len_unit_cf(float l2) {
+  const uint32_t b = __float_as_uint(l2);
+  const uint32_t up = 0x7F000000u - (b & ~1u), dn = 0x3F800000u + ((0x3F800003u - b) >> 2);
+  return __uint_as_float((int)b >= 0x3F800000 ? up : dn);
+}
 __device__ __forceinline__ float inv_len_unit(float l2) {
   const int d = (int)__float_as_uint(l2) - 0x3F800000;
   if (__builtin_expect(d < -1024 || d > 1024, 0)) return inv_len_nrm(l2);
-  const int u = d >= 0 ? -(d & ~1) : (((-d + 1) >> 1) + 1) >> 1;
-  return __int_as_float(0x3F800000 + u);
+  return inv_len_unit_cf(l2);
 }
 
 // 1 / sqrt(l2) for every float l2 (bit-identical to 1.0f / sqrtf(l2), checked over all 2^32 inputs by

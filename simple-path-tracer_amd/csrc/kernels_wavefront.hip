@@ -950,7 +950,7 @@ __device__ __forceinline__ void primary_at(const FrameView& f, const ImageDiv& d
   const float jx = rand01(r);
   const float jy = rand01(r);
   const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, dv.w), div_nrm(float(y) + jy, dv.h));
-  out.d = safe_renormalize_dir(dir);
+  out.d = renormalized_again(dir);  // dir: camera_dir normalized it
   out.rng = wang_hash((ps ^ acc) ^ 1u);
 }
 __device__ __forceinline__ bool primary_path(const FrameView& f, const ImageDiv& dv, uint32_t p, Primary& out,
@@ -1203,17 +1203,23 @@ __device__ __forceinline__ vec3 cube_texel(const float4* env, int S, int face, i
 template <bool kCube>
 __device__ __forceinline__ vec3 env_color(const EnvView& sh, vec3 dir) {
   if (!kCube) return sky_color(dir);
-  const vec3 d = renormalize_dir(dir);
+  const vec3 d = renormalized_again(dir);  // every caller passes a normalized direction
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-  // Cubemap::directionToUV's face cases as selects (no divergent branches): x-major, else y-major,
-  // else z-major, in the reference's order of tests
-  const bool xm = ax >= ay && ax >= az;
-  const bool ym = !xm && ay >= ax && ay >= az;
-  const float ma = xm ? ax : (ym ? ay : az);
-  const bool pos = xm ? d.x > 0.0f : (ym ? d.y > 0.0f : d.z > 0.0f);
+  // Cubemap::directionToUV's face cases as selects: x-major, else y-major, else z-major, in the
+  // reference's order of tests.  The conditions are combined with & (no short-circuit, which the
+  // compiler turned into divergent branches), and the cases share their operands: the major component
+  // dmaj (face sign, ma = |dmaj|), the u component (d.z on x faces, else d.x) and the v component (d.z on
+  // y faces, else d.y), each negated by a sign-bit flip as the face's case says.
+  const bool xm = (ax >= ay) & (ax >= az);
+  const bool ym = !xm & (ay >= ax) & (ay >= az);
+  const float dmaj = xm ? d.x : (ym ? d.y : d.z);
+  const float ma = fabsf(dmaj);
+  const bool pos = dmaj > 0.0f;
   const int face = (xm ? 0 : (ym ? 2 : 4)) + (pos ? 0 : 1);
-  const float uc = xm ? (pos ? -d.z : d.z) : (ym ? d.x : (pos ? d.x : -d.x));
-  const float vc = xm ? -d.y : (ym ? (pos ? d.z : -d.z) : -d.y);
+  const bool uneg = xm ? pos : (!ym & !pos);  // x: pos ? -d.z : d.z; y: d.x; z: pos ? d.x : -d.x
+  const bool vneg = !ym | !pos;               // x, z: -d.y; y: pos ? d.z : -d.z
+  const float uc = __uint_as_float(__float_as_uint(xm ? d.z : d.x) ^ (uneg ? 0x80000000u : 0u));
+  const float vc = __uint_as_float(__float_as_uint(ym ? d.z : d.y) ^ (vneg ? 0x80000000u : 0u));
   // uc / ma and vc / ma share the divisor (ma in [1/sqrt(3), 1]): correctly rounded for |uc| >=
   // 2^-100 (cr_math.h div_nrm, checked by tests/hip/crmath_check.hip); below that the quotient is
   // under 2^-99 either way and q + 1 rounds to 1 exactly
@@ -1363,7 +1369,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
         if (!hit) {
           vec3 rv = v3(0.0f, 0.0f, 0.0f);
           if (sh.debug_mode != 1) {
-            const vec3 e = (ablate(f) & 1u) ? pr.d : env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+            const vec3 e = (ablate(f) & 1u) ? pr.d : env_color<kCube>(sh, renormalized_again(pr.d));
             rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           }
           if (!fold) w.rad[p] = f4(rv, 0.0f);
@@ -1478,7 +1484,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_W
           hit = traverse_w<kW4, false, kCount>(sc, sv, r, 0.0f, tfar, ref, vc, s_stack);
           if (kCount) hist_ray(s_hist, vc.nodes - v0);
         }
-        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+        if (!hit && sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, renormalized_again(pr.d));
       }
       // this pixel group's hits of the round -> number of leading misses still to fold
       const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
@@ -1589,7 +1595,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         if (sh.debug_mode == 1) {
           w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = (ablate(f) & 1u) ? d : env_color<kCube>(sh, safe_renormalize_dir(d));
+          const vec3 e = (ablate(f) & 1u) ? d : env_color<kCube>(sh, renormalized_again(d));
           vec3 rv;
           if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
           else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -1835,11 +1841,11 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     const bool defer = !kPrimary && w.defer_miss != 0u;
     if (fin && !wk.hit) {
       if (defer) {  // the miss record's slot carries thr * env (k_shade adds it to rad[pid])
-        if (sh.debug_mode != 1) rs.thr[id] = f4(xyz(rs.thr[id]) * env_color<kCube>(sh, safe_renormalize_dir(r.d)), 0.0f);
+        if (sh.debug_mode != 1) rs.thr[id] = f4(xyz(rs.thr[id]) * env_color<kCube>(sh, renormalized_again(r.d)), 0.0f);
       } else if (sh.debug_mode == 1) {
         w.rad[pid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       } else {
-        const vec3 e = env_color<kCube>(sh, safe_renormalize_dir(r.d));
+        const vec3 e = env_color<kCube>(sh, renormalized_again(r.d));
         vec3 rv;
         if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
         else rv = xyz(w.rad[pid]) + xyz(rs.thr[id]) * e;
@@ -2234,7 +2240,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
         if (sh.debug_mode == 1) {
           w.rad[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         } else {
-          const vec3 e = env_color<kCube>(sh.env, safe_renormalize_dir(rd));
+          const vec3 e = env_color<kCube>(sh.env, renormalized_again(rd));
           w.rad[p] = f4(xyz(w.rad[p]) + thr * e, 0.0f);
         }
       } else if (sh.debug_mode == 1) {
@@ -2505,7 +2511,7 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
         loaded = true;
       }
       if (!hit) {
-        radv = radv + thr * env_color<kCube>(sh.env, safe_renormalize_dir(rd));
+        radv = radv + thr * env_color<kCube>(sh.env, renormalized_again(rd));
         break;
       }
       const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
@@ -2606,7 +2612,7 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
         if (valid && smp < f.k && sh.debug_mode != 1) {
           Primary pr;
           primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
-          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, renormalized_again(pr.d));
         }
         const uint32_t nact = min(kLanes, f.k - r * kLanes);
 #pragma unroll
@@ -2630,7 +2636,7 @@ __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
         Primary pr;
         primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
         vec3 rv = v3(0.0f, 0.0f, 0.0f);
-        if (sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, safe_renormalize_dir(pr.d));
+        if (sh.debug_mode != 1) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, renormalized_again(pr.d));
         return rv;
       };
       // kSkyIlp independent samples (their environment fetches in flight together), then their adds
@@ -3289,7 +3295,7 @@ __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, ui
     const float jx = rand01(r);
     const float jy = rand01(r);
     const vec3 dir = camera_dir(f, div_nrm(float(x) + jx, idiv.w), div_nrm(float(y) + jy, idiv.h));  // as primary_path
-    const vec3 d = safe_renormalize_dir(dir);
+    const vec3 d = renormalized_again(dir);
     dirs[(size_t)i * 3 + 0] = d.x;
     dirs[(size_t)i * 3 + 1] = d.y;
     dirs[(size_t)i * 3 + 2] = d.z;

@@ -58,10 +58,12 @@ inline float sq_root(float x) { return std::sqrt(x); }
 __device__ __forceinline__ float inv_length(float l2) { return inv_len(l2); }
 __device__ __forceinline__ float inv_length_dir(float l2) { return inv_len_nrm(l2); }
 __device__ __forceinline__ float inv_length_unit(float l2) { return inv_len_unit(l2); }
+__device__ __forceinline__ float inv_length_renorm(float l2) { return inv_len_unit_cf(l2); }
 #else
 SPTR_HD float inv_length(float l2) { return 1.0f / sq_root(l2); }
 SPTR_HD float inv_length_dir(float l2) { return 1.0f / sq_root(l2); }
 SPTR_HD float inv_length_unit(float l2) { return 1.0f / sq_root(l2); }
+SPTR_HD float inv_length_renorm(float l2) { return 1.0f / sq_root(l2); }
 #endif
 SPTR_HD vec3 normalize(vec3 v) { return v * inv_length(dot(v, v)); }
 SPTR_HD vec3 safe_normalize(vec3 v) {
@@ -87,6 +89,11 @@ SPTR_HD vec3 safe_renormalize_dir(vec3 v) {
   if (l2 <= 0.0f) return v3(0.0f, 0.0f, 0.0f);
   return v * inv_length_unit(l2);
 }
+// The same result again for the output of a normalization (normalize_dir, renormalize_dir,
+// renormalized_again): its squared length lies within a few ulps of 1, never 0, so neither the zero
+// test of safe_renormalize_dir nor inv_len_unit's range test can fire, and the device evaluates the
+// closed form with no branch.  (A NaN vector stays NaN: its l2 gives a NaN scale.)
+SPTR_HD vec3 renormalized_again(vec3 v) { return v * inv_length_renorm(dot(v, v)); }
 
 // normalize(vec3(0.3, 0.6, -0.8)), the sun direction of EnvironmentManager::getSkyColor
 // (src/EnvironmentManager.cpp:48), evaluated once in glm's order; tests/cpp/test_index_math.cpp checks

@@ -37,7 +37,8 @@ __global__ void k_rcp(uint32_t lo, uint32_t hi) {
     const float ref = 1.0f / y;
     const uint32_t il = __float_as_uint(1.0f / sqrtf(y));
     if (__float_as_uint(rcp_nrm(y)) != __float_as_uint(ref) || __float_as_uint(inv_len_nrm(y)) != il ||
-        __float_as_uint(inv_len_unit(y)) != il) {
+        __float_as_uint(inv_len_unit(y)) != il ||
+        ((__float_as_uint(y) + 1024u - 0x3F800000u) <= 2048u && __float_as_uint(inv_len_unit_cf(y)) != il)) {
       atomicAdd(&g_bad[1], 1ull);
       atomicMin(&g_first[1], (uint32_t)u);
     }

@@ -16,3 +16,6 @@ for wl in c5 c3 c2; do
   timeout -k 10 300 python3 bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-interactive > $out/bench_$wl.json 2> $out/bench_$wl.err || exit 3
   python3 -c "import json;d=json.loads(open('$out/bench_$wl.json').read().splitlines()[-1]);r=d['roofline'];print('$wl',d['ms_per_step'],d['value'],'trace',r['avg_launch_us'],r['frac'],'hist',r.get('visit_hist_log2'),'serial',json.dumps(d.get('roofline_serial')),'step',d.get('step_roofline',{}).get('frac'),'graph',d.get('graph_replay'),'stages',d['stage_ms_per_step'])"
 done
+# the 8-way C2 per-rank cost (one GPU rendering shard 0 of 8): direct launches vs the graph replay pass
+timeout -k 10 300 python3 bench.py --workload c2 --emulate-shards 8 --steps 20 --warmup 3 --no-cpu-baseline --no-interactive > $out/bench_c2_g8.json 2> $out/bench_c2_g8.err || exit 4
+python3 -c "import json;d=json.loads(open('$out/bench_c2_g8.json').read().splitlines()[-1]);print('c2 g8',d['ms_per_step'],'render',d['render_ms'],'graph',d.get('graph_replay'),'stages',d['stage_ms_per_step'])"
