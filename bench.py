@@ -439,6 +439,8 @@ def main():
     ap.add_argument("--leaf-size", type=int, default=0)
     ap.add_argument("--bvh-width", type=int, default=0, choices=[0, 2, 4])
     ap.add_argument("--split-refs", type=int, default=0, help="most references per split triangle (0 = library default, 1 = none)")
+    ap.add_argument("--stragglers", type=int, default=-1,
+                    help="straggler hand-off lane threshold (-1 = library default, 0 = off; HBM scenes)")
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
     ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2, 3],
                     help="0: replay captured launch graphs where they pay (default); 1: direct launches; 2: direct "
@@ -498,6 +500,8 @@ def main():
         r.set_bvh_width(args.bvh_width)
     if args.split_refs:
         r.set_split_refs(args.split_refs)
+    if args.stragglers >= 0:
+        r.set_stragglers(args.stragglers)
     if args.tail_depth:
         r.set_tail_depth(args.tail_depth)
     if args.launch_mode:
@@ -650,6 +654,8 @@ def main():
             knobs["launch_mode"] = args.launch_mode
         if args.split_refs:
             knobs["split_refs"] = args.split_refs
+        if args.stragglers >= 0:
+            knobs["stragglers"] = args.stragglers
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),
@@ -678,6 +684,8 @@ def main():
             "cull_ms": round(sum(s.ms_cull for s in stats) / args.steps, 4),
             "cull_launches_per_step": sum(s.cull_launches for s in stats) / args.steps,
             "tail_rays_per_step": int(sum(s.rays_tail for s in stats) / args.steps),
+            # paths the bounce traces handed to the straggler kernel (sptr_set_stragglers)
+            "paths_handed_off_per_step": int(sum(s.paths_handed_off for s in stats) / args.steps),
             "rays_per_step": int(rays / args.steps),
             # queries answered without a traversal: the camera rays of frustum-culled pixels (all ranks)
             "culled_primary_per_step": int((samples - traced_p) / args.steps) if args.integrator == "wavefront" else 0,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 5
+#define SPTR_ABI_VERSION 6
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -195,6 +195,8 @@ typedef struct sptr_stats {
   uint64_t shadow_visit_hist[16];
   uint64_t hits_primary, hits_bounce; /* SPTR_FRAME_COUNT_VISITS: closest hits the trace kernels found
                                          (of traced_primary / traced_bounce) */
+  uint64_t paths_handed_off;          /* ABI 6: paths a bounce trace handed to the straggler kernel
+                                         (sptr_set_stragglers) */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */
@@ -222,6 +224,13 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
  * else a power of two up to 32; applies to the next sptr_upload_scene.  Results do not depend on it
  * (each reference tests the same triangle). */
 int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
+/* Straggler hand-off (ABI 6) for scenes traversed from HBM (a wide BVH beyond an XCD's L2): once a
+ * wave of a bounce trace has no rays left to start and at most `lanes` of its 64 lanes are still
+ * tracing, those rays are handed to a path-per-thread kernel beside the launch chain, which traces
+ * them again and finishes their paths, so the launch no longer lasts as long as its longest ray.
+ * 0 = off, 1..64 (default 8).  Results do not depend on it (each path makes the same operations in
+ * the same order wherever it runs); sptr_stats::paths_handed_off counts the paths. */
+int sptr_set_stragglers(sptr_ctx* ctx, uint32_t lanes);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
  * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument —

@@ -1779,16 +1779,19 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   float tfar = 0.0f;
   Ray r;
   WideWalk wk;
+  bool drained = false;  // (wave-uniform) a lane of this wave asked for a ray and none was left
   for (;;) {
     uint32_t item = kNoHit;
     bool more;  // unstarted items may remain for this wave
     if constexpr (kQueue) {
       item = xcd_take(xq, !have, &s_taken, cap);
       more = !xq.drained;
+      drained = xq.drained;
     } else {
       const uint32_t k = block_take(&s_next, !have);
       if (!have && k < nb) item = block_item(sd, k);
       more = __ballot(!have && k < nb) != 0ull;
+      if (__ballot(!have && k >= nb) != 0ull) drained = true;
     }
     if (item != kNoHit) {
       const uint32_t i = item;
@@ -1836,6 +1839,36 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
 #ifdef SPTR_EXPERIMENT_STEP_CAP
     if (have && !done && ++rounds >= (uint32_t)SPTR_EXPERIMENT_STEP_CAP) done = true;
 #endif
+    // Straggler hand-off: the wave has no rays left to start and at most strag_lanes lanes are still
+    // tracing (the long rays that would otherwise set the launch's length while the rest of the chip
+    // idles).  Their rays are written to the bounce's straggler records and k_strag, beside the chain,
+    // traces each again from the root and carries its path to the end; no hit record is written here.
+    if (!kCount && w.strag_lanes != 0u && drained && (uint32_t)depth < kStragBounces) {
+      const unsigned long long act = __ballot(have && !done);
+      if (act != 0ull && (uint32_t)__popcll(act) <= w.strag_lanes && have && !done) {
+        const uint32_t slot = atomicAdd(&w.work[kWorkStrag + (uint32_t)depth * 32u], 1u);
+        if (slot < w.strag_cap) {
+          float4* rec = w.strag + ((size_t)depth * w.strag_cap + slot) * kStragRec;
+          // the walk as it stands (k_strag resumes it: same node order, same hit)
+          rec[3] = make_float4(__uint_as_float(wk.cur), __uint_as_float((uint32_t)wk.sp | (wk.hit ? 0x10000u : 0u)),
+                               __uint_as_float(ref), tfar);
+          uint32_t* st = reinterpret_cast<uint32_t*>(rec + 4);
+          for (int q = 0; q < wk.sp; ++q) st[q] = stack.get(q);
+          if (kPrimary) {
+            Primary pr;
+            (void)primary_path(f, idiv, pid, pr);
+            rec[0] = f4(f.cam_pos, __uint_as_float(pr.rng));
+            rec[1] = f4(r.d, __uint_as_float(pid));
+            rec[2] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(0u));
+          } else {
+            rec[0] = rs.o[id];
+            rec[1] = rs.d[id];
+            rec[2] = f4(xyz(rs.thr[id]), __uint_as_float((uint32_t)depth));
+          }
+          have = false;
+        }
+      }
+    }
     const bool fin = have && done;
     if (kCount && fin && v0 != ~0u) hist_ray(s_hist, vc.nodes - v0);
     const bool defer = !kPrimary && w.defer_miss != 0u;
@@ -1995,7 +2028,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   const float rr = sqrtf(r2);
   const float lx = rr * cosf(phi), ly = rr * sinf(phi);
   const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
-  const vec3 nn = safe_renormalize_dir(nrm);
+  const vec3 nn = renormalized_again(nrm);  // s.n: safe_normalize's output (or its negation)
   const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize_dir(cross(nn, v3(0.0f, 0.0f, 1.0f)))
                                          : normalize_dir(cross(nn, v3(0.0f, 1.0f, 0.0f)));
   const vec3 bt = cross(tg, nn);
@@ -2010,7 +2043,7 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   } else {
     thr = thr * albedo;
   }
-  nd = safe_renormalize_dir(sdir);
+  nd = renormalized_again(sdir);  // sdir: safe_renormalize_dir's output
   return cont;
 }
 
@@ -2554,6 +2587,138 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   report_stack(vc, w.tot);
 }
 
+// --------------------------------------------------------------------------------- k_strag
+// The paths whose bounce-`depth0` ray k_trace_dyn handed off (WaveView::strag), one thread per path,
+// refilled per bounce as in k_tail: the ray is traced again from the root, then the path is carried to
+// its end with k_tail's per-bounce steps — the operations and radiance-update order of k_trace + k_shade
+// + k_shadow — so a handed-off path adds exactly what the wavefront stages would have added.  The host
+// launches it after the trace and after the shadow launch of the previous bounce (which may still add to
+// these paths' radiance) and joins it before the batch's k_accum; no other kernel touches the paths in
+// between.  A bounce-0 path starts from zero radiance, as k_shade<primary> does.  The handed-off ray
+// itself was counted by its trace launch; the later bounces' closest-hit and the any-hit queries are
+// added to the totals here (atomics: k_shadow_dyn may be updating the per-block tallies meanwhile).
+static_assert(SPTR_PRIMARY_UNIFIED == 1 || SPTR_WALK_UNIFIED == 0, "k_strag resumes camera and bounce rays with one walk kind");
+template <bool kW4, bool kCube>
+__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv, ShadeView sh, FrameView f, WaveView w,
+                                                                    int depth0) {
+  __shared__ KernelStack<false> s_stack;
+  __shared__ DevMaterial smat[32];
+  __shared__ uint32_t s_rays[2], s_next;
+  const uint32_t nm = stage_materials(sh, smat);
+  if (threadIdx.x < 2u) s_rays[threadIdx.x] = 0u;
+  if (threadIdx.x == 0u) s_next = 0u;
+  const Staged sc = stage_scene<false>(sv, nullptr);
+  __syncthreads();
+  const uint32_t n = min(w.work[kWorkStrag + (uint32_t)depth0 * 32u], w.strag_cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&w.tot[kTotStrag], (unsigned long long)n);
+  const float4* in = w.strag + (size_t)depth0 * w.strag_cap * kStragRec;
+  TravStack<kLdsStackG> stack;  // the resumed walks' stack (later bounces use traverse_w's own)
+  stack.lds = &s_stack.e[0][threadIdx.x];
+  WideWalk wk;
+  float tfar0 = 0.0f;
+  uint32_t ref0 = kNoHit;
+  const uint32_t L = w.L, D = f.max_depth;
+  Visits vc;
+  uint32_t n_closest = 0u, n_shadow = 0u;
+  const Sched sd = block_sched(n);
+  const uint32_t nb = block_items(sd, n);
+  bool have = false, loaded = false, first = false;
+  vec3 ro, rd, thr, radv;
+  uint32_t rng = 0u, p = 0u, depth = 0u;
+  for (;;) {
+    const uint32_t k = block_take(&s_next, !have);
+    if (!have && k < nb) {
+      const float4* rec = in + (size_t)block_item(sd, k) * kStragRec;
+      const float4 o4 = rec[0], d4 = rec[1], t4 = rec[2], w4 = rec[3];
+      wk.cur = __float_as_uint(w4.x);
+      wk.sp = (int)(__float_as_uint(w4.y) & 0xFFFFu);
+      wk.hit = (__float_as_uint(w4.y) >> 16) != 0u;
+      ref0 = __float_as_uint(w4.z);
+      tfar0 = w4.w;
+      const uint32_t* st = reinterpret_cast<const uint32_t*>(rec + 4);
+      for (int q = 0; q < wk.sp; ++q) stack.put(q, st[q]);
+      ro = xyz(o4);
+      rd = xyz(d4);
+      thr = xyz(t4);
+      rng = __float_as_uint(o4.w);
+      p = __float_as_uint(d4.w);
+      depth = __float_as_uint(t4.w);
+      loaded = depth == 0u;  // bounce 0: the path's radiance starts at zero (rad[p] holds an older batch's)
+      radv = v3(0.0f, 0.0f, 0.0f);
+      first = true;
+      have = depth < D;
+    }
+    if (__ballot(have) == 0ull) break;
+    if (!have) continue;
+    bool fin = true;
+    do {
+      float tfar = __builtin_huge_valf();
+      uint32_t ref = kNoHit;
+      bool hit;
+      if (first) {  // the handed-off ray: its walk resumes where k_trace_dyn left it (the same walk kind)
+        tfar = tfar0;
+        ref = ref0;
+        (void)walk_steps<false, false, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, nullptr, 0u, make_ray(ro, rd), 0.0f,
+                                                                   tfar, ref, vc, 0x7FFFFFFF);
+        hit = wk.hit;
+      } else {
+        ++n_closest;
+        hit = traverse_w<kW4, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
+      }
+      first = false;
+      if (sh.debug_mode == 1) {
+        radv = hit ? v3(1.0f, 1.0f, 1.0f) : v3(0.0f, 0.0f, 0.0f);
+        loaded = true;
+        break;
+      }
+      if (!loaded) {
+        radv = xyz(w.rad[p]);
+        loaded = true;
+      }
+      if (!hit) {
+        radv = radv + thr * env_color<kCube>(sh.env, renormalized_again(rd));
+        break;
+      }
+      const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
+      const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
+      if (dot(emission, emission) > 0.0f) radv = radv + thr * emission;
+      const vec3 view = -rd;
+      for (uint32_t li = 0; li < L; ++li) {
+        vec3 so, ldir, contrib;
+        float st;
+        if (!light_term(sh.lights[li], sf, view, thr, so, ldir, st, contrib)) continue;
+        ++n_shadow;
+        uint32_t sref = kNoHit;
+        if (!traverse_w<kW4, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
+          radv = radv + contrib;
+      }
+      vec3 no, nd;
+      if (!continue_path(sf, rd, depth, thr, rng, no, nd)) break;
+      ro = no;
+      rd = nd;
+      fin = ++depth >= D;
+    } while (false);
+    if (fin) {
+      if (loaded) w.rad[p] = f4(radv, 0.0f);
+      have = false;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    n_closest += __shfl_xor(n_closest, off);
+    n_shadow += __shfl_xor(n_shadow, off);
+  }
+  if (lane_id() == 0u) {
+    atomicAdd(&s_rays[0], n_closest);
+    atomicAdd(&s_rays[1], n_shadow);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)s_rays[0]);
+    atomicAdd(&w.tot[kTotShadow], (unsigned long long)s_rays[1]);
+  }
+  report_stack(vc, w.tot);
+}
+
 // --------------------------------------------------------------------------------- k_sky
 // Path-major bounce 0 with a cull mask (f.sky_fold): the culled pixels' camera rays all miss, so
 // their samples are nothing but raygen + environment.  One thread per culled pixel sums them into
@@ -2710,6 +2875,8 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
     if (f.dyn && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
     if (f.dyn && threadIdx.x >= 64 && threadIdx.x < 64 + kXcds) const_cast<uint32_t*>(f.dyn)[kDynSkyQueue + 32u * (threadIdx.x - 64)] = 0u;
     if (threadIdx.x < kXcds) w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;
+    // the straggler counts of this batch's bounces (their k_strag launches were joined before this one)
+    if (threadIdx.x >= 128 && threadIdx.x < 128 + kStragBounces) w.work[kWorkStrag + (threadIdx.x - 128) * 32u] = 0u;
   }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     uint32_t s0 = 0u;
@@ -3617,6 +3784,24 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
         }(fl);
       },
       Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
+}
+
+bool strag_applies(const SceneView& sv) {
+  return sv.lds_bytes == 0u && sv.width == (uint32_t)kWide && sv.scene_bytes > kL2BytesPerXcd && !no_dyn();
+}
+
+// a fixed grid: the number of handed-off paths is known only on the device (k_strag reads it).  Small,
+// so that it holds few of the wave slots the chain's resident grids expect (r04k: 1024 blocks, 16 waves
+// per CU, made C5 8.38 -> 10.17 ms/step), large enough to finish its paths before the batch's k_accum
+// (r04l/m at 16 lanes: 64 / 128 / 256 / 512 blocks 13.1 / 9.6 / 7.9 / 8.1 ms)
+#ifndef SPTR_STRAG_GRID
+#define SPTR_STRAG_GRID 256
+#endif
+void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                  hipStream_t s) {
+  constexpr unsigned kStragGrid = SPTR_STRAG_GRID;
+  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_strag<true, true>), dim3(kStragGrid), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+  else hipLaunchKernelGGL((k_strag<true, false>), dim3(kStragGrid), dim3(kBlock), 0, s, sv, sh, f, w, depth);
 }
 
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {

@@ -132,6 +132,8 @@ int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_sl
     API_HIP(ensure_buf(b.seg, seg_table_bytes()));
     API_HIP(hipMemset(b.seg.p, 0, seg_table_bytes()));
   }
+  // straggler records (k_trace_dyn -> k_strag, scenes beyond an XCD's L2): kStragCap per bounce
+  if (strag_applies(scene_view(c))) API_HIP(ensure_buf(b.strag, (size_t)kStragHandoffBounces * kStragCap * kStragRec * 16u));
   API_HIP(ensure_buf(b.hrec, hrec_bytes));
   if (b.cap >= cap && b.L * b.ts >= L * ts && b.rad.p) return SPTR_OK;
   // Segmented streams: a stage with G blocks writes block b's outputs at [b*per, b*per + count)
@@ -184,6 +186,9 @@ WaveView wave_view(Context& c) {
   w.defer_miss = 0u;
   w.seg_cap = (uint32_t)(wb.cap + (uint64_t)kMaxSegs * kBlock);
   w.hrec_cap = (uint32_t)hcap;
+  w.strag = static_cast<float4*>(wb.strag.p);
+  w.strag_cap = wb.strag.p ? kStragCap : 0u;
+  w.strag_lanes = 0u;  // set per trace launch (enqueue_wavefront)
   return w;
 }
 
@@ -377,6 +382,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   }
   stats->hits_primary = tot[kTotHitP];
   stats->hits_bounce = tot[kTotHitB];
+  stats->paths_handed_off = tot[kTotStrag];
   stats->cull_launches = culls;
   return SPTR_OK;
 }
@@ -572,6 +578,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   // alone (misses deferred to k_shade, WaveView::defer_miss); k_shade(d + 1) overwrites the shadow
   // tasks and updates rad[], so it, the tail and k_accum wait for shadow(d) (ev.join)
   const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, w);
+  const bool strag = c.strag_lanes != 0u && !count && w.strag != nullptr && strag_applies(sv);
   w.defer_miss = shadow_side ? 1u : 0u;
   StageTimer tside{c, tm.on, tm.trace_only, ss};
   tside.capturing = tm.capturing;
@@ -633,8 +640,11 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         if (!cap) c.last_forked = true;
         check(hipEventRecord(ev.fork, s), "sky fork record");
       }
+      // straggler hand-off of this bounce's trace (scenes beyond an XCD's L2; not the visit-count pass)
+      WaveView wt = w;
+      wt.strag_lanes = (strag && (uint32_t)d < kStragHandoffBounces) ? c.strag_lanes : 0u;
       tm.begin(d == 0 ? 5 : 1);
-      const uint32_t g_trace = launch_trace(sv, sh, fv, w, d, count, g_shade, s);
+      const uint32_t g_trace = launch_trace(sv, sh, fv, wt, d, count, g_shade, s);
       tm.end();
       if (sky_side) {
         check(hipStreamWaitEvent(ks, ev.fork, 0), "sky fork wait");
@@ -643,6 +653,18 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         join_sky = true;
       }
       join_shadow();  // shadow(d - 1) before shade(d)
+      if (wt.strag_lanes) {
+        // k_strag(d) after trace(d) and shadow(d - 1) (both may have updated the handed-off paths'
+        // radiance), on the k_sky stream, joined before k_accum with k_sky (ev.sky)
+        if (overlap) {
+          fork_to(ks);
+          launch_strag(sv, sh, fv, w, d, ks);
+          check(hipEventRecord(ev.sky, ks), "straggler join record");
+          join_sky = true;
+        } else {
+          launch_strag(sv, sh, fv, w, d, s);
+        }
+      }
       tm.begin(d == 0 ? 6 : 2);
       g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
       tm.end();
@@ -1006,7 +1028,7 @@ int sptr_destroy(sptr_ctx* x) {
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
                     &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist};
   for (DevBuf* b : bufs) free_buf(*b);
-  for (DevBuf* b : {&c.wb.hrec, &c.wb.rad, &c.wb.stask, &c.wb.seg}) free_buf(*b);
+  for (DevBuf* b : {&c.wb.hrec, &c.wb.rad, &c.wb.stask, &c.wb.seg, &c.wb.strag}) free_buf(*b);
   for (auto& r : c.wb.rs)
     for (DevBuf& x : r) free_buf(x);
   for (hipStream_t st : {c.side2_stream, c.cap_side2})
@@ -1062,9 +1084,17 @@ int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
   if (!x) return SPTR_ERR_INVALID;
   if (max_pieces == 0u) max_pieces = 1u;
   if (max_pieces > 32u || (max_pieces & (max_pieces - 1u)))
-    return fail(x->c, SPTR_ERR_INVALID, "split references: 0 (default 16) or a power of two up to 32");
+    return fail(x->c, SPTR_ERR_INVALID, "split references: 0 (default: 1, none) or a power of two up to 32");
   x->c.split_pieces = max_pieces;
   ++x->c.epoch;
+  return SPTR_OK;
+}
+
+int sptr_set_stragglers(sptr_ctx* x, uint32_t lanes) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (lanes > 64u) return fail(x->c, SPTR_ERR_INVALID, "straggler lanes: 0 (no hand-off) to 64");
+  x->c.strag_lanes = lanes;
+  ++x->c.epoch;  // part of every captured launch sequence's arguments
   return SPTR_OK;
 }
 

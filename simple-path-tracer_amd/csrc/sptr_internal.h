@@ -173,10 +173,12 @@ struct FrameView {
 };
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
 // the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
-// r04 work distribution (A/B builds; measured r04f, DESIGN.md §8: each slower or within noise, so off):
+// r04 work distribution (A/B builds; measured r04f, DESIGN.md §8: the first two slower, so off):
 // SPTR_PM_QUEUE, the pixel-major bounce 0 takes 64-pixel chunks from a queue in k_cull's order;
 // SPTR_SKY_LANES, k_sky runs lane groups over k_cull's culled list through per-XCD queues;
-// SPTR_TRACE_QUEUE, k_trace_dyn of scenes beyond an XCD's L2 takes work from per-XCD queues
+// SPTR_TRACE_QUEUE, k_trace_dyn of scenes beyond an XCD's L2 takes work from per-XCD queues: within
+// noise alone (r04f), on since the straggler hand-off (r04l: with k_strag's blocks resident beside it
+// a static share leaves late-starting blocks a tail; C5 8.68 -> 8.49 ms at 8 lanes, grid 128)
 #ifndef SPTR_PM_QUEUE
 #define SPTR_PM_QUEUE 0
 #endif
@@ -184,7 +186,7 @@ struct FrameView {
 #define SPTR_SKY_LANES 0
 #endif
 #ifndef SPTR_TRACE_QUEUE
-#define SPTR_TRACE_QUEUE 0
+#define SPTR_TRACE_QUEUE 1
 #endif
 // hit-record segments hold twice the static shares when a producer takes work from a queue
 constexpr uint32_t kHrecQueueMult = (SPTR_PM_QUEUE || SPTR_TRACE_QUEUE) ? 2u : 1u;
@@ -199,9 +201,25 @@ constexpr uint64_t kGraphForkedMaxSamples = 1ull << 22;  // run_call: graphs for
 enum : uint32_t { kFoldNone = 0, kFoldThread = 1, kFoldWave = 2 };
 
 // work-queue counters (WaveView::work), 8 XCDs 128 B apart per slot: k_shadow_dyn's two bounce slots
-// (words 0 and 256), k_trace_dyn's (kWorkTraceQueue)
-constexpr uint32_t kWorkWords = 768;
+// (words 0 and 256), k_trace_dyn's (kWorkTraceQueue); then the straggler counts of bounces
+// 0..kStragBounces-1 (kWorkStrag, 128 B apart; zeroed by k_accum)
 constexpr uint32_t kWorkTraceQueue = 512;
+constexpr uint32_t kWorkStrag = 768;
+constexpr uint32_t kStragBounces = 4;  // bounces whose trace may hand long rays off (k_trace_dyn -> k_strag)
+constexpr uint32_t kWorkWords = kWorkStrag + 32u * kStragBounces;
+// Straggler hand-off (k_trace_dyn, k_strag): records per bounce, each {o, rng} {d, path} {thr, depth}
+// {walk: node, depth | hit << 16, ref, tfar} and the walk's stack entries (kStragRec float4s), and the
+// default lane threshold (a drained wave hands its rays off once this few lanes are still busy)
+constexpr uint32_t kStragCap = 1u << 17;
+constexpr uint32_t kStragRec = 4u + (uint32_t)kStack / 4u;
+constexpr uint32_t kStragLanesDefault = 8;  // r04n A/B (C5, grid 256, bounce 0): 0/8/16/32 lanes 8.03/7.76/7.95/8.48 ms
+// bounces whose traces hand off (<= kStragBounces): a handed-off path must be finished before the
+// batch's k_accum, so the later a bounce, the less time its stragglers have beside the chain (r04n,
+// C5 at 8 lanes: bounce 0 / 0-1 / 0-2: 7.76 / 7.82 / 7.94 ms)
+#ifndef SPTR_STRAG_MAXD
+#define SPTR_STRAG_MAXD 1
+#endif
+constexpr uint32_t kStragHandoffBounces = SPTR_STRAG_MAXD;
 constexpr uint32_t kMaxSegs = 2048;  // max producer grid (256 CUs x 8 blocks)
 
 // 64-bit totals block
@@ -222,12 +240,13 @@ enum : int {
   kTotHistS = kTotHistT + 16,        // [kHistBins] any-hit queries of the shadow stage, likewise
   kTotHitP = kTotHistS + 16,         // closest hits found by the bounce-0 trace kernels (COUNT_VISITS)
   kTotHitB,                          // closest hits found by the later trace kernels (COUNT_VISITS)
+  kTotStrag,                         // paths k_trace_dyn handed off to k_strag
   kTotWords
 };
 
 constexpr int kStatDepths = 8;  // per-bounce statistics: bounces 0..6, and 7 = every later one
 constexpr int kHistBins = 16;   // per-ray visit histograms: bin b holds 2^(b-1) <= visits < 2^b (bin 0: none)
-static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 2, "totals layout");
+static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 3, "totals layout");
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
@@ -298,6 +317,12 @@ struct WaveView {
   // slot's throughput becomes thr * env and a record with prim kNoHit is queued, so that no kernel of
   // the bounce but k_shade writes rad[] and k_shadow_dyn(d - 1) may run beside it (enqueue_wavefront)
   uint32_t defer_miss;
+  // straggler hand-off (k_trace_dyn of scenes beyond an XCD's L2): once a wave's share of rays is used
+  // up and at most strag_lanes of its lanes are still tracing, those rays are written to strag (bounce
+  // d's region, strag_cap records of 3 float4) and the paths are finished by k_strag beside the chain;
+  // strag_lanes = 0: no hand-off
+  float4* strag;
+  uint32_t strag_cap, strag_lanes;
 };
 
 struct DevBuf {
@@ -309,7 +334,7 @@ struct DevBuf {
 struct WaveBufs {
   uint64_t cap = 0;  // paths
   uint32_t L = 0, ts = 0;
-  DevBuf rs[2][3], hrec, rad, stask, seg;
+  DevBuf rs[2][3], hrec, rad, stask, seg, strag;
 };
 
 struct StageMark {
@@ -358,6 +383,7 @@ struct Context {
   // excepted, run_call); 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
   uint32_t launch_mode = 0;
   bool last_forked = false;          // the last direct launch sequence forked launches to a side stream
+  uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
   GraphCache graph;
@@ -447,6 +473,11 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
                      uint32_t nseg_in, hipStream_t s);
 unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count, uint32_t nseg_in,
                    hipStream_t s);
+// the paths bounce d's trace handed off (k_strag), each carried to its end path-per-thread
+void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+                  hipStream_t s);
+// whether bounce traces of this scene hand their stragglers off (wide BVH beyond an XCD's L2)
+bool strag_applies(const SceneView& sv);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 // resolve: also tone-map the sums into tiles (+ image) in the same launch (the call's last batch)
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,

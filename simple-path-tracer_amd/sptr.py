@@ -88,7 +88,7 @@ class Stats(C.Structure):
                 ("cull_launches", C.c_uint64), ("shadow_launches", C.c_uint64),
                 ("traced_by_depth", C.c_uint64 * 8), ("nodes_by_depth", C.c_uint64 * 8),
                 ("trace_visit_hist", C.c_uint64 * 16), ("shadow_visit_hist", C.c_uint64 * 16),
-                ("hits_primary", C.c_uint64), ("hits_bounce", C.c_uint64)]
+                ("hits_primary", C.c_uint64), ("hits_bounce", C.c_uint64), ("paths_handed_off", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(v) if isinstance(v, C.Array) else v) for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}
@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_stragglers", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -144,6 +144,7 @@ def lib() -> C.CDLL:
         "sptr_set_tail_depth": (C.c_int, [vp, u32]),
         "sptr_set_leaf_size": (C.c_int, [vp, u32]),
         "sptr_set_split_refs": (C.c_int, [vp, u32]),
+        "sptr_set_stragglers": (C.c_int, [vp, u32]),
         "sptr_set_bvh_width": (C.c_int, [vp, u32]),
         "sptr_upload_scene": (C.c_int, [vp, C.POINTER(Scene)]),
         "sptr_set_materials": (C.c_int, [vp, C.POINTER(Material), u32]),
@@ -430,8 +431,13 @@ class Renderer:
         self._check(self._L.sptr_set_leaf_size(self._h, n), "set_leaf_size")
 
     def set_split_refs(self, max_pieces: int):
-        """sptr_set_split_refs: most references per split triangle (0 = default 16, 1 = none); next upload."""
+        """sptr_set_split_refs: most references per split triangle (0 = default 1: none); next upload."""
         self._check(self._L.sptr_set_split_refs(self._h, max_pieces), "set_split_refs")
+
+    def set_stragglers(self, lanes: int):
+        """sptr_set_stragglers: hand a drained wave's rays off once at most `lanes` lanes still trace
+        (0 = off, default 8); HBM-resident scenes only."""
+        self._check(self._L.sptr_set_stragglers(self._h, lanes), "set_stragglers")
 
     def set_bvh_width(self, n: int):
         self._check(self._L.sptr_set_bvh_width(self._h, n), "set_bvh_width")

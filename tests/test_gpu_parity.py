@@ -535,6 +535,36 @@ def test_many_calls_without_collect(renderer, mode):
         renderer.set_launch_mode(0)
 
 
+@pytest.mark.parametrize("lanes", [64, 8])
+def test_straggler_handoff_changes_no_result(renderer, lanes):
+    """Straggler hand-off (sptr_set_stragglers, scenes beyond an XCD's L2): bounce traces hand the rays
+    still running in their drained waves to k_strag, which finishes those paths beside the chain.  With
+    every drained wave's rays handed off (64 lanes) and with the default (8), the accumulation is
+    bit-identical to no hand-off, the query counts are equal, and paths were handed off — in direct
+    launches (mode 1), a captured graph (mode 3) and one stream (mode 2)."""
+    W, H, S = 128, 96, 8
+    sptr.setup_default(renderer, "sphere_mesh", 300, 600)  # 360 K triangles, 17 MB: beyond one L2
+    cam = sptr.camera_lookat(aspect=W / H)
+    try:
+        renderer.set_stragglers(0)
+        st0 = renderer.render(cam, W, H, spp=S)
+        ref = renderer.read_accum().copy()
+        assert st0.paths_handed_off == 0
+        renderer.set_stragglers(lanes)
+        for mode in (1, 3, 2):
+            renderer.set_launch_mode(mode)
+            for _ in range(3):
+                st = renderer.render(cam, W, H, spp=S)
+                assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32)), (mode, lanes)
+                assert (st.rays_closest, st.rays_shadow) == (st0.rays_closest, st0.rays_shadow), (mode, lanes)
+                if lanes == 64:
+                    assert st.paths_handed_off > 0, mode
+            print("stragglers", lanes, "mode", mode, "handed off", st.paths_handed_off)
+    finally:
+        renderer.set_launch_mode(0)
+        renderer.set_stragglers(8)
+
+
 def test_large_forked_call_launches_direct(renderer):
     """Launch mode 0 leaves a large call whose launches fork to the side streams (here 8.4 M samples,
     the shadow launches beside the traces of the L2-resident sphere mesh) to direct launches — the
