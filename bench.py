@@ -167,6 +167,11 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     stream_read = tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))  # coalesced reads
     residency, footprint = _residency(layout)
     scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * tb}[residency]
+    # straggler hand-off (hbm scenes): the rest of a handed-off ray's walk runs in k_strag, not in the
+    # trace launch; its visits (counted in every call) are not the trace launch's bytes
+    sv = [sum(list(getattr(s, "strag_visits", (0, 0, 0)))[i] for s in stats) for i in range(3)]
+    strag_bytes = node_b * sv[0] + 48.0 * sv[1] + 16.0 * sv[2] if residency == "hbm" else 0.0
+    scene -= strag_bytes
     per_launch = (stream + scene) / max(1, launches)
     achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     s8d = ((STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (tp + tb) + 64.0 * (pp[0] * tp + pb[0] * tb)
@@ -185,6 +190,8 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches_per_step": round(launches / max(1, steps), 3),
         "traversed_rays_per_launch": round((tp + tb) / max(1, launches)),
+        "handed_off": {"paths_per_launch": round(sum(getattr(s, "paths_handed_off", 0) for s in stats) / max(1, launches)),
+                       "resumed_walk_bytes_per_launch": round(strag_bytes / max(1, launches))},
         "hit_fraction": {"primary": round(hp, 4), "bounce": round(hb, 4)},
         "scene_in_lds": residency == "lds", "scene_residency": residency, "scene_bytes": int(footprint),
         "per_ray": {"primary": {"nodes": round(pp[0], 3), "tris": round(pp[1], 3), "spheres": round(pp[2], 3)},

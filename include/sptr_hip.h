@@ -197,6 +197,8 @@ typedef struct sptr_stats {
                                          (of traced_primary / traced_bounce) */
   uint64_t paths_handed_off;          /* ABI 6: paths a bounce trace handed to the straggler kernel
                                          (sptr_set_stragglers) */
+  uint64_t strag_visits[3];           /* ABI 6: node visits, triangle and sphere tests of the handed-off
+                                         rays' walks made by the straggler kernel (every call) */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */

@@ -926,7 +926,7 @@ __device__ __forceinline__ void flush_visits(const Visits& vc, unsigned long lon
   if (lane_id() == 0) {
     atomicAdd(&tot[base + 0], a);
     atomicAdd(&tot[base + 1], b);
-    if (base == kTotNodes || base == kTotNodesP) atomicAdd(&tot[base + 2], c);
+    if (base == kTotNodes || base == kTotNodesP || base == kTotStragNodes) atomicAdd(&tot[base + 2], c);
   }
 }
 
@@ -2618,7 +2618,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
   float tfar0 = 0.0f;
   uint32_t ref0 = kNoHit;
   const uint32_t L = w.L, D = f.max_depth;
-  Visits vc;
+  Visits vc, vr;  // vr: the resumed walks' visits (the part of the handed-off rays' traversal done here)
   uint32_t n_closest = 0u, n_shadow = 0u;
   const Sched sd = block_sched(n);
   const uint32_t nb = block_items(sd, n);
@@ -2658,8 +2658,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
       if (first) {  // the handed-off ray: its walk resumes where k_trace_dyn left it (the same walk kind)
         tfar = tfar0;
         ref = ref0;
-        (void)walk_steps<false, false, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, nullptr, 0u, make_ray(ro, rd), 0.0f,
-                                                                   tfar, ref, vc, 0x7FFFFFFF);
+        (void)walk_steps<false, true, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, nullptr, 0u, make_ray(ro, rd), 0.0f,
+                                                                  tfar, ref, vr, 0x7FFFFFFF);
         hit = wk.hit;
       } else {
         ++n_closest;
@@ -2716,7 +2716,9 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
     atomicAdd(&w.tot[kTotClosest], (unsigned long long)s_rays[0]);
     atomicAdd(&w.tot[kTotShadow], (unsigned long long)s_rays[1]);
   }
+  flush_visits(vr, w.tot, kTotStragNodes);
   report_stack(vc, w.tot);
+  report_stack(vr, w.tot);
 }
 
 // --------------------------------------------------------------------------------- k_sky

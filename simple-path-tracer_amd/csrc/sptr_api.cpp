@@ -383,6 +383,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   stats->hits_primary = tot[kTotHitP];
   stats->hits_bounce = tot[kTotHitB];
   stats->paths_handed_off = tot[kTotStrag];
+  for (int i = 0; i < 3; ++i) stats->strag_visits[i] = tot[kTotStragNodes + i];
   stats->cull_launches = culls;
   return SPTR_OK;
 }

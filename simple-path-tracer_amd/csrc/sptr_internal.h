@@ -241,12 +241,13 @@ enum : int {
   kTotHitP = kTotHistS + 16,         // closest hits found by the bounce-0 trace kernels (COUNT_VISITS)
   kTotHitB,                          // closest hits found by the later trace kernels (COUNT_VISITS)
   kTotStrag,                         // paths k_trace_dyn handed off to k_strag
+  kTotStragNodes, kTotStragTris, kTotStragSph,  // the handed-off walks' visits made by k_strag (every call)
   kTotWords
 };
 
 constexpr int kStatDepths = 8;  // per-bounce statistics: bounces 0..6, and 7 = every later one
 constexpr int kHistBins = 16;   // per-ray visit histograms: bin b holds 2^(b-1) <= visits < 2^b (bin 0: none)
-static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 3, "totals layout");
+static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 6, "totals layout");
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.

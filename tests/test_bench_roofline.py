@@ -159,3 +159,18 @@ def test_step_roofline_components(bench, layout, env):
     else:
         assert parts["tail"] == 0
     assert a["frac"] == pytest.approx(a["bytes_per_step"] / 3e-3 / 1e9 / 8000.0, rel=1e-3)
+
+
+def test_handed_off_walk_bytes_not_charged(bench):
+    """hbm residency: the visits k_strag made for handed-off rays (sptr_stats.strag_visits, every call)
+    leave the trace launch's bytes; l2/lds scenes (no hand-off) are unaffected."""
+    base = bench.roofline(CNT, [_step_stats(2)], HBM, "no_such_workload", 2)
+    st = _step_stats(2)
+    st.strag_visits = (1_000_000, 200_000, 10_000)
+    st.paths_handed_off = 5000
+    r = bench.roofline(CNT, [st], HBM, "no_such_workload", 2)
+    cut = (64.0 * 1_000_000 + 48.0 * 200_000 + 16.0 * 10_000) / 12
+    assert r["bytes_per_launch"] == pytest.approx(base["bytes_per_launch"] - cut, abs=1)
+    assert r["handed_off"]["resumed_walk_bytes_per_launch"] == round(cut)
+    l = bench.roofline(CNT, [st], LDS, "no_such_workload", 2)
+    assert l["handed_off"]["resumed_walk_bytes_per_launch"] == 0
