@@ -1316,13 +1316,17 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
-  const Sched sd = block_sched(f.P);
+  const uint32_t* order = f.pm_order;  // k_cull's list (null without a cull mask: local pixel order)
+  const uint32_t n_unc = order ? order[f.P] : f.P;
+  // f.sky_fold (r04): k_sky sums the culled pixels beside this launch, so only k_cull's unculled pixels
+  // are this kernel's (in the list's order); otherwise every local pixel, culled ones as sky loops
+  const bool split = f.sky_fold != 0u && order != nullptr;
+  const uint32_t n_pix = split ? n_unc : f.P;
+  const Sched sd = block_sched(n_pix);
   constexpr bool kQ = SPTR_PM_QUEUE != 0;
   const uint32_t cap = kQ ? 2u * sd.per : sd.per;  // pixels this block may take: its hit-record segment holds cap * k records
   const uint32_t per = cap * f.k;                  // hit-record segment stride
   const uint32_t seg0 = logical_block() * per;
-  const uint32_t* order = f.pm_order;  // k_cull's list (null without a cull mask: local pixel order)
-  const uint32_t n_unc = order ? order[f.P] : f.P;
   uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
   const uint32_t lane = lane_id();
   for (uint32_t it = 0;; ++it) {
@@ -1334,13 +1338,14 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
         if (t + 64u <= cap) base = atomicAdd(queue, 64u);
       }
       base = __shfl(base, 0);
-      if (base >= f.P) break;  // the frame is taken (or this block's segment is full)
+      if (base >= n_pix) break;  // the frame is taken (or this block's segment is full)
       const uint32_t i = base + lane;
-      l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
+      l = i >= n_pix ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
     } else {  // the static share: 256-pixel chunks dealt round-robin
       const uint32_t base = sd.first + it * sd.step;
       if (base >= sd.end) break;
       l = base + threadIdx.x;
+      if (split) l = l < n_unc ? order[l] : kNoHit;
     }
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);

@@ -589,7 +589,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
     fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     fv.pixel_major = bounce0_pixel_major(sv, fv);
-    fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
+    // culled pixels summed by k_sky (beside the trace when launches overlap): path-major batches, and
+    // the thread-per-pixel bounce 0 (SPTR_PM_SKY: k_trace_pm then takes only k_cull's unculled pixels)
+    fv.sky_fold = (fv.cull != nullptr && (fv.pixel_major == kFoldNone ||
+                                          (SPTR_PM_SKY != 0 && fv.pixel_major == kFoldThread))) ? 1u : 0u;
     fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     fv.pm_order = (fv.cull != nullptr && fv.pixel_major != kFoldNone) ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),

@@ -185,6 +185,9 @@ struct FrameView {
 #ifndef SPTR_SKY_LANES
 #define SPTR_SKY_LANES 0
 #endif
+#ifndef SPTR_PM_SKY
+#define SPTR_PM_SKY 1  // the thread-per-pixel bounce 0 leaves its culled pixels to k_sky (see enqueue_wavefront)
+#endif
 #ifndef SPTR_TRACE_QUEUE
 #define SPTR_TRACE_QUEUE 1
 #endif
