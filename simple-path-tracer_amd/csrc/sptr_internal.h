@@ -186,7 +186,7 @@ struct FrameView {
 #define SPTR_SKY_LANES 0
 #endif
 #ifndef SPTR_PM_SKY
-#define SPTR_PM_SKY 1  // the thread-per-pixel bounce 0 leaves its culled pixels to k_sky (see enqueue_wavefront)
+#define SPTR_PM_SKY 0  // 1: the thread-per-pixel bounce 0 leaves its culled pixels to k_sky (r04s: C2 3.09-3.20 -> 3.54-3.57 ms, off)
 #endif
 #ifndef SPTR_TRACE_QUEUE
 #define SPTR_TRACE_QUEUE 1
