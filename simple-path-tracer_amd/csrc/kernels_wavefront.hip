@@ -698,103 +698,129 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
 #ifndef SPTR_PRIMARY_UNIFIED
 #define SPTR_PRIMARY_UNIFIED 1  // camera rays too (k_trace_dyn<primary>); 0: the leaf-inline walk
 #endif
+// One step of the unified walk, split into its fetch (the 56 B of the item wk.cur names: a wide node
+// from the LDS top levels or L2/HBM, or a direct leaf's triangle / sphere record) and the step proper
+// (walk_apply), so that a kernel tracing two rays per lane can issue both rays' fetches before either
+// waits (k_trace_dyn2).  wide_walk_u is fetch + apply per step: the arithmetic is one code path.
+struct WalkItem {
+  uint4 h, l4, q4;
+  uint2 q2;
+};
+__device__ __forceinline__ WalkItem walk_fetch(uint32_t cur, const WideNode* nodes, const uint4* top, uint32_t ntop,
+                                               const float4* tris, const float4* sph) {
+  const bool leaf = (cur & kLeafBit) != 0u;
+  const bool direct = (cur & (kLeafBit | kLeafDirect)) == (kLeafBit | kLeafDirect);
+  const bool dsph = direct && (cur & kLeafDirectSphere) != 0u;
+  const uint32_t slot = (cur & ~kLeafBit) >> kLeafCountBits;
+  const uint4* a = !leaf ? reinterpret_cast<const uint4*>(nodes + cur)
+                         : (dsph ? reinterpret_cast<const uint4*>(sph + slot)
+                                 : reinterpret_cast<const uint4*>(tris + (direct ? 3u * slot : 0u)));
+  WalkItem it;
+  if (cur < ntop) {
+    const uint4* t = top + 4u * cur;
+    it.h = t[0];
+    it.l4 = t[1];
+    it.q4 = t[2];
+    it.q2 = *reinterpret_cast<const uint2*>(t + 3);
+    // pins the LDS loads inside this branch: otherwise the compiler sinks both branches' loads past
+    // the join as flat loads of a selected address
+    asm volatile("" ::"v"(it.h.x), "v"(it.l4.x), "v"(it.q4.x), "v"(it.q2.x));
+  } else {
+    it.h = a[0];
+    it.l4 = a[1];
+    it.q4 = a[2];
+    it.q2 = *reinterpret_cast<const uint2*>(a + 3);
+  }
+  return it;
+}
+// the step on the fetched item; true when the traversal is over
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool walk_apply(WideWalk& wk, TravStack<N>& stack, const WalkItem& it, const uint32_t* prim_ref,
+                                           const float4* tris, const float4* sph, const Ray& r, float tnear, float& tfar,
+                                           uint32_t& ref, Visits& vc) {
+  const uint32_t cur = wk.cur;
+  const bool leaf = (cur & kLeafBit) != 0u;
+  const bool direct = (cur & (kLeafBit | kLeafDirect)) == (kLeafBit | kLeafDirect);
+  const bool dsph = direct && (cur & kLeafDirectSphere) != 0u;
+  const uint32_t slot = (cur & ~kLeafBit) >> kLeafCountBits;
+  if (leaf) {
+    bool hit = false;
+    if (direct) {
+      const float4 p0 = make_float4(__uint_as_float(it.h.x), __uint_as_float(it.h.y), __uint_as_float(it.h.z), __uint_as_float(it.h.w));
+      float t;
+      if (dsph) {
+        if (kCount) ++vc.sph;
+        if (kAny) hit = sphere_occ(p0, r, tnear, tfar);
+        else if (sphere_hit(p0, r, tnear, tfar, t)) {
+          tfar = t;
+          ref = slot | kSphereBit;
+          hit = true;
+        }
+      } else {
+        if (kCount) ++vc.tris;
+        const float4 p1 = make_float4(__uint_as_float(it.l4.x), __uint_as_float(it.l4.y), __uint_as_float(it.l4.z), __uint_as_float(it.l4.w));
+        const float4 p2 = make_float4(__uint_as_float(it.q4.x), __uint_as_float(it.q4.y), __uint_as_float(it.q4.z), __uint_as_float(it.q4.w));
+        if (tri_hit4(p0, p1, p2, r, tnear, tfar, t)) {
+          if (!kAny) {
+            tfar = t;
+            ref = slot;
+          }
+          hit = true;
+        }
+      }
+    } else {
+      hit = leaf_test<kAny, kCount>(cur, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
+    }
+    if (hit) {
+      wk.hit = true;
+      if (kAny) return true;
+    }
+    if (wk.sp == 0) return true;
+    wk.cur = stack.get(--wk.sp);
+    return false;
+  }
+  const uint32_t ln[4] = {it.l4.x, it.l4.y, it.l4.z, it.l4.w};
+  const uint32_t qw[6] = {it.q4.x, it.q4.y, it.q4.z, it.q4.w, it.q2.x, it.q2.y};
+  if (kCount) ++vc.nodes;
+  const QAxis ax = q_axis(__uint_as_float(it.h.x), it.h.w & 0xFFu, qw + 0, qw + 1, r.o.x, r.inv.x);
+  const QAxis ay = q_axis(__uint_as_float(it.h.y), (it.h.w >> 8) & 0xFFu, qw + 2, qw + 3, r.o.y, r.inv.y);
+  const QAxis az = q_axis(__uint_as_float(it.h.z), (it.h.w >> 16) & 0xFFu, qw + 4, qw + 5, r.o.z, r.inv.z);
+  float t[4];
+  bool hc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) && ln[k] != kNoHit;
+  int kn = 4;
+  float tn = __builtin_huge_valf();
+  uint32_t npush = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
+    if (hc[k] && (kn == 4 || better)) {
+      tn = t[k];
+      kn = k;
+    }
+    npush += hc[k] ? 1u : 0u;
+  }
+  if (kn < 4) {
+    if (wk.sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
+#pragma unroll
+    for (int k = 3; k >= 0; --k)
+      if (hc[k] && k != kn && wk.sp < kStack) stack.put(wk.sp++, ln[k]);
+    wk.cur = ln[kn];
+    return false;
+  }
+  if (wk.sp == 0) return true;
+  wk.cur = stack.get(--wk.sp);
+  return false;
+}
 template <bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
                                             uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
                                             const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
   static_assert(kWide == 4, "unified walk: 4-wide nodes");
   for (int it = 0; it < steps; ++it) {
-    const uint32_t cur = wk.cur;
-    const bool leaf = (cur & kLeafBit) != 0u;
-    const bool direct = (cur & (kLeafBit | kLeafDirect)) == (kLeafBit | kLeafDirect);
-    const bool dsph = direct && (cur & kLeafDirectSphere) != 0u;
-    const uint32_t slot = (cur & ~kLeafBit) >> kLeafCountBits;
-    const uint4* a = !leaf ? reinterpret_cast<const uint4*>(nodes + cur)
-                           : (dsph ? reinterpret_cast<const uint4*>(sph + slot)
-                                   : reinterpret_cast<const uint4*>(tris + (direct ? 3u * slot : 0u)));
-    uint4 h, l4, q4;
-    uint2 q2;
-    if (cur < ntop) {
-      const uint4* t = top + 4u * cur;
-      h = t[0];
-      l4 = t[1];
-      q4 = t[2];
-      q2 = *reinterpret_cast<const uint2*>(t + 3);
-      asm volatile("" ::"v"(h.x), "v"(l4.x), "v"(q4.x), "v"(q2.x));
-    } else {
-      h = a[0];
-      l4 = a[1];
-      q4 = a[2];
-      q2 = *reinterpret_cast<const uint2*>(a + 3);
-    }
-    if (leaf) {
-      bool hit = false;
-      if (direct) {
-        const float4 p0 = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
-        float t;
-        if (dsph) {
-          if (kCount) ++vc.sph;
-          if (kAny) hit = sphere_occ(p0, r, tnear, tfar);
-          else if (sphere_hit(p0, r, tnear, tfar, t)) {
-            tfar = t;
-            ref = slot | kSphereBit;
-            hit = true;
-          }
-        } else {
-          if (kCount) ++vc.tris;
-          const float4 p1 = make_float4(__uint_as_float(l4.x), __uint_as_float(l4.y), __uint_as_float(l4.z), __uint_as_float(l4.w));
-          const float4 p2 = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z), __uint_as_float(q4.w));
-          if (tri_hit4(p0, p1, p2, r, tnear, tfar, t)) {
-            if (!kAny) {
-              tfar = t;
-              ref = slot;
-            }
-            hit = true;
-          }
-        }
-      } else {
-        hit = leaf_test<kAny, kCount>(cur, prim_ref, tris, sph, r, tnear, tfar, ref, vc);
-      }
-      if (hit) {
-        wk.hit = true;
-        if (kAny) return true;
-      }
-      if (wk.sp == 0) return true;
-      wk.cur = stack.get(--wk.sp);
-      continue;
-    }
-    const uint32_t ln[4] = {l4.x, l4.y, l4.z, l4.w};
-    const uint32_t qw[6] = {q4.x, q4.y, q4.z, q4.w, q2.x, q2.y};
-    if (kCount) ++vc.nodes;
-    const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0, qw + 1, r.o.x, r.inv.x);
-    const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2, qw + 3, r.o.y, r.inv.y);
-    const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4, qw + 5, r.o.z, r.inv.z);
-    float t[4];
-    bool hc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) && ln[k] != kNoHit;
-    int kn = 4;
-    float tn = __builtin_huge_valf();
-    uint32_t npush = 0u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
-      if (hc[k] && (kn == 4 || better)) {
-        tn = t[k];
-        kn = k;
-      }
-      npush += hc[k] ? 1u : 0u;
-    }
-    if (kn < 4) {
-      if (wk.sp + (int)npush - 1 > kStack) vc.stack_overflow = 1u;
-#pragma unroll
-      for (int k = 3; k >= 0; --k)
-        if (hc[k] && k != kn && wk.sp < kStack) stack.put(wk.sp++, ln[k]);
-      wk.cur = ln[kn];
-    } else {
-      if (wk.sp == 0) return true;
-      wk.cur = stack.get(--wk.sp);
-    }
+    const WalkItem item = walk_fetch(wk.cur, nodes, top, ntop, tris, sph);
+    if (walk_apply<kAny, kCount>(wk, stack, item, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) return true;
   }
   return false;
 }
@@ -1911,6 +1937,175 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_depth_nodes(vc, w.tot, depth);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
+}
+
+// --------------------------------------------------------------------------------- two rays per lane
+// k_trace_dyn with two rays in flight per lane (SPTR_TRACE_PAIR; wide BVH from L2/HBM, timed passes):
+// each refill round fills the lane's two slots, and each walk step issues both slots' fetches
+// (walk_fetch) before either step proper (walk_apply), so a wave keeps twice the dependent loads in
+// flight at the occupancy two ray states allow.  Per ray the walk is the single-ray kernel's, step for
+// step (same hits, same records, same hand-off); only which lane and slot carries a ray differs.
+#ifndef SPTR_TRACE_PAIR
+#define SPTR_TRACE_PAIR 0  // r04x: bit-identical, but C5 7.9 -> 9.2 ms (4 waves/SIMD) / 10.0 (5 waves), C3 3.7 -> 3.9
+#endif
+#ifndef SPTR_TRACE2_WAVES
+#define SPTR_TRACE2_WAVES 4
+#endif
+template <bool kPrimary, bool kCube, bool kQueue>
+__global__ void __launch_bounds__(kBlock, SPTR_TRACE2_WAVES)
+    k_trace_dyn2(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  const FrameView f = frame_dyn(fin);
+  __shared__ LdsStackN<kLdsStackG> s_stack[2];
+  extern __shared__ float4 lds[];
+  __shared__ uint32_t s_cnt, s_next, s_taken;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
+  if (threadIdx.x == 0) s_cnt = s_next = s_taken = 0u;
+  const Staged sc = stage_scene<false>(sv, lds);
+  const uint32_t ntop = sv.num_top4;
+  const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, false, kPrimary, nseg_in)) : nullptr;
+  uint32_t n, per_in = 0u, nlist = 0u;
+  if (kPrimary) {
+    nlist = f.plist ? f.plist[f.P] : 0u;
+    n = f.plist ? nlist * f.k : f.P * f.k;
+    __syncthreads();
+  } else {
+    n = seg_scan(w.segN, nseg_in, s_off, per_in);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)(kPrimary ? (unsigned long long)f.valid * f.k : n));
+    const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
+    atomicAdd(&w.tot[kPrimary ? kTotTracedP : kTotTracedB], (unsigned long long)(t));
+    atomicAdd(&w.tot[kTotTracedD + stat_depth(depth)], (unsigned long long)(t));
+  }
+  const ImageDiv idiv = image_div(f);
+  const RayStream rs = w.rs[depth & 1];
+  Visits vc;
+  const Sched sd = block_sched(n);
+  const uint32_t nb = block_items(sd, n);
+  const uint32_t cap = kQueue ? 2u * sd.per : sd.per;
+  const uint32_t seg0 = logical_block() * cap;
+  XcdQueue xq = xcd_queue(w.work + kWorkTraceQueue, n);
+  TravStack<kLdsStackG> stack[2];
+  stack[0].lds = &s_stack[0].e[0][threadIdx.x];
+  stack[1].lds = &s_stack[1].e[0][threadIdx.x];
+  bool have[2] = {false, false}, done[2] = {false, false};
+  uint32_t id[2] = {0u, 0u}, pid[2] = {0u, 0u}, ref[2] = {kNoHit, kNoHit};
+  float tfar[2] = {0.0f, 0.0f};
+  Ray r[2];
+  WideWalk wk[2];
+  bool drained = false;
+  for (;;) {
+    bool more = false;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      uint32_t item = kNoHit;
+      if constexpr (kQueue) {
+        item = xcd_take(xq, !have[q], &s_taken, cap);
+        more = more || !xq.drained;
+        drained = xq.drained;
+      } else {
+        const uint32_t k = block_take(&s_next, !have[q]);
+        if (!have[q] && k < nb) item = block_item(sd, k);
+        more = more || (__ballot(!have[q] && k < nb) != 0ull);
+        if (__ballot(!have[q] && k >= nb) != 0ull) drained = true;
+      }
+      if (item != kNoHit) {
+        bool valid = true, culled = false;
+        vec3 o, d;
+        if (kPrimary) {
+          Primary pr;
+          uint32_t l, p = item;
+          if (f.plist) p = primary_item(f, nlist, item);
+          id[q] = pid[q] = p;
+          valid = primary_path(f, idiv, p, pr, l);
+          culled = !f.plist && pixel_culled(f, l);
+          o = f.cam_pos;
+          d = pr.d;
+        } else {
+          id[q] = seg_slot(s_off, nseg_in, per_in, item);
+          const float4 o4 = rs.o[id[q]], d4 = rs.d[id[q]];
+          o = xyz(o4);
+          d = xyz(d4);
+          pid[q] = __float_as_uint(d4.w);
+        }
+        if (valid) {
+          r[q] = make_ray(o, d);
+          tfar[q] = __builtin_huge_valf();
+          ref[q] = kNoHit;
+          done[q] = walk_start<false, false, true>(wk[q], sc, culled ? kNoHit : sv.root4, r[q], 0.0f, tfar[q], ref[q], vc);
+          have[q] = true;
+        }
+      }
+    }
+    if (__ballot(have[0] || have[1]) == 0ull) {
+      if (!more) break;
+      continue;
+    }
+    for (int it = 0; it < kDynSteps; ++it) {
+      const bool a0 = have[0] && !done[0], a1 = have[1] && !done[1];
+      if (__ballot(a0 || a1) == 0ull) break;
+      WalkItem i0, i1;
+      if (a0) i0 = walk_fetch(wk[0].cur, sc.nodes4, top, ntop, sc.tris, sc.sph);
+      if (a1) i1 = walk_fetch(wk[1].cur, sc.nodes4, top, ntop, sc.tris, sc.sph);
+      if (a0) done[0] = walk_apply<false, false>(wk[0], stack[0], i0, sc.prim_ref, sc.tris, sc.sph, r[0], 0.0f, tfar[0], ref[0], vc);
+      if (a1) done[1] = walk_apply<false, false>(wk[1], stack[1], i1, sc.prim_ref, sc.tris, sc.sph, r[1], 0.0f, tfar[1], ref[1], vc);
+    }
+    const bool defer = !kPrimary && w.defer_miss != 0u;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      // straggler hand-off, as in k_trace_dyn (counted over both slots of the wave's lanes)
+      if (w.strag_lanes != 0u && drained && (uint32_t)depth < kStragBounces) {
+        const unsigned long long act = __ballot((have[0] && !done[0]) || (have[1] && !done[1]));
+        if (act != 0ull && (uint32_t)__popcll(act) <= w.strag_lanes && have[q] && !done[q]) {
+          const uint32_t slot = atomicAdd(&w.work[kWorkStrag + (uint32_t)depth * 32u], 1u);
+          if (slot < w.strag_cap) {
+            float4* rec = w.strag + ((size_t)depth * w.strag_cap + slot) * kStragRec;
+            rec[3] = make_float4(__uint_as_float(wk[q].cur),
+                                 __uint_as_float((uint32_t)wk[q].sp | (wk[q].hit ? 0x10000u : 0u)), __uint_as_float(ref[q]),
+                                 tfar[q]);
+            uint32_t* st = reinterpret_cast<uint32_t*>(rec + 4);
+            for (int e = 0; e < wk[q].sp; ++e) st[e] = stack[q].get(e);
+            if (kPrimary) {
+              Primary pr;
+              (void)primary_path(f, idiv, pid[q], pr);
+              rec[0] = f4(f.cam_pos, __uint_as_float(pr.rng));
+              rec[1] = f4(r[q].d, __uint_as_float(pid[q]));
+              rec[2] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(0u));
+            } else {
+              rec[0] = rs.o[id[q]];
+              rec[1] = rs.d[id[q]];
+              rec[2] = f4(xyz(rs.thr[id[q]]), __uint_as_float((uint32_t)depth));
+            }
+            have[q] = false;
+          }
+        }
+      }
+      const bool fin = have[q] && done[q];
+      if (fin && !wk[q].hit) {
+        if (defer) {
+          if (sh.debug_mode != 1) rs.thr[id[q]] = f4(xyz(rs.thr[id[q]]) * env_color<kCube>(sh, renormalized_again(r[q].d)), 0.0f);
+        } else if (sh.debug_mode == 1) {
+          w.rad[pid[q]] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+          const vec3 e = env_color<kCube>(sh, renormalized_again(r[q].d));
+          vec3 rv;
+          if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
+          else rv = xyz(w.rad[pid[q]]) + xyz(rs.thr[id[q]]) * e;
+          w.rad[pid[q]] = f4(rv, 0.0f);
+        }
+      }
+      const bool rec = fin && (wk[q].hit || defer);
+      const uint32_t j = block_append(&s_cnt, rec);
+      if (rec) {
+        if (seg0 + j < w.hrec_cap)
+          w.hrec.put(seg0 + j, id[q], wk[q].hit ? __float_as_uint(tfar[q]) : pid[q], wk[q].hit ? ref[q] : kNoHit);
+        else w.tot[kTotOverflow] = 1ull;
+      }
+      if (fin) have[q] = false;
+    }
+  }
+  seg_publish(w.segH, &s_cnt, cap);
+  report_stack(vc, w.tot);
 }
 
 // --------------------------------------------------------------------------------- shading steps
@@ -3666,6 +3861,19 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
     const unsigned lbd = lb + (!L && W ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (as k_shadow_dyn)
     const bool queue = !L && W && sv.scene_bytes > kL2BytesPerXcd && trace_queue();
+    if constexpr (SPTR_TRACE_PAIR != 0) {
+      if (!L && W && !count && kWide == 4) {  // two rays per lane (measured slower, off: DESIGN.md §8)
+      return dispatch(
+          [&](auto fl) -> unsigned {
+            return [&]<bool Pc, bool Cube, bool Q>(Flags<Pc, Cube, Q>) {
+              const unsigned g = resident_grid((const void*)&k_trace_dyn2<Pc, Cube, Q>, lbd);
+              hipLaunchKernelGGL((k_trace_dyn2<Pc, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
+              return g;
+            }(fl);
+          },
+          Flags<>{}, P, cube, queue);
+      }
+    }
     return dispatch(
         [&](auto fl) -> unsigned {
           return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube, bool Q>(Flags<Lc, C, Pc, Wc, Cube, Q>) {
