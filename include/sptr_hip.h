@@ -230,7 +230,7 @@ int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
  * wave of a bounce trace has no rays left to start and at most `lanes` of its 64 lanes are still
  * tracing, those rays are handed to a path-per-thread kernel beside the launch chain, which traces
  * them again and finishes their paths, so the launch no longer lasts as long as its longest ray.
- * 0 = off, 1..64 (default 8).  Results do not depend on it (each path makes the same operations in
+ * 0 = off, 1..64 (default 12).  Results do not depend on it (each path makes the same operations in
  * the same order wherever it runs); sptr_stats::paths_handed_off counts the paths. */
 int sptr_set_stragglers(sptr_ctx* ctx, uint32_t lanes);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,

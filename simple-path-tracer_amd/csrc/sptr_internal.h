@@ -215,7 +215,7 @@ constexpr uint32_t kWorkWords = kWorkStrag + 32u * kStragBounces;
 // default lane threshold (a drained wave hands its rays off once this few lanes are still busy)
 constexpr uint32_t kStragCap = 1u << 17;
 constexpr uint32_t kStragRec = 4u + (uint32_t)kStack / 4u;
-constexpr uint32_t kStragLanesDefault = 8;  // r04n A/B (C5, grid 256, bounce 0): 0/8/16/32 lanes 8.03/7.76/7.95/8.48 ms
+constexpr uint32_t kStragLanesDefault = 12;  // C5, grid 256, bounce 0: r04n 0/8/16/32 lanes 8.03/7.76/7.95/8.48 ms; r04zb 4/8/12 lanes 7.96/7.83/7.73
 // bounces whose traces hand off (<= kStragBounces): a handed-off path must be finished before the
 // batch's k_accum, so the later a bounce, the less time its stragglers have beside the chain (r04n,
 // C5 at 8 lanes: bounce 0 / 0-1 / 0-2: 7.76 / 7.82 / 7.94 ms)

@@ -436,7 +436,7 @@ class Renderer:
 
     def set_stragglers(self, lanes: int):
         """sptr_set_stragglers: hand a drained wave's rays off once at most `lanes` lanes still trace
-        (0 = off, default 8); HBM-resident scenes only."""
+        (0 = off, default 12); HBM-resident scenes only."""
         self._check(self._L.sptr_set_stragglers(self._h, lanes), "set_stragglers")
 
     def set_bvh_width(self, n: int):

@@ -535,11 +535,11 @@ def test_many_calls_without_collect(renderer, mode):
         renderer.set_launch_mode(0)
 
 
-@pytest.mark.parametrize("lanes", [64, 8])
+@pytest.mark.parametrize("lanes", [64, 12])
 def test_straggler_handoff_changes_no_result(renderer, lanes):
     """Straggler hand-off (sptr_set_stragglers, scenes beyond an XCD's L2): bounce traces hand the rays
     still running in their drained waves to k_strag, which finishes those paths beside the chain.  With
-    every drained wave's rays handed off (64 lanes) and with the default (8), the accumulation is
+    every drained wave's rays handed off (64 lanes) and with the default (12), the accumulation is
     bit-identical to no hand-off, the query counts are equal, and paths were handed off — in direct
     launches (mode 1), a captured graph (mode 3) and one stream (mode 2)."""
     W, H, S = 128, 96, 8
@@ -562,7 +562,7 @@ def test_straggler_handoff_changes_no_result(renderer, lanes):
             print("stragglers", lanes, "mode", mode, "handed off", st.paths_handed_off)
     finally:
         renderer.set_launch_mode(0)
-        renderer.set_stragglers(8)
+        renderer.set_stragglers(12)
 
 
 def test_large_forked_call_launches_direct(renderer):
