@@ -99,7 +99,8 @@ def test_no_shadow_launches_no_entry(bench):
 
 
 @pytest.mark.parametrize("tag,wl", [("r03za", "c2"), ("r03za", "c4"), ("r03zf", "c3"), ("r03zf", "c5"),
-                                    ("r04p", "c2"), ("r04p", "c4"), ("r04p", "c5"), ("r04q", "c2"), ("r04q", "c4"), ("r04q", "c5")])
+                                    ("r04p", "c2"), ("r04p", "c4"), ("r04p", "c5"), ("r04q", "c2"), ("r04q", "c4"), ("r04q", "c5"),
+                                    ("r04z", "c2"), ("r04z", "c4"), ("r04z", "c5")])
 def test_committed_lines_recompute_from_kernel_stats(tag, wl):
     """Each committed bench line's roofline fraction recomputes from the rocprofv3 kernel statistics of
     the same session (tools/recompute_roofline.py: the timed-path instantiations pooled over their
