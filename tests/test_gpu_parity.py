@@ -731,3 +731,19 @@ def test_split_references_change_no_result(renderer):
     assert np.array_equal(o1, o16)
     assert (rgb1 == rgb16).all(axis=2).mean() >= 0.9999
     assert abs(int(st1.rays_closest) - int(st16.rays_closest)) <= 1e-4 * st1.rays_closest
+
+
+def test_setter_argument_checks(renderer):
+    """The r04 setters refuse out-of-range values with a message and leave the context usable."""
+    with pytest.raises(sptr.SptrError, match="straggler lanes"):
+        renderer.set_stragglers(65)
+    with pytest.raises(sptr.SptrError, match="launch mode"):
+        renderer.set_launch_mode(4)
+    with pytest.raises(sptr.SptrError, match="split references"):
+        renderer.set_split_refs(3)
+    renderer.set_stragglers(12)
+    renderer.set_launch_mode(0)
+    W, H = 64, 48
+    sptr.setup_default(renderer, "default")
+    st = renderer.render(sptr.camera_lookat(aspect=W / H), W, H, spp=1)
+    assert st.samples == W * H
