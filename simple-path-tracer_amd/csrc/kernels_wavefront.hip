@@ -915,6 +915,27 @@ __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv
   return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
 }
 
+// traverse_w with the wide BVH's top levels read from an LDS copy (stage_top; ntop = 0: none) — the
+// path-per-thread kernels of L2/HBM scenes (k_tail, k_strag), whose every ray starts at the root
+#ifndef SPTR_TAIL_TOP
+#define SPTR_TAIL_TOP 1
+#endif
+template <bool kW4, bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool traverse_w_top(const Staged& sc, const SceneView& sv, const uint4* top, uint32_t ntop,
+                                               const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
+                                               LdsStackN<N>& ls) {
+  if constexpr (kW4) {
+    WideWalk wk;
+    if (wide_start<kAny, kCount>(wk, sv.root4, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc)) return wk.hit;
+    TravStack<N> stack;
+    stack.lds = &ls.e[0][threadIdx.x];
+    (void)wide_walk<kAny, kCount>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
+                                  0x7FFFFFFF);
+    return wk.hit;
+  }
+  return traverse<kAny, kCount>(sc.nodes, sc.prim_ref, sc.tris, sc.sph, sv.root, r, tnear, tfar, ref, vc, ls);
+}
+
 // Per-bounce and per-ray statistics (sptr_stats traced_by_depth / nodes_by_depth / *_visit_hist).
 __device__ __forceinline__ uint32_t stat_depth(int depth) { return depth < kStatDepths - 1 ? (uint32_t)depth : kStatDepths - 1u; }
 // The instrumented pass bins every ray's node visits into a block-local LDS histogram (s_hist, zeroed
@@ -2698,6 +2719,9 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   if (threadIdx.x < 2u) s_rays[threadIdx.x] = 0u;
   if (threadIdx.x == 0u) s_next = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
+  // the wide BVH's top levels in LDS (L2/HBM scenes), published by seg_scan's barriers
+  const uint32_t ntop = (SPTR_TAIL_TOP && kW4 && !kLds) ? sv.num_top4 : 0u;
+  const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, kLds, false, nseg_in)) : nullptr;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
   const RayStream rin = w.rs[depth0 & 1];
@@ -2733,7 +2757,7 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
       ++n_closest;
       float tfar = __builtin_huge_valf();
       uint32_t ref = kNoHit;
-      const bool hit = traverse_w<kW4, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
+      const bool hit = traverse_w_top<kW4, false, false>(sc, sv, top, ntop, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
       if (sh.debug_mode == 1) {  // hit/miss visualisation (never continues past bounce 0)
         radv = hit ? v3(1.0f, 1.0f, 1.0f) : v3(0.0f, 0.0f, 0.0f);
         loaded = true;
@@ -2757,7 +2781,7 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
         if (!light_term(sh.lights[li], sf, view, thr, so, ldir, st, contrib)) continue;
         ++n_shadow;
         uint32_t sref = kNoHit;
-        if (!traverse_w<kW4, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
+        if (!traverse_w_top<kW4, true, false>(sc, sv, top, ntop, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
           radv = radv + contrib;
       }
       vec3 no, nd;
@@ -2808,6 +2832,9 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
   if (threadIdx.x < 2u) s_rays[threadIdx.x] = 0u;
   if (threadIdx.x == 0u) s_next = 0u;
   const Staged sc = stage_scene<false>(sv, nullptr);
+  extern __shared__ float4 lds[];
+  const uint32_t ntop = SPTR_TAIL_TOP ? sv.num_top4 : 0u;
+  const uint4* top = ntop ? stage_top(sv, lds) : nullptr;
   __syncthreads();
   const uint32_t n = min(w.work[kWorkStrag + (uint32_t)depth0 * 32u], w.strag_cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&w.tot[kTotStrag], (unsigned long long)n);
@@ -2858,12 +2885,12 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
       if (first) {  // the handed-off ray: its walk resumes where k_trace_dyn left it (the same walk kind)
         tfar = tfar0;
         ref = ref0;
-        (void)walk_steps<false, true, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, nullptr, 0u, make_ray(ro, rd), 0.0f,
+        (void)walk_steps<false, true, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, top, ntop, make_ray(ro, rd), 0.0f,
                                                                   tfar, ref, vr, 0x7FFFFFFF);
         hit = wk.hit;
       } else {
         ++n_closest;
-        hit = traverse_w<kW4, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
+        hit = traverse_w_top<kW4, false, false>(sc, sv, top, ntop, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack);
       }
       first = false;
       if (sh.debug_mode == 1) {
@@ -2889,7 +2916,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv,
         if (!light_term(sh.lights[li], sf, view, thr, so, ldir, st, contrib)) continue;
         ++n_shadow;
         uint32_t sref = kNoHit;
-        if (!traverse_w<kW4, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
+        if (!traverse_w_top<kW4, true, false>(sc, sv, top, ntop, make_ray(so, ldir), 1e-4f, st, sref, vc, s_stack))
           radv = radv + contrib;
       }
       vec3 no, nd;
@@ -3989,7 +4016,8 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
 unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth0,
                      uint32_t nseg, hipStream_t s) {
   const bool L = sv.lds_bytes != 0;
-  const unsigned lb = trace_lds(sv, L, false, nseg);
+  const bool W = sv.width == (uint32_t)kWide;
+  const unsigned lb = trace_lds(sv, L, false, nseg) + ((SPTR_TAIL_TOP && !L && W) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);
   return dispatch(
       [&](auto fl) -> unsigned {
         return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
@@ -4015,8 +4043,9 @@ bool strag_applies(const SceneView& sv) {
 void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s) {
   constexpr unsigned kStragGrid = SPTR_STRAG_GRID;
-  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_strag<true, true>), dim3(kStragGrid), dim3(kBlock), 0, s, sv, sh, f, w, depth);
-  else hipLaunchKernelGGL((k_strag<true, false>), dim3(kStragGrid), dim3(kBlock), 0, s, sv, sh, f, w, depth);
+  const unsigned lb = SPTR_TAIL_TOP ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u;  // the top levels in LDS
+  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_strag<true, true>), dim3(kStragGrid), dim3(kBlock), lb, s, sv, sh, f, w, depth);
+  else hipLaunchKernelGGL((k_strag<true, false>), dim3(kStragGrid), dim3(kBlock), lb, s, sv, sh, f, w, depth);
 }
 
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s) {

@@ -11,7 +11,7 @@ for v in "$@"; do
 done
 for rep in 1 2; do
 for v in base "$@"; do
-  lib=$GRAFT_REPO_ROOT/variants/$v/libsptr_hip.so
+  lib=$GRAFT_REPO_ROOT/variants/$v/libsptr_hip.so; [ -f $lib ] || lib=$GRAFT_REPO_ROOT/simple-path-tracer_amd/libsptr_hip.so
   for wl in c5 c3; do
     SPTR_LIB=$lib timeout -k 10 300 python3 bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-interactive --no-serial-pass \
       > $o/${wl}_$v.json 2> $o/${wl}_$v.err || { tail -5 $o/${wl}_$v.err; exit 4; }
