@@ -565,6 +565,34 @@ def test_straggler_handoff_changes_no_result(renderer, lanes):
         renderer.set_stragglers(12)
 
 
+def test_straggler_handoff_multibatch(renderer):
+    """Hand-off in a call of several sample batches (set_wave_paths: 4 samples per batch): each batch's
+    k_strag is joined before that batch's k_accum, which zeroes the counts for the next batch; the
+    accumulation equals the one-batch call without hand-off, bit for bit, direct and captured."""
+    W, H, S = 96, 64, 16
+    sptr.setup_default(renderer, "sphere_mesh", 300, 600)
+    cam = sptr.camera_lookat(aspect=W / H)
+    P = 3 * 2 * 1024  # local pixels: 3 x 2 tiles
+    try:
+        renderer.set_stragglers(0)
+        st0 = renderer.render(cam, W, H, spp=S)
+        ref = renderer.read_accum().copy()
+        renderer.set_stragglers(64)
+        renderer.set_wave_paths(P * 4)
+        for mode in (1, 3):
+            renderer.set_launch_mode(mode)
+            for _ in range(3):
+                st = renderer.render(cam, W, H, spp=S)
+                assert st.waves == S // 4
+                assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32)), mode
+                assert (st.rays_closest, st.rays_shadow) == (st0.rays_closest, st0.rays_shadow), mode
+                assert st.paths_handed_off > 0, mode
+    finally:
+        renderer.set_wave_paths(0)
+        renderer.set_launch_mode(0)
+        renderer.set_stragglers(12)
+
+
 def test_large_forked_call_launches_direct(renderer):
     """Launch mode 0 leaves a large call whose launches fork to the side streams (here 8.4 M samples,
     the shadow launches beside the traces of the L2-resident sphere mesh) to direct launches — the
