@@ -2822,8 +2822,11 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
 // itself was counted by its trace launch; the later bounces' closest-hit and the any-hit queries are
 // added to the totals here (atomics: k_shadow_dyn may be updating the per-block tallies meanwhile).
 static_assert(SPTR_PRIMARY_UNIFIED == 1 || SPTR_WALK_UNIFIED == 0, "k_strag resumes camera and bounce rays with one walk kind");
+#ifndef SPTR_STRAG_WAVES
+#define SPTR_STRAG_WAVES SPTR_TAIL_WAVES
+#endif
 template <bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, SPTR_TAIL_WAVES) k_strag(SceneView sv, ShadeView sh, FrameView f, WaveView w,
+__global__ void __launch_bounds__(kBlock, SPTR_STRAG_WAVES) k_strag(SceneView sv, ShadeView sh, FrameView f, WaveView w,
                                                                     int depth0) {
   __shared__ KernelStack<false> s_stack;
   __shared__ DevMaterial smat[32];
