@@ -1462,8 +1462,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // chunks round-robin).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
 // 289 us, 8 lanes 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
-template <bool kLds, bool kCount, bool kW4, bool kCube>
-__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_WP_WAVES)
+// kHiOcc: 8 waves/SIMD for shards whose pixels fill the resident waves only a few times (r04u: the
+// 8-way C2 shard 0.554 -> 0.541 ms, while 2- and 4-way shards lose ~1.5 % at 8 waves)
+template <bool kLds, bool kCount, bool kW4, bool kCube, bool kHiOcc = false>
+__global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 : SPTR_TRACE_WP_WAVES))
     k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
@@ -3794,6 +3796,9 @@ constexpr uint32_t kPixelMajorMaxK = 128;  // samples per batch above which < 8 
 // Lane-group bounce 0 (k_trace_wp) from this many samples per batch: 8 lanes take 8 samples of one
 // pixel per round, so smaller batches would leave lanes idle.
 constexpr uint32_t kWaveFoldMinK = 16;
+// k_trace_wp runs at 8 waves/SIMD when the shard's pixels fill the 7-wave resident grid's 8-pixel wave
+// groups fewer than this many times (1080p: G = 8 ~4.5 rounds, G = 4 ~9, G = 2 ~18)
+constexpr uint64_t kWpHiOccRounds = 6;
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f) {
 #ifdef SPTR_EXPERIMENT_KNOBS
   if (const char* e = getenv("SPTR_FOLD")) {  // timing experiments: force kFoldNone/Thread/Wave
@@ -3866,15 +3871,22 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   const unsigned lb = trace_lds(sv, L, P, nseg);
   const EnvView ev = sh.env;
   if (P && f.pixel_major == kFoldWave) {
+    // rounds of 8-pixel wave groups over the resident grid: few rounds (a small shard) -> 8 waves/SIMD
+    const unsigned g7 = resident_grid((const void*)&k_trace_wp<true, false, false, false>, lb);
+    const bool hi = L && !W && (uint64_t)f.P < (uint64_t)g7 * (kBlock / 64u) * 8u * kWpHiOccRounds;
     return dispatch(
         [&](auto fl) -> unsigned {
-          return [&]<bool Lc, bool C, bool Wc, bool Cube>(Flags<Lc, C, Wc, Cube>) {
-            const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube>, lb);
-            hipLaunchKernelGGL((k_trace_wp<Lc, C, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w);
-            return g;
+          return [&]<bool Lc, bool C, bool Wc, bool Cube, bool Hi>(Flags<Lc, C, Wc, Cube, Hi>) {
+            if constexpr (Hi && (Wc || !Lc)) {
+              return 0u;  // not instantiated: the high-occupancy form is for LDS-staged BVH2 scenes
+            } else {
+              const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube, Hi>, lb);
+              hipLaunchKernelGGL((k_trace_wp<Lc, C, Wc, Cube, Hi>), dim3(g), b, lb, s, sv, ev, f, w);
+              return g;
+            }
           }(fl);
         },
-        Flags<>{}, L, count, W, cube);
+        Flags<>{}, L, count, W, cube, hi);
   }
   if (P && L && f.pixel_major == kFoldThread) {
     return dispatch(
