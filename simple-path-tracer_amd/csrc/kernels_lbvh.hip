@@ -20,13 +20,13 @@
 //                   Guideline 16 R1)
 //   k_treelet     : (L2/HBM scenes) SAH treelet restructuring after k_refit, bottom-up by subtree height, 3 passes;
 //                   never deepens a subtree (k_heights, k_height_count / k_height_scatter order the launches)
-//   k_wide_count + scan + k_wide_emit, one wide level at a time (SPTR_WIDE_GREEDY, the default):
-//                   wide BVH (4 or 8 children) by the greedy surface-area collapse — a wide node
-//                   opens its largest-area internal child until it has kWide children; leaves stay
-//                   ranges; wide nodes are numbered level by level (top levels first)
-//   k_depth_wide + scans + k_wide_index + k_collapse_wide (SPTR_WIDE_GREEDY=0): fixed collapse —
-//                   every reachable BVH2 node at a depth that is a multiple of kWideLevels becomes a
-//                   wide node whose children are its descendants kWideLevels levels down
+//   k_wide_count + scan + k_wide_emit, one wide level at a time: wide BVH (4 children) by the greedy
+//                   surface-area collapse — a wide node opens its largest-area internal child until
+//                   it has kWide children; single-primitive leaves become direct links, others stay
+//                   ranges; wide nodes are numbered level by level (top levels first).  (r02i: the
+//                   fixed collapse of every second LBVH level it replaced left nodes half empty:
+//                   C5 15.58 -> 15.38 ms/step; opening by area x primitives and a host-built SAH BVH2
+//                   were A/B-only experiments, removed r05.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,24 +37,9 @@
 
 #include "sptr_internal.h"
 
-#ifndef SPTR_GREEDY_WEIGHT
-#define SPTR_GREEDY_WEIGHT 0  // 1: the greedy collapse opens the child of largest area x primitives
-#endif
-#ifndef SPTR_EXPERIMENT_HOST_SAH
-#define SPTR_EXPERIMENT_HOST_SAH 0
-#endif
-#ifndef SPTR_WIDE_DIRECT
-#define SPTR_WIDE_DIRECT 1  // wide single-primitive leaves as direct links (0: prim_ref ranges, A/B builds)
-#endif
-#ifndef SPTR_WIDE_GREEDY
-#define SPTR_WIDE_GREEDY 1  // 0: every kWideLevels-th LBVH level becomes a wide level (A/B builds)
-#endif
-#ifndef SPTR_TREELET_HCAP
-#define SPTR_TREELET_HCAP 0  // a restructured treelet may deepen its subtree up to this height (A/B builds)
-#endif
-#ifndef SPTR_TREELET
-#define SPTR_TREELET 5  // treelet size (leaves) of the SAH restructuring of L2/HBM scenes' LBVH; 0: off (r03u/v A/B)
-#endif
+// treelet size (leaves) of the SAH restructuring of L2/HBM scenes' LBVH (r03u/v A/B); a restructured
+// treelet never deepens its subtree
+constexpr int kTreeletLeaves = 5;
 
 namespace sptr {
 
@@ -730,7 +715,7 @@ __global__ void __launch_bounds__(kTreeletBlock) k_treelet(const uint32_t* order
     // kept unless cheaper and no deeper: the traversal stacks are sized by the tree height (the wide
     // collapse of a deeper tree can exceed the BVH4 stack bound, sptr_internal.h kStack)
     const uint32_t h_old = max(h_l, h_r) + 1u, h_new = (uint32_t)(s_part[full][t] >> 8);
-    if (!(opt < cur * 0.99999f) || (h_new > h_old && h_new > (uint32_t)SPTR_TREELET_HCAP)) {
+    if (!(opt < cur * 0.99999f) || h_new > h_old) {
       cost[x] = cur;
       newh[x] = max(h_l, h_r) + 1u;
       continue;
@@ -786,35 +771,6 @@ __global__ void __launch_bounds__(kTreeletBlock) k_treelet(const uint32_t* order
   }
 }
 
-// Wide collapse, pass 1: keep[i] = 1 for BVH2 nodes that are reachable through internal links
-// (covering more than leaf_max primitives) and lie at a depth that is a multiple of kWideLevels;
-// top[i] = 1 for the kept nodes of the top kTopLevels wide levels.
-__global__ void k_depth_wide(int N, uint32_t leaf_max, const BvhNode* nodes, uint32_t* keep, uint32_t* top) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
-    uint32_t k = 0u, t = 0u;
-    if (nodes[i].link.w > leaf_max) {
-      uint32_t dep = 0u, q = (uint32_t)i;
-      while (q != 0u) {
-        q = nodes[q].link.z;
-        ++dep;
-      }
-      k = (dep % (uint32_t)kWideLevels) ? 0u : 1u;
-      t = k && dep / (uint32_t)kWideLevels < (uint32_t)kTopLevels ? 1u : 0u;
-    }
-    keep[i] = k;
-    top[i] = t;
-  }
-}
-
-// Wide collapse, pass 1b: wide index of kept node i — the top-level nodes first (0..ntop-1, in
-// BVH2 index order, so the root stays 0), then the others in BVH2 index order.  slot / tslot: the
-// exclusive scans of keep / top; ntop comes from the last elements.
-__global__ void k_wide_index(int N, const uint32_t* keep, const uint32_t* top, uint32_t* slot, const uint32_t* tslot) {
-  const uint32_t ntop = tslot[N - 2] + top[N - 2];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x)
-    if (keep[i]) slot[i] = top[i] ? tslot[i] : ntop + (slot[i] - tslot[i]);
-}
-
 struct WideBoxes {
   float lo[3][kWide], hi[3][kWide];
   uint32_t link[kWide];
@@ -866,78 +822,12 @@ __device__ __forceinline__ WideNode quantize_wide(const WideBoxes& b, int n, uin
   return o;
 }
 
-// Wide collapse, pass 2: node i (kept) -> wide node idx[i]; its children are the BVH2 nodes
-// kWideLevels levels down (kept themselves), or the leaf ranges met on the way, in left-to-right
-// order.
-__global__ void k_collapse_wide(int N, const BvhNode* nodes, const uint32_t* keep, const uint32_t* idx, WideNode* out) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N - 1; i += gridDim.x * blockDim.x) {
-    if (!keep[i]) continue;
-    WideBoxes b;
-    for (int k = 0; k < kWide; ++k) {
-      b.link[k] = kNoHit;
-      for (int a = 0; a < 3; ++a) b.lo[a][k] = b.hi[a][k] = 0.0f;
-    }
-    // level 1: the two children of node i
-    const BvhNode nd = nodes[i];
-    int n = 2;
-    b.link[0] = nd.link.x;
-    b.lo[0][0] = nd.lxy.x; b.hi[0][0] = nd.lxy.y; b.lo[1][0] = nd.lxy.z; b.hi[1][0] = nd.lxy.w;
-    b.lo[2][0] = nd.z.x;   b.hi[2][0] = nd.z.y;
-    b.link[1] = nd.link.y;
-    b.lo[0][1] = nd.rxy.x; b.hi[0][1] = nd.rxy.y; b.lo[1][1] = nd.rxy.z; b.hi[1][1] = nd.rxy.w;
-    b.lo[2][1] = nd.z.z;   b.hi[2][1] = nd.z.w;
-    // further levels: every internal entry is replaced by its two children, in place order
-    for (int lev = 1; lev < kWideLevels; ++lev) {
-      WideBoxes nb;
-      int m = 0;
-      for (int e = 0; e < n; ++e) {
-        const uint32_t c = b.link[e];
-        if (c & kLeafBit) {
-          nb.link[m] = c;
-          for (int a = 0; a < 3; ++a) {
-            nb.lo[a][m] = b.lo[a][e];
-            nb.hi[a][m] = b.hi[a][e];
-          }
-          ++m;
-          continue;
-        }
-        const BvhNode cn = nodes[c];
-        nb.link[m] = cn.link.x;
-        nb.lo[0][m] = cn.lxy.x; nb.hi[0][m] = cn.lxy.y; nb.lo[1][m] = cn.lxy.z; nb.hi[1][m] = cn.lxy.w;
-        nb.lo[2][m] = cn.z.x;   nb.hi[2][m] = cn.z.y;
-        ++m;
-        nb.link[m] = cn.link.y;
-        nb.lo[0][m] = cn.rxy.x; nb.hi[0][m] = cn.rxy.y; nb.lo[1][m] = cn.rxy.z; nb.hi[1][m] = cn.rxy.w;
-        nb.lo[2][m] = cn.z.z;   nb.hi[2][m] = cn.z.w;
-        ++m;
-      }
-      for (int e = 0; e < m; ++e) {
-        b.link[e] = nb.link[e];
-        for (int a = 0; a < 3; ++a) {
-          b.lo[a][e] = nb.lo[a][e];
-          b.hi[a][e] = nb.hi[a][e];
-        }
-      }
-      n = m;
-    }
-    for (int e = 0; e < n; ++e)
-      if (!(b.link[e] & kLeafBit)) b.link[e] = idx[b.link[e]];  // kept nodes kWideLevels below
-    uint32_t par = kNoHit;
-    if (i != 0) {
-      uint32_t q = (uint32_t)i;
-      for (int l = 0; l < kWideLevels; ++l) q = nodes[q].link.z;
-      par = idx[q];
-    }
-    out[idx[i]] = quantize_wide(b, n, par);
-  }
-}
-
-// Greedy surface-area collapse (SPTR_WIDE_GREEDY), top-down one wide level per launch pair: a wide
+// Greedy surface-area collapse, top-down one wide level per launch pair: a wide
 // node's child list starts as its BVH2 node's two children and grows, up to kWide entries, by
 // opening the internal entry whose box has the largest surface area (lowest slot on ties) — it is
 // replaced in place by its left and right children, so the list stays in left-to-right order.
-// Unlike the fixed two-level collapse this fills nodes whose grandchildren include leaves and
-// spends the wide levels where the big boxes are, so deep LBVH chains give shallower wide trees.
+// Unlike a fixed two-level collapse this fills nodes whose grandchildren include leaves and spends
+// the wide levels where the big boxes are, so deep LBVH chains give shallower wide trees.
 // Its internal entries become the next level's wide nodes.
 __device__ __forceinline__ float box_area(const WideBoxes& b, int e) {
   const float dx = b.hi[0][e] - b.lo[0][e], dy = b.hi[1][e] - b.lo[1][e], dz = b.hi[2][e] - b.lo[2][e];
@@ -968,10 +858,7 @@ __device__ int expand_greedy(const BvhNode* nodes, uint32_t node, WideBoxes& b) 
     float ba = -1.0f;
     for (int e = 0; e < n; ++e)
       if (!(b.link[e] & kLeafBit)) {
-        float a = box_area(b, e);
-#if SPTR_GREEDY_WEIGHT
-        a *= (float)nodes[b.link[e]].link.w;  // area x primitives: the child's SAH cost term
-#endif
+        const float a = box_area(b, e);
         if (a > ba) {
           ba = a;
           best = e;
@@ -1005,9 +892,9 @@ __global__ void k_wide_count(uint32_t ncur, const uint2* cur, const BvhNode* nod
 // pass 2: wide node base + j; its m-th internal child becomes next[off[j] + m] = wide node
 // base + ncur + off[j] + m of the next level
 // Single-primitive leaf children become direct links (the primitive's ref in the link: its test
-// needs no prim_ref load) when `direct` (SPTR_WIDE_DIRECT).
+// needs no prim_ref load; r03: C5 13.58 -> 12.29 ms/step).
 __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, const BvhNode* nodes, const uint32_t* off,
-                            uint2* next, WideNode* out, const uint32_t* prim_ref, uint32_t direct) {
+                            uint2* next, WideNode* out, const uint32_t* prim_ref) {
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ncur; j += gridDim.x * blockDim.x) {
     WideBoxes b;
     const int n = expand_greedy(nodes, cur[j].x, b);
@@ -1017,7 +904,7 @@ __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, cons
         next[m] = make_uint2(b.link[e], base + j);
         b.link[e] = base + ncur + m;
         ++m;
-      } else if (direct && (b.link[e] & kLeafRangeMask) == 0u) {
+      } else if ((b.link[e] & kLeafRangeMask) == 0u) {
         const uint32_t ref = prim_ref[(b.link[e] & ~kLeafBit) >> kLeafCountBits];
         b.link[e] = kLeafBit | ((ref & kIndexMask) << kLeafCountBits) | kLeafDirect |
                     ((ref & kSphereBit) ? kLeafDirectSphere : 0u);
@@ -1025,150 +912,6 @@ __global__ void k_wide_emit(uint32_t ncur, const uint2* cur, uint32_t base, cons
     out[base + j] = quantize_wide(b, n, cur[j].y);
   }
 }
-
-#if SPTR_EXPERIMENT_HOST_SAH
-// Timing experiment only (A/B builds): a binned-SAH BVH2 built on the host over the primitives'
-// centroids (16 bins per axis, single-primitive leaves), numbered in preorder from the root (node 0),
-// to measure what BVH2 quality is worth for the device traversal against the Karras LBVH.  Output: the
-// leaf order of the primitives (order[i] = primitive at sorted position i), the nodes with boxes and
-// links (leaf links are ranges of one sorted position), and the tree height.
-struct HostBox {
-  float lo[3], hi[3];
-};
-static void host_sah(const float* pos, const uint32_t* idx, uint32_t ntri, const float* sph, uint32_t nsph,
-                     std::vector<uint32_t>& order, std::vector<BvhNode>& nodes, uint32_t& height) {
-  const uint32_t N = ntri + nsph;
-  std::vector<HostBox> box(N);
-  std::vector<float> cen((size_t)N * 3);
-  for (uint32_t i = 0; i < N; ++i) {
-    HostBox b;
-    if (i < ntri) {
-      for (int a = 0; a < 3; ++a) {
-        float v0 = pos[3 * idx[3 * i] + a], v1 = pos[3 * idx[3 * i + 1] + a], v2 = pos[3 * idx[3 * i + 2] + a];
-        b.lo[a] = std::min(v0, std::min(v1, v2));
-        b.hi[a] = std::max(v0, std::max(v1, v2));
-      }
-    } else {
-      const float* q = sph + 4 * (i - ntri);
-      for (int a = 0; a < 3; ++a) {
-        b.lo[a] = q[a] - q[3];
-        b.hi[a] = q[a] + q[3];
-      }
-    }
-    box[i] = b;
-    for (int a = 0; a < 3; ++a) cen[(size_t)i * 3 + a] = 0.5f * (b.lo[a] + b.hi[a]);
-  }
-  order.resize(N);
-  for (uint32_t i = 0; i < N; ++i) order[i] = i;
-  nodes.assign(N - 1, BvhNode{});
-  auto area = [](const HostBox& b) {
-    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
-    return dx * dy + dy * dz + dz * dx;
-  };
-  auto grow = [](HostBox& a, const HostBox& b) {
-    for (int k = 0; k < 3; ++k) {
-      a.lo[k] = std::min(a.lo[k], b.lo[k]);
-      a.hi[k] = std::max(a.hi[k], b.hi[k]);
-    }
-  };
-  const HostBox empty{{FLT_MAX, FLT_MAX, FLT_MAX}, {-FLT_MAX, -FLT_MAX, -FLT_MAX}};
-  struct Task {
-    uint32_t lo, hi, node, depth;  // range [lo, hi) becomes node
-  };
-  uint32_t next = 1;
-  height = 0;
-  std::vector<Task> st{{0u, N, 0u, 0u}};
-  // returns the link of range [lo, hi) and its box (one primitive: a leaf; else a new node index)
-  auto child = [&](uint32_t lo, uint32_t hi, uint32_t depth, HostBox& b, std::vector<Task>& stk) -> uint32_t {
-    b = empty;
-    for (uint32_t i = lo; i < hi; ++i) grow(b, box[order[i]]);
-    if (hi - lo == 1) {
-      height = std::max(height, depth);
-      return kLeafBit | (lo << kLeafCountBits);
-    }
-    const uint32_t id = next++;
-    stk.push_back(Task{lo, hi, id, depth});
-    return id;
-  };
-  while (!st.empty()) {
-    const Task t = st.back();
-    st.pop_back();
-    const uint32_t n = t.hi - t.lo;
-    HostBox cb = empty;
-    for (uint32_t i = t.lo; i < t.hi; ++i)
-      for (int a = 0; a < 3; ++a) {
-        cb.lo[a] = std::min(cb.lo[a], cen[(size_t)order[i] * 3 + a]);
-        cb.hi[a] = std::max(cb.hi[a], cen[(size_t)order[i] * 3 + a]);
-      }
-    constexpr int B = 16;
-    float best = FLT_MAX;
-    int bax = -1, bsplit = 0;
-    for (int a = 0; a < 3; ++a) {
-      const float ext = cb.hi[a] - cb.lo[a];
-      if (!(ext > 0.0f)) continue;
-      HostBox bb[B];
-      uint32_t bc[B] = {0};
-      for (int k = 0; k < B; ++k) bb[k] = empty;
-      for (uint32_t i = t.lo; i < t.hi; ++i) {
-        int k = (int)((cen[(size_t)order[i] * 3 + a] - cb.lo[a]) / ext * B);
-        k = std::min(std::max(k, 0), B - 1);
-        grow(bb[k], box[order[i]]);
-        ++bc[k];
-      }
-      HostBox L = empty;
-      uint32_t nl = 0;
-      float al[B];
-      uint32_t cl[B];
-      for (int k = 0; k < B - 1; ++k) {
-        grow(L, bb[k]);
-        nl += bc[k];
-        al[k] = nl ? area(L) : 0.0f;
-        cl[k] = nl;
-      }
-      HostBox R = empty;
-      uint32_t nr = 0;
-      for (int k = B - 1; k >= 1; --k) {
-        grow(R, bb[k]);
-        nr += bc[k];
-        if (cl[k - 1] == 0 || nr == 0) continue;
-        const float cost = al[k - 1] * (float)cl[k - 1] + area(R) * (float)nr;
-        if (cost < best) {
-          best = cost;
-          bax = a;
-          bsplit = k;
-        }
-      }
-    }
-    uint32_t mid;
-    if (bax < 0) {
-      mid = t.lo + n / 2;
-    } else {
-      const float ext = cb.hi[bax] - cb.lo[bax];
-      auto it = std::partition(order.begin() + t.lo, order.begin() + t.hi, [&](uint32_t pi) {
-        int k = (int)((cen[(size_t)pi * 3 + bax] - cb.lo[bax]) / ext * B);
-        k = std::min(std::max(k, 0), B - 1);
-        return k < bsplit;
-      });
-      mid = (uint32_t)(it - order.begin());
-      if (mid == t.lo || mid == t.hi) mid = t.lo + n / 2;
-    }
-    HostBox lb, rb;
-    BvhNode nd{};
-    const uint32_t l = child(t.lo, mid, t.depth + 1, lb, st);
-    const uint32_t r = child(mid, t.hi, t.depth + 1, rb, st);
-    nd.lxy = make_float4(lb.lo[0], lb.hi[0], lb.lo[1], lb.hi[1]);
-    nd.rxy = make_float4(rb.lo[0], rb.hi[0], rb.lo[1], rb.hi[1]);
-    nd.z = make_float4(lb.lo[2], lb.hi[2], rb.lo[2], rb.hi[2]);
-    nd.link = make_uint4(l, r, kNoHit, n);
-    nodes[t.node] = nd;
-  }
-  for (uint32_t i = 0; i < N - 1; ++i) {
-    const BvhNode& nd = nodes[i];
-    if (!(nd.link.x & kLeafBit)) nodes[nd.link.x].link.z = i;
-    if (!(nd.link.y & kLeafBit)) nodes[nd.link.y].link.z = i;
-  }
-}
-#endif
 
 struct Tmp {
   std::vector<void*> ptrs;
@@ -1250,7 +993,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   hipLaunchKernelGGL(k_prim_bounds, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi);
   const bool small = ((uint64_t)(NP - 1) * 64 + (uint64_t)ntris * 48 + (uint64_t)nsph * 16 + ((uint64_t)NP + 3) / 4 * 16) <=
                      kLdsSceneBytes;
-  const uint32_t max_pieces = (small || SPTR_EXPERIMENT_HOST_SAH || (c.leaf_size != 0 && c.leaf_size != 1))
+  const uint32_t max_pieces = (small || (c.leaf_size != 0 && c.leaf_size != 1))
                                   ? 1u : std::min<uint32_t>(c.split_pieces, 1u << kMaxSplitDepth);
   hipLaunchKernelGGL(k_split_count, dim3(blocks_for(NP)), dim3(256), 0, s, in, pblo, pbhi, max_pieces, rcnt);
   size_t rbytes = 0;
@@ -1311,16 +1054,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   void* tstore = nullptr;
   LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&tstore), tbytes));
   LB_CHECK(radix_sort_pairs_u64(tstore, tbytes, keys, keys_s, vals, vals_s, NR, s));
-#if SPTR_EXPERIMENT_HOST_SAH
-  std::vector<uint32_t> sah_order;
-  std::vector<BvhNode> sah_nodes;
-  uint32_t sah_height = 0;
-  const bool use_sah = NP > 1 && c.leaf_size != 8 && !small;
-  if (use_sah) {  // (no split references in this experiment: references = primitives)
-    host_sah(h_pos, h_idx, ntris, h_sph, nsph, sah_order, sah_nodes, sah_height);
-    LB_CHECK(hipMemcpyAsync(vals_s, sah_order.data(), (size_t)NP * 4, hipMemcpyHostToDevice, s));
-  }
-#endif
   hipLaunchKernelGGL(k_is_tri, dim3(blocks_for(NR)), dim3(256), 0, s, NR, ntris, vals_s, rprim, flag);
   size_t sbytes = 0;
   LB_CHECK(scan_u32(nullptr, sbytes, flag, slot, NR, s));
@@ -1346,7 +1079,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
   // to be staged in LDS (fewer, divergence-free node steps), single primitives for meshes traversed
   // from L2/HBM (with the greedy wide collapse: C5 14.9 -> 13.9, C3 5.04 -> 4.87 ms/step vs 2)
   const uint32_t auto_leaf = ((uint64_t)(N > 1 ? N - 1 : 0) * 64 + (uint64_t)ntri_refs * 48 + (uint64_t)nsph * 16 +
-                              ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : (SPTR_WIDE_GREEDY ? 1u : 2u);
+                              ((uint64_t)N + 3) / 4 * 16) <= kLdsSceneBytes ? 8u : 1u;
   const uint32_t leaf_max = std::max(1u, std::min(c.leaf_size ? c.leaf_size : auto_leaf, kMaxLeafSize));
   c.leaf_used = leaf_max;
   if (N == 1) {
@@ -1360,13 +1093,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
     BvhNode* nodes = static_cast<BvhNode*>(c.nodes.p);
     LB_CHECK(hipMemsetAsync(nodes, 0, (size_t)(N - 1) * sizeof(BvhNode), s));
     uint32_t dep = 0;
-#if SPTR_EXPERIMENT_HOST_SAH
-    if (use_sah) {
-      LB_CHECK(hipMemcpyAsync(nodes, sah_nodes.data(), (size_t)(N - 1) * sizeof(BvhNode), hipMemcpyHostToDevice, s));
-      LB_CHECK(hipStreamSynchronize(s));
-      dep = sah_height;
-    } else
-#endif
     {
       LB_CHECK(hipMemsetAsync(rflags, 0, (size_t)N * 4, s));
       hipLaunchKernelGGL(k_karras, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, keys_s, leaf_max, nodes, kids,
@@ -1376,7 +1102,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       LB_CHECK(hipGetLastError());
       LB_CHECK(hipMemcpyAsync(&dep, dmax, 4, hipMemcpyDeviceToHost, s));
       LB_CHECK(hipStreamSynchronize(s));
-#if SPTR_TREELET
       // SAH treelet restructuring (k_treelet) for the single-primitive-leaf trees of L2/HBM scenes:
       // launch h rewrites the nodes of height h; each pass's new heights order the next pass
       if (leaf_max == 1u && N >= 3u && c.treelet_passes > 0u) {
@@ -1411,7 +1136,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
           hipLaunchKernelGGL(k_height_scatter, dim3(kHeightBlocks), dim3(256), 0, s, nn, per, lab, hist, order);
           for (uint32_t h = 1; h < kMaxHeight; ++h)
             if (hh[h])
-              hipLaunchKernelGGL(k_treelet<SPTR_TREELET>, dim3((hh[h] + kTreeletBlock - 1) / kTreeletBlock),
+              hipLaunchKernelGGL(k_treelet<kTreeletLeaves>, dim3((hh[h] + kTreeletBlock - 1) / kTreeletBlock),
                                  dim3(kTreeletBlock), 0, s, order + off[h], hh[h], nodes, cst, nh, leaf_parent);
           LB_CHECK(hipGetLastError());
           LB_CHECK(hipMemcpyAsync(&dep, nh, 4, hipMemcpyDeviceToHost, s));  // the root's new height
@@ -1419,7 +1144,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
           std::swap(lab, nh);
         }
       }
-#endif
     }
     c.root = N <= leaf_max ? (kLeafBit | (N - 1u)) : 0u;  // whole scene in one leaf range, or node 0
     c.bvh_depth = dep;
@@ -1437,7 +1161,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       c.num_top4 = 0;
       c.root4 = c.root;
     } else {
-#if SPTR_WIDE_GREEDY
       // wide BVH, greedy surface-area collapse, top-down: level L's wide nodes are numbered after
       // levels 0..L-1 (so the top kTopLevels levels come first); cnt -> exclusive scan -> emit
       uint2 *cur = nullptr, *nxt = nullptr;
@@ -1459,8 +1182,7 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
         LB_CHECK(hipGetLastError());
         LB_CHECK(scan_u32(stw, sw, flag, off, ncur, s));
         hipLaunchKernelGGL(k_wide_emit, dim3(blocks_for(ncur)), dim3(256), 0, s, ncur, cur, base, nodes, off, nxt,
-                           static_cast<WideNode*>(c.nodes4.p), static_cast<const uint32_t*>(c.prim_ref.p),
-                           (uint32_t)SPTR_WIDE_DIRECT);
+                           static_cast<WideNode*>(c.nodes4.p), static_cast<const uint32_t*>(c.prim_ref.p));
         LB_CHECK(hipGetLastError());
         uint32_t last[2] = {0u, 0u};  // cnt, off of the level's last node
         LB_CHECK(hipMemcpyAsync(&last[0], flag + (ncur - 1u), 4, hipMemcpyDeviceToHost, s));
@@ -1476,34 +1198,6 @@ int build_lbvh(Context& c, const float* h_pos, uint32_t nverts, const uint32_t* 
       c.num_nodes4 = base;
       // a wide node at wide depth d holds at most (kWide-1)*d stack entries and pushes up to kWide-1
       c.stack_need4 = (uint32_t)(kWide - 1) * levels;
-#else
-      // fixed collapse: keep / top flags -> exclusive scans -> wide indices (top levels first) -> collapse
-      // (reusing the flag/slot scratch arrays; top flags and their scan in kids / leaf_parent)
-      uint32_t* topf = reinterpret_cast<uint32_t*>(kids);
-      uint32_t* tslot = leaf_parent;
-      hipLaunchKernelGGL(k_depth_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, leaf_max, nodes, flag, topf);
-      LB_CHECK(hipGetLastError());
-      size_t s4 = 0;
-      LB_CHECK(scan_u32(nullptr, s4, flag, slot, N - 1, s));
-      void* st4 = nullptr;
-      LB_CHECK(tmp.alloc(reinterpret_cast<char**>(&st4), s4));
-      LB_CHECK(scan_u32(st4, s4, flag, slot, N - 1, s));
-      LB_CHECK(scan_u32(st4, s4, topf, tslot, N - 1, s));
-      uint32_t last[4] = {0u, 0u, 0u, 0u};  // keep, slot, top, tslot of node N - 2
-      LB_CHECK(hipMemcpyAsync(&last[0], flag + (N - 2), 4, hipMemcpyDeviceToHost, s));
-      LB_CHECK(hipMemcpyAsync(&last[1], slot + (N - 2), 4, hipMemcpyDeviceToHost, s));
-      LB_CHECK(hipMemcpyAsync(&last[2], topf + (N - 2), 4, hipMemcpyDeviceToHost, s));
-      LB_CHECK(hipMemcpyAsync(&last[3], tslot + (N - 2), 4, hipMemcpyDeviceToHost, s));
-      hipLaunchKernelGGL(k_wide_index, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, flag, topf, slot, tslot);
-      LB_CHECK(hipGetLastError());
-      LB_CHECK(hipStreamSynchronize(s));
-      c.num_nodes4 = last[1] + last[0];
-      c.num_top4 = last[3] + last[2];
-      LB_CHECK(realloc_buf(c.nodes4, (size_t)c.num_nodes4 * sizeof(WideNode)));
-      hipLaunchKernelGGL(k_collapse_wide, dim3(blocks_for(N)), dim3(256), 0, s, (int)N, nodes, flag, slot,
-                         static_cast<WideNode*>(c.nodes4.p));
-      LB_CHECK(hipGetLastError());
-#endif
       c.root4 = 0u;  // node 0 (depth 0) is kept and scans to index 0
     }
   }

@@ -58,24 +58,17 @@
 #ifndef SPTR_SKY_ILP
 #define SPTR_SKY_ILP 4  // independent samples per step of k_sky's per-pixel loop
 #endif
-#ifndef SPTR_SORT_OCTANT
-#define SPTR_SORT_OCTANT 0  // k_shade groups its continuation rays by direction octant (A/B builds)
-#endif
-#ifndef SPTR_TOP_LDS
-#define SPTR_TOP_LDS 1  // wide-BVH top levels staged in LDS by the refilling kernels (0: A/B builds)
-#endif
-#ifndef SPTR_ANYHIT_FAR
-#define SPTR_ANYHIT_FAR 1  // any-hit wide walks visit the farthest hit child first: a ray leaving a surface has
-                           // no occluder among the boxes around its origin, so the near-first order explores
-                           // them before the far occluder (r03b A/B: C5 shadow 4.42 -> 3.88 ms/step, C3
-                           // 0.81 -> 0.80); 0: nearest first
-#endif
-#ifndef SPTR_ANYHIT_FAR2
-#define SPTR_ANYHIT_FAR2 0  // 1: any-hit BVH2 walks (LDS scenes) visit the farther child first (A/B builds)
-#endif
 #ifndef SPTR_SHADOW4_WAVES
 #define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
+
+namespace sptr {
+// Any-hit wide walks visit the farthest hit child first: a ray leaving a surface has no occluder among
+// the boxes around its origin, so the near-first order explores them before the far occluder (r03b A/B:
+// C5 shadow 4.42 -> 3.88 ms/step, C3 0.81 -> 0.80).  The any-hit BVH2 walk of LDS scenes stays
+// near-first (far-first: no change on C2).
+constexpr bool kAnyHitFar = true;
+}  // namespace sptr
 
 namespace sptr {
 
@@ -93,43 +86,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* s_cnt, bool pred) {
   if ((int)lane == leader) base = atomicAdd(s_cnt, (uint32_t)__popcll(m));
   base = __shfl(base, leader);
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-}
-// Block-local append grouped by a 3-bit key (a continuation ray's direction octant): the chunk's
-// outputs land in the block's segment ordered by key, so that the consumer's waves trace rays of
-// one octant together (same near-child order, fewer divergent node visits).  Every thread of the
-// block must call it together (block barriers).  s_hist: 16 words of LDS.
-__device__ __forceinline__ uint32_t block_append_key(uint32_t* s_cnt, uint32_t* s_hist, bool pred, uint32_t key) {
-  if (threadIdx.x < 8u) s_hist[threadIdx.x] = 0u;
-  __syncthreads();
-  const uint32_t lane = lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t rank = 0u;
-#pragma unroll
-  for (uint32_t k = 0; k < 8u; ++k) {
-    const bool mine = pred && key == k;
-    const unsigned long long m = __ballot(mine);
-    if (m) {
-      const int leader = __ffsll(m) - 1;
-      uint32_t b = 0u;
-      if ((int)lane == leader) b = atomicAdd(&s_hist[k], (uint32_t)__popcll(m));
-      b = __shfl(b, leader);
-      if (mine) rank = b + (uint32_t)__popcll(m & below);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0u) {
-    uint32_t run = *s_cnt;
-    for (uint32_t k = 0; k < 8u; ++k) {
-      s_hist[8u + k] = run;
-      run += s_hist[k];
-    }
-    *s_cnt = run;
-  }
-  __syncthreads();
-  return s_hist[8u + key] + rank;
-}
-__device__ __forceinline__ uint32_t octant(float x, float y, float z) {
-  return (x < 0.0f ? 1u : 0u) | (y < 0.0f ? 2u : 0u) | (z < 0.0f ? 4u : 0u);
 }
 // Block-local work counter: every lane with pred takes the next index (one LDS atomic per wave).
 __device__ __forceinline__ uint32_t block_take(uint32_t* s_next, bool pred) { return block_append(s_next, pred); }
@@ -149,11 +105,6 @@ __device__ __forceinline__ uint32_t logical_block() {
 // blocks that drew the expensive region; dealing chunks balances statistically and keeps all CUs
 // on one band of the frame at a time (shared BVH working set).  Every block processes at most
 // `per` items, which is the stride of its output segment: seg0 = logical block * per.
-// SPTR_SCHED_CONTIG (timing experiment): block b takes the contiguous items [b*per, b*per + per)
-// instead, so every output segment keeps its input's order.
-#ifndef SPTR_SCHED_CONTIG
-#define SPTR_SCHED_CONTIG 0
-#endif
 struct Sched {
   uint32_t first, step, per, seg0, end;  // items first + j*step + [0, kBlock), below end
 };
@@ -163,15 +114,9 @@ __device__ __forceinline__ Sched block_sched(uint32_t n) {
   const uint32_t span = gridDim.x * kBlock;
   s.per = (n + span - 1) / span * kBlock;
   s.seg0 = lb * s.per;
-  if (SPTR_SCHED_CONTIG) {
-    s.first = s.seg0;
-    s.step = kBlock;
-    s.end = min(n, s.seg0 + s.per);
-  } else {
-    s.first = lb * kBlock;
-    s.step = span;
-    s.end = n;
-  }
+  s.first = lb * kBlock;
+  s.step = span;
+  s.end = n;
   return s;
 }
 
@@ -219,12 +164,15 @@ __device__ uint32_t seg_scan(const SegTable& t, uint32_t nseg, uint32_t* s_off, 
 }
 // Compacted index i -> physical slot: the largest segment b with s_off[b] <= i (a fixed 11-step
 // search over LDS; empty segments are skipped because the largest such b is the non-empty one).
+// Candidates past the last segment read s_off[nseg] = the total, which exceeds every valid i, so
+// each step is an unconditional LDS read and a select (r05: the bounds test in front of the read
+// made every step a branch with its own exec-mask bookkeeping and a full memory wait).
 __device__ __forceinline__ uint32_t seg_slot(const uint32_t* s_off, uint32_t nseg, uint32_t per, uint32_t i) {
   uint32_t b = 0u;
 #pragma unroll
   for (uint32_t step = kMaxSegs / 2; step; step >>= 1) {
-    const uint32_t c = b + step;
-    if (c < nseg && s_off[c] <= i) b = c;
+    const uint32_t c = min(b + step, nseg);
+    b = s_off[c] <= i ? c : b;
   }
   return b * per + (i - s_off[b]);
 }
@@ -275,18 +223,14 @@ __device__ __forceinline__ FrameView frame_dyn(FrameView f) {
   }
   return f;
 }
-// clear (may be null): the two counters an in-sequence k_cull accumulates from zero (its unculled and
-// culled pixel counts), zeroed here instead of by a memset node of their own.  dyn[kDynPmQueue]: the
-// work queue of the pixel-major bounce 0 (k_trace_pm), zeroed here and by every k_accum, so each batch's
-// k_trace_pm starts from zero.
+// clear (may be null): the two words after an in-sequence k_cull's list (its unculled pixel count and a
+// spare), zeroed here instead of by a memset node of their own.
 __global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear) {
   if (threadIdx.x == 0) {
     dyn[0] = frame_begin;
     dyn[1] = reset;
     dyn[2] = total;
-    dyn[kDynPmQueue] = 0u;
   }
-  if (threadIdx.x < kXcds) dyn[kDynSkyQueue + 32u * threadIdx.x] = 0u;
   if (threadIdx.x == 0) {
     if (clear) {
       clear[0] = 0u;
@@ -447,16 +391,6 @@ constexpr int kLdsStack = 12;  // kernels that also stage the scene in LDS
 #define SPTR_LDS_STACK_G 12
 #endif
 constexpr int kLdsStackG = SPTR_LDS_STACK_G;  // kernels traversing from L2/HBM (LDS holds only the stack)
-#ifdef SPTR_EXPERIMENT_NO_SPILL  // timing experiment only: drops pushes beyond the LDS part (wrong hits)
-template <int N>
-struct TravStack {
-  uint32_t* lds;
-  __device__ __forceinline__ void put(int i, uint32_t v) {
-    if (i < N) lds[i * kBlock] = v;
-  }
-  __device__ __forceinline__ uint32_t get(int i) const { return i < N ? lds[i * kBlock] : 0u; }
-};
-#else
 template <int N>
 struct TravStack {
   uint32_t* lds;  // &s_stack[0][threadIdx.x]
@@ -467,7 +401,6 @@ struct TravStack {
   }
   __device__ __forceinline__ uint32_t get(int i) const { return i < N ? lds[i * kBlock] : spill[i - N]; }
 };
-#endif
 template <int N>
 struct alignas(16) LdsStackN {
   uint32_t e[N][kBlock];
@@ -508,7 +441,7 @@ __device__ __forceinline__ bool bvh2_walk(uint32_t& cur, int& sp, bool& hit, Tra
       hr = false;
     }
     if (hl && hr) {
-      if ((kAny && SPTR_ANYHIT_FAR2) ? tl < tr : tr < tl) {
+      if (tr < tl) {
         const uint32_t s = L;
         L = R;
         R = s;
@@ -549,7 +482,7 @@ __device__ __forceinline__ bool traverse(const BvhNode* nodes, const uint32_t* p
 // one.  qn / qf: the plane words that are near / far for this ray direction.
 struct QAxis {
   float A, Bn, Bf;
-  uint32_t qn[kQWords], qf[kQWords];
+  uint32_t qn[1], qf[1];
 };
 __device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, const uint32_t* qlo, const uint32_t* qhi, float ro,
                                         float inv) {
@@ -560,11 +493,8 @@ __device__ __forceinline__ QAxis q_axis(float org, uint32_t ebyte, const uint32_
   a.Bn = B - pad;
   a.Bf = B + pad;
   const bool pos = inv >= 0.0f;
-#pragma unroll
-  for (int j = 0; j < kQWords; ++j) {
-    a.qn[j] = pos ? qlo[j] : qhi[j];
-    a.qf[j] = pos ? qhi[j] : qlo[j];
-  }
+  a.qn[0] = pos ? qlo[0] : qhi[0];
+  a.qf[0] = pos ? qhi[0] : qlo[0];
   return a;
 }
 __device__ __forceinline__ float q_byte(const uint32_t* w, int k) { return (float)((w[k / 4] >> (8 * (k % 4))) & 0xFFu); }
@@ -599,45 +529,29 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
                                           const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
   for (int it = 0; it < steps; ++it) {
     const uint4* nq = reinterpret_cast<const uint4*>(nodes + wk.cur);
-    uint4 h;
-    uint32_t ln[kWide], qw[6 * kQWords];
-    if (kWide == 4) {
-      uint4 l4, q4;
-      uint2 q2;
-      if (wk.cur < ntop) {
-        const uint4* t = top + 4u * wk.cur;
-        h = t[0];
-        l4 = t[1];
-        q4 = t[2];
-        q2 = *reinterpret_cast<const uint2*>(t + 3);
-        // pins the LDS loads inside this branch: otherwise the compiler sinks both branches' loads
-        // past the join as flat loads of a selected address
-        asm volatile("" ::"v"(h.x), "v"(l4.x), "v"(q4.x), "v"(q2.x));
-      } else {
-        h = nq[0];
-        l4 = nq[1];
-        q4 = nq[2];
-        q2 = *reinterpret_cast<const uint2*>(nq + 3);
-      }
-      ln[0] = l4.x; ln[1] = l4.y; ln[2] = l4.z; ln[3] = l4.w;
-      qw[0] = q4.x; qw[1] = q4.y; qw[2] = q4.z; qw[3] = q4.w; qw[4] = q2.x; qw[5] = q2.y;
+    uint4 h, l4, q4;
+    uint2 q2;
+    if (wk.cur < ntop) {
+      const uint4* t = top + 4u * wk.cur;
+      h = t[0];
+      l4 = t[1];
+      q4 = t[2];
+      q2 = *reinterpret_cast<const uint2*>(t + 3);
+      // pins the LDS loads inside this branch: otherwise the compiler sinks both branches' loads
+      // past the join as flat loads of a selected address
+      asm volatile("" ::"v"(h.x), "v"(l4.x), "v"(q4.x), "v"(q2.x));
     } else {
       h = nq[0];
-#pragma unroll
-      for (int j = 0; j < kWide / 4; ++j) {
-        const uint4 v = nq[1 + j];
-        ln[4 * j] = v.x; ln[4 * j + 1] = v.y; ln[4 * j + 2] = v.z; ln[4 * j + 3] = v.w;
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const uint4 v = nq[1 + kWide / 4 + j];
-        qw[4 * j] = v.x; qw[4 * j + 1] = v.y; qw[4 * j + 2] = v.z; qw[4 * j + 3] = v.w;
-      }
+      l4 = nq[1];
+      q4 = nq[2];
+      q2 = *reinterpret_cast<const uint2*>(nq + 3);
     }
+    const uint32_t ln[4] = {l4.x, l4.y, l4.z, l4.w};
+    const uint32_t qw[6] = {q4.x, q4.y, q4.z, q4.w, q2.x, q2.y};
     if (kCount) ++vc.nodes;
-    const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0 * kQWords, qw + 1 * kQWords, r.o.x, r.inv.x);
-    const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2 * kQWords, qw + 3 * kQWords, r.o.y, r.inv.y);
-    const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4 * kQWords, qw + 5 * kQWords, r.o.z, r.inv.z);
+    const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0, qw + 1, r.o.x, r.inv.x);
+    const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2, qw + 3, r.o.y, r.inv.y);
+    const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4, qw + 5, r.o.z, r.inv.z);
     float t[kWide];
     bool hc[kWide];
 #pragma unroll
@@ -656,13 +570,13 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
         hc[k] = false;
       }
     }
-    // next node: the nearest hit internal child; any-hit walks with SPTR_ANYHIT_FAR take the farthest
+    // next node: the nearest hit internal child; any-hit walks take the farthest (kAnyHitFar)
     int kn = kWide;
     float tn = __builtin_huge_valf();
     uint32_t npush = 0u;
 #pragma unroll
     for (int k = 0; k < kWide; ++k) {
-      const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
+      const bool better = (kAny && kAnyHitFar) ? t[k] > tn : t[k] < tn;
       if (hc[k] && (kn == kWide || better)) {
         tn = t[k];
         kn = k;
@@ -692,16 +606,11 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
 // leaves (leaf size > 1) are tested with leaf_test on their step.  Same hits: the closest hit is the
 // minimum over the same set of primitives tested against the same rays (ties at exactly equal t
 // may resolve to another primitive, as with any change of traversal order).
-#ifndef SPTR_WALK_UNIFIED
-#define SPTR_WALK_UNIFIED 1
+#ifndef SPTR_WALK_BF
+#define SPTR_WALK_BF 1  // r05: the unified step without divergent branches (walk_step_bf); 0: walk_fetch + walk_apply
 #endif
-#ifndef SPTR_PRIMARY_UNIFIED
-#define SPTR_PRIMARY_UNIFIED 1  // camera rays too (k_trace_dyn<primary>); 0: the leaf-inline walk
-#endif
-// One step of the unified walk, split into its fetch (the 56 B of the item wk.cur names: a wide node
-// from the LDS top levels or L2/HBM, or a direct leaf's triangle / sphere record) and the step proper
-// (walk_apply), so that a kernel tracing two rays per lane can issue both rays' fetches before either
-// waits (k_trace_dyn2).  wide_walk_u is fetch + apply per step: the arithmetic is one code path.
+// One step of the unified walk: its fetch (the 56 B of the item wk.cur names: a wide node from the
+// LDS top levels or L2/HBM, or a direct leaf's triangle / sphere record) and the step proper.
 struct WalkItem {
   uint4 h, l4, q4;
   uint2 q2;
@@ -794,7 +703,7 @@ __device__ __forceinline__ bool walk_apply(WideWalk& wk, TravStack<N>& stack, co
   uint32_t npush = 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const bool better = (kAny && SPTR_ANYHIT_FAR) ? t[k] > tn : t[k] < tn;
+    const bool better = (kAny && kAnyHitFar) ? t[k] > tn : t[k] < tn;
     if (hc[k] && (kn == 4 || better)) {
       tn = t[k];
       kn = k;
@@ -824,12 +733,146 @@ __device__ __forceinline__ bool wide_walk_u(WideWalk& wk, TravStack<N>& stack, c
   }
   return false;
 }
-// kU: the unified walk (default SPTR_WALK_UNIFIED); callers choose per ray class (see the kernels)
-template <bool kAny, bool kCount, bool kU = (SPTR_WALK_UNIFIED != 0), int N>
+
+// The unified step without divergent branches (r05).  r04's step (walk_fetch + walk_apply) split the
+// wave at every per-lane decision — leaf or node, top-LDS or global fetch, sphere or triangle, each
+// push into the LDS part or the scratch part of the stack, pop or descend — and every split costs
+// exec-mask bookkeeping (s_and_saveexec / s_xor / s_cbranch_execz / s_or: 430 of k_shadow_dyn's 882
+// SALU).  Here every lane runs one instruction stream per step:
+//   * one 64-B fetch from a selected address (node, direct triangle or sphere record; the top levels
+//     are read from L2 like the rest — the LDS copy measured within noise on C5, r02g);
+//   * the four quantised slab tests and the triangle test both evaluated, their results selected by
+//     the item's kind (the division of a triangle hit runs only in lanes that hit);
+//   * the child order by selects; the pushes as unconditional LDS writes at the running push
+//     position (a slot that is not a push is overwritten by the next push or lies above the new
+//     stack top), while the stack top stays below the LDS part (sp + 3 < N); a lane that may cross
+//     into the scratch part takes the branchy put of the r04 step;
+//   * the pop as an LDS read of row min(sp - 1, N - 1), replaced from scratch only below the LDS part.
+// Spheres and range leaves (leaf size > 1: LDS-staged scenes in BVH4 test mode) keep a branch: they
+// are rare or absent in the scenes this walk serves.  Same node order, same tests, same hits as the r04
+// step (k_strag resumes either's state).
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool walk_step_bf(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes,
+                                             const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                             const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc) {
+  const uint32_t cur = wk.cur;
+  const int sp = wk.sp;
+  const bool leaf = (cur & kLeafBit) != 0u;
+  const bool direct = (cur & (kLeafBit | kLeafDirect)) == (kLeafBit | kLeafDirect);
+  const bool dsph = direct && (cur & kLeafDirectSphere) != 0u;
+  const uint32_t slot = (cur & ~kLeafBit) >> kLeafCountBits;
+  // pointer arithmetic on the kernel's global pointers (an address computed through an integer would
+  // lose their address space, and the fetch would become flat loads, which also wait on the LDS counter)
+  const uint4* an = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(nodes) + (size_t)cur * sizeof(WideNode));
+  const uint4* ap = dsph ? reinterpret_cast<const uint4*>(sph + slot) : reinterpret_cast<const uint4*>(tris + 3u * (direct ? slot : 0u));
+  const uint4* a = leaf ? ap : an;
+  const uint4 h = a[0], l4 = a[1], q4 = a[2];
+  const uint2 q2 = *reinterpret_cast<const uint2*>(a + 3);
+  // the pop candidate: row min(sp - 1, N - 1) of the LDS part (an LDS read by address space, and pinned:
+  // otherwise the compiler selects between the LDS and the scratch address and issues a flat load),
+  // replaced from scratch below the LDS part
+  const int ps = sp > 0 ? sp - 1 : 0;
+  uint32_t popv = *(const __attribute__((address_space(3))) uint32_t*)(stack.lds + (ps < N ? ps : N - 1) * kBlock);
+  asm volatile("" : "+v"(popv));
+  if (ps >= N) popv = stack.spill[ps - N];
+  // node: quantised slab tests of the four children
+  const uint32_t ln[4] = {l4.x, l4.y, l4.z, l4.w};
+  const uint32_t qw[6] = {q4.x, q4.y, q4.z, q4.w, q2.x, q2.y};
+  const QAxis ax = q_axis(__uint_as_float(h.x), h.w & 0xFFu, qw + 0, qw + 1, r.o.x, r.inv.x);
+  const QAxis ay = q_axis(__uint_as_float(h.y), (h.w >> 8) & 0xFFu, qw + 2, qw + 3, r.o.y, r.inv.y);
+  const QAxis az = q_axis(__uint_as_float(h.z), (h.w >> 16) & 0xFFu, qw + 4, qw + 5, r.o.z, r.inv.z);
+  float t[4];
+  bool hc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hc[k] = q_slab(k, ax, ay, az, tnear, tfar, t[k]) & (ln[k] != kNoHit) & !leaf;
+  // leaf: a direct triangle (Embree's test, tri_hit4, with the division deferred to the lanes that hit)
+  bool lhit = false;
+  {
+    const float4 p0 = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
+    const float4 p1 = make_float4(__uint_as_float(l4.x), __uint_as_float(l4.y), __uint_as_float(l4.z), __uint_as_float(l4.w));
+    const float4 p2 = make_float4(__uint_as_float(q4.x), __uint_as_float(q4.y), __uint_as_float(q4.z), __uint_as_float(q4.w));
+    const vec3 v0 = v3(p0.x, p0.y, p0.z), e1 = v3(p0.w, p1.x, p1.y), e2 = v3(p1.z, p1.w, p2.x), ng = v3(p2.y, p2.z, p2.w);
+    const vec3 C = v0 - r.o;
+    const vec3 R = e_cross(C, r.d);
+    const float den = e_dot(ng, r.d);
+    const float aden = fabsf(den);
+    const float U = xorsign(e_dot(R, e2), den);
+    const float V = xorsign(e_dot(R, e1), den);
+    const float T = xorsign(e_dot(ng, C), den);
+    const bool tri = direct && !dsph;
+    const bool inside = (den != 0.0f) & (U >= 0.0f) & (V >= 0.0f) & (U + V <= aden);
+    const bool range = (aden * tnear < T) & (T <= aden * tfar);
+    lhit = tri & inside & range;
+    if (kCount) vc.tris += tri ? 1u : 0u;
+    if (!kAny && lhit) {
+      tfar = T / aden;
+      ref = slot;
+    }
+  }
+  if (dsph) {  // a direct sphere (rare: the reference's analytic spheres)
+    if (kCount) ++vc.sph;
+    const float4 p0 = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w));
+    float ts;
+    if (kAny) lhit = sphere_occ(p0, r, tnear, tfar);
+    else if (sphere_hit(p0, r, tnear, tfar, ts)) {
+      tfar = ts;
+      ref = slot | kSphereBit;
+      lhit = true;
+    }
+  }
+  if (leaf && !direct) lhit = leaf_test<kAny, kCount>(cur, prim_ref, tris, sph, r, tnear, tfar, ref, vc);  // range leaf
+  if (kCount) vc.nodes += leaf ? 0u : 1u;
+  // child order: the nearest hit child next (far-first for any-hit, kAnyHitFar), lowest slot on ties
+  int kn = 4;
+  float tn = __builtin_huge_valf();
+  uint32_t nxt = 0u, nh = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool better = (kAny && kAnyHitFar) ? t[k] > tn : t[k] < tn;
+    const bool take = hc[k] & ((kn == 4) | better);
+    tn = take ? t[k] : tn;
+    kn = take ? k : kn;
+    nxt = take ? ln[k] : nxt;
+    nh += hc[k] ? 1u : 0u;
+  }
+  const bool descend = kn < 4;
+  // pushes: the other hit children, highest slot first
+  if (sp + 3 < N) {
+    int pos = sp;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+      stack.lds[pos * kBlock] = ln[k];
+      pos += (hc[k] & (k != kn)) ? 1 : 0;
+    }
+  } else {
+    if (sp + (int)nh - 1 > kStack) vc.stack_overflow = 1u;
+    int pos = sp;
+#pragma unroll
+    for (int k = 3; k >= 0; --k)
+      if (hc[k] && k != kn && pos < kStack) stack.put(pos++, ln[k]);
+  }
+  const int spd = sp + (int)nh - 1;
+  wk.hit = wk.hit | lhit;
+  wk.cur = descend ? nxt : popv;
+  wk.sp = descend ? (spd < kStack ? spd : kStack) : ps;
+  return (kAny && lhit) || (!descend && sp == 0);
+}
+template <bool kAny, bool kCount, int N>
+__device__ __forceinline__ bool wide_walk_bf(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes,
+                                             const uint32_t* prim_ref, const float4* tris, const float4* sph,
+                                             const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
+  for (int it = 0; it < steps; ++it)
+    if (walk_step_bf<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) return true;
+  return false;
+}
+// kU: the unified walk; callers choose per ray class (see the kernels)
+template <bool kAny, bool kCount, bool kU = true, int N>
 __device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
                                           uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
                                           const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
-  if constexpr (kU && kWide == 4)
+  if constexpr (kU && SPTR_WALK_BF)
+    return wide_walk_bf<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
+  else if constexpr (kU)
     return wide_walk_u<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
   return wide_walk_inl<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
 }
@@ -1088,20 +1131,16 @@ __device__ __forceinline__ bool pixel_frustum_misses(const SceneView& sv, const 
   return true;
 }
 // bit l of mask: pixel l is culled (see above).  plist: the valid pixels that are not culled, from
-// plist[0] (count at plist[P]), and every other local pixel — culled, or a tile slot outside the image —
-// from plist[P - 1] downwards (count at plist[P + 1]); both counts zeroed before.  So plist[0..P) is a
-// permutation of the local pixels, the expensive ones first (the order of the pixel-major bounce 0,
-// k_trace_pm).  One block per local tile: thread (qx, qy) tests the 2x2 pixel quad at (2qx, 2qy) of the
-// tile and sets the quad's bits in the tile's 32 LDS row words; then each thread lists the pixels of 4
-// consecutive local indices, the tile's runs at ranges one atomic per tile and list reserves.  (r02: a
-// pyramid per pixel and one atomic per wave, C2 108 us; per pixel and per tile 65-75 us.)
-// the list of the other pixels is written only when a work queue reads it (SPTR_PM_QUEUE, SPTR_SKY_LANES)
-constexpr bool kCullListBoth = SPTR_PM_QUEUE != 0 || SPTR_SKY_LANES != 0;
+// plist[0] (count at plist[P], zeroed before).  One block per local tile: thread (qx, qy) tests the 2x2
+// pixel quad at (2qx, 2qy) of the tile and sets the quad's bits in the tile's 32 LDS row words; then
+// each thread lists the pixels of 4 consecutive local indices, the tile's run at a range one atomic per
+// tile reserves.  (r02: a pyramid per pixel and one atomic per wave, C2 108 us; per pixel and per tile
+// 65-75 us.)
 __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint32_t* mask, uint32_t* plist) {
   static_assert(kTile == 32 && kBlock == 256, "16 x 16 quads per 32 x 32 tile");
   __shared__ uint32_t s_row[kTile];
-  __shared__ uint32_t s_cnt[kBlock / 64u], s_ccnt[kBlock / 64u];
-  __shared__ uint32_t s_base, s_cbase;
+  __shared__ uint32_t s_cnt[kBlock / 64u];
+  __shared__ uint32_t s_base;
   const uint32_t t0 = blockIdx.x * kTilePixels;  // the tile's first local pixel
   if (threadIdx.x < (uint32_t)kTile) s_row[threadIdx.x] = 0u;
   __syncthreads();
@@ -1139,43 +1178,29 @@ __global__ void __launch_bounds__(kBlock) k_cull(SceneView sv, FrameView f, uint
   uint32_t w = mbits << col;
   for (int off = 1; off < 8; off <<= 1) w |= __shfl_xor(w, off);
   if ((threadIdx.x & 7u) == 0u) mask[(t0 >> 5) + row] = w;
-  // list the kept pixels (and the others from the top): per-thread counts, wave scans, block offsets,
-  // one atomic per tile and list
-  const uint32_t drop = ~keep & 0xFu;
-  const uint32_t n = (uint32_t)__popc(keep), nd = (uint32_t)__popc(drop), lane = lane_id();
-  uint32_t incl = n, incd = nd;
+  // list the kept pixels: per-thread counts, wave scans, block offsets, one atomic per tile
+  const uint32_t n = (uint32_t)__popc(keep), lane = lane_id();
+  uint32_t incl = n;
   for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t v = __shfl_up(incl, off), vd = __shfl_up(incd, off);
-    if (lane >= (uint32_t)off) {
-      incl += v;
-      incd += vd;
-    }
+    const uint32_t v = __shfl_up(incl, off);
+    if (lane >= (uint32_t)off) incl += v;
   }
-  if (lane == 63u) {
-    s_cnt[threadIdx.x >> 6] = incl;
-    s_ccnt[threadIdx.x >> 6] = incd;
-  }
+  if (lane == 63u) s_cnt[threadIdx.x >> 6] = incl;
   __syncthreads();
   if (threadIdx.x == 0u) {
-    uint32_t run = 0u, runc = 0u;
+    uint32_t run = 0u;
     for (uint32_t i = 0; i < kBlock / 64u; ++i) {
-      const uint32_t c = s_cnt[i], cd = s_ccnt[i];
+      const uint32_t c = s_cnt[i];
       s_cnt[i] = run;
-      s_ccnt[i] = runc;
       run += c;
-      runc += cd;
     }
     s_base = run ? atomicAdd(&plist[f.P], run) : 0u;
-    s_cbase = (kCullListBoth && runc) ? atomicAdd(&plist[f.P + 1u], runc) : 0u;
   }
   __syncthreads();
   uint32_t o = s_base + s_cnt[threadIdx.x >> 6] + incl - n;
-  uint32_t od = s_cbase + s_ccnt[threadIdx.x >> 6] + incd - nd;
 #pragma unroll
-  for (uint32_t j = 0; j < 4u; ++j) {
+  for (uint32_t j = 0; j < 4u; ++j)
     if ((keep >> j) & 1u) plist[o++] = t0 + 4u * threadIdx.x + j;
-    if (kCullListBoth && ((drop >> j) & 1u)) plist[f.P - 1u - od++] = t0 + 4u * threadIdx.x + j;
-  }
 }
 // Path-major bounce 0 over the unculled pixel list (f.plist: nlist pixels x k samples): compacted
 // item i -> path p.  Items run in groups of kPrimaryGroup listed pixels — neighbours, since k_cull lists
@@ -1334,25 +1359,18 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 // resumes there (accum.w = resume slot).  A kernel of its own (not a branch of k_trace), so that
 // its registers are allocated for this loop alone.
 //
-// Work distribution (r04): a thread's unit of work is one pixel's whole sample loop (its misses fold in
-// sample order), so a statically dealt schedule — 256-pixel chunks round-robin, 4.5 per block on C2 —
-// left the kernel waiting for the blocks that drew a fifth chunk or the costly pixels, with the average
-// wave alive for ~55 % of the launch (r03 SQ_WAVE_CYCLES).  Now every wave takes 64 pixels at a time
-// from a global queue (FrameView::dyn[kDynPmQueue], zeroed by k_frame_dyn and k_accum), in the order of
-// k_cull's list: the unculled pixels (traversals) first, the culled ones (raygen + sky only) after them,
-// so the launch ends on the cheap chunks.  A block's hit records stay in its own segment, sized for twice
-// its static share: a wave takes pixels only while its block has room (s_taken), and since all
-// segments together hold twice the frame, some block always has room while pixels remain.  The pixel
-// order changes no result: each pixel's samples are summed in sample order by the thread that owns it.
+// Work distribution: 256-pixel chunks dealt round-robin over the blocks (block_sched).  (r04 A/B: a
+// global 64-pixel queue in k_cull's unculled-first order left this launch unchanged and slowed k_shade,
+// whose hit records then came from all over the frame)
 template <bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_PM_WAVES)
     k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt, s_taken;
+  __shared__ uint32_t s_cnt;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
-  if (threadIdx.x == 0) s_cnt = s_taken = 0u;
+  if (threadIdx.x == 0) s_cnt = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<true>(sv, lds);
   __syncthreads();
@@ -1363,37 +1381,13 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
   }
   const ImageDiv idiv = image_div(f);
   Visits vc;
-  const uint32_t* order = f.pm_order;  // k_cull's list (null without a cull mask: local pixel order)
-  const uint32_t n_unc = order ? order[f.P] : f.P;
-  // f.sky_fold (r04): k_sky sums the culled pixels beside this launch, so only k_cull's unculled pixels
-  // are this kernel's (in the list's order); otherwise every local pixel, culled ones as sky loops
-  const bool split = f.sky_fold != 0u && order != nullptr;
-  const uint32_t n_pix = split ? n_unc : f.P;
-  const Sched sd = block_sched(n_pix);
-  constexpr bool kQ = SPTR_PM_QUEUE != 0;
-  const uint32_t cap = kQ ? 2u * sd.per : sd.per;  // pixels this block may take: its hit-record segment holds cap * k records
-  const uint32_t per = cap * f.k;                  // hit-record segment stride
+  const Sched sd = block_sched(f.P);
+  const uint32_t per = sd.per * f.k;  // hit-record segment stride: the block's pixels x k records
   const uint32_t seg0 = logical_block() * per;
-  uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
-  const uint32_t lane = lane_id();
   for (uint32_t it = 0;; ++it) {
-    uint32_t l;
-    if constexpr (kQ) {
-      uint32_t base = kNoHit;
-      if (lane == 0u) {
-        const uint32_t t = atomicAdd(&s_taken, 64u);
-        if (t + 64u <= cap) base = atomicAdd(queue, 64u);
-      }
-      base = __shfl(base, 0);
-      if (base >= n_pix) break;  // the frame is taken (or this block's segment is full)
-      const uint32_t i = base + lane;
-      l = i >= n_pix ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
-    } else {  // the static share: 256-pixel chunks dealt round-robin
-      const uint32_t base = sd.first + it * sd.step;
-      if (base >= sd.end) break;
-      l = base + threadIdx.x;
-      if (split) l = l < n_unc ? order[l] : kNoHit;
-    }
+    const uint32_t base = sd.first + it * sd.step;
+    if (base >= sd.end) break;
+    const uint32_t l = base + threadIdx.x;
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
@@ -1457,9 +1451,8 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // sample r*8 + q of round r), so a wave's rays come from 8 neighbouring pixels.  A pixel's leading
 // misses (the samples before its first hit) are summed into the accumulator in sample order — an
 // 8-step shuffle loop per round, the same adds in the same order as k_accum; later misses go to
-// rad[p] and accum.w records where k_accum resumes.  Waves take 8 pixels at a time from the global
-// queue in k_cull's order (unculled pixels first), as k_trace_pm does (r04; r03 dealt 32-pixel block
-// chunks round-robin).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
+// rad[p] and accum.w records where k_accum resumes.  Blocks take 32-pixel chunks round-robin (a
+// global queue in k_cull's order measured slower, r04f).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
 // 289 us, 8 lanes 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 // kHiOcc: 8 waves/SIMD for shards whose pixels fill the resident waves only a few times (r04u: the
@@ -1470,9 +1463,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt, s_taken;
+  __shared__ uint32_t s_cnt;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
-  if (threadIdx.x == 0) s_cnt = s_taken = 0u;
+  if (threadIdx.x == 0) s_cnt = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
   __syncthreads();
@@ -1484,35 +1477,17 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
   const ImageDiv idiv = image_div(f);
   Visits vc;
   constexpr uint32_t kPix = kBlock / kFoldLanes;   // pixels per block round of the static share
-  constexpr uint32_t kWavePix = 64u / kFoldLanes;  // pixels per wave grab
   const uint32_t lane = lane_id(), q = lane & (kFoldLanes - 1u), g0 = lane & ~(kFoldLanes - 1u);
   const uint32_t lb = logical_block();
   const uint32_t step = gridDim.x * kPix;
-  constexpr bool kQ = SPTR_PM_QUEUE != 0;
-  const uint32_t cap = (kQ ? 2u : 1u) * ((f.P + step - 1u) / step * kPix);  // pixels per block at most
-  const uint32_t per = cap * f.k;                                           // hit-record segment stride
+  const uint32_t cap = (f.P + step - 1u) / step * kPix;  // pixels per block at most
+  const uint32_t per = cap * f.k;                          // hit-record segment stride
   const uint32_t seg0 = lb * per;
   const uint32_t rounds = (f.k + kFoldLanes - 1u) / kFoldLanes;
-  const uint32_t* order = f.pm_order;
-  const uint32_t n_unc = order ? order[f.P] : f.P;
-  uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynPmQueue;
   for (uint32_t it = 0;; ++it) {
-    uint32_t l;
-    if constexpr (kQ) {
-      uint32_t base = kNoHit;
-      if (lane == 0u) {
-        const uint32_t t = atomicAdd(&s_taken, kWavePix);
-        if (t + kWavePix <= cap) base = atomicAdd(queue, kWavePix);
-      }
-      base = __shfl(base, 0);
-      if (base >= f.P) break;
-      const uint32_t i = base + lane / kFoldLanes;
-      l = i >= f.P ? kNoHit : (!order ? i : (i < n_unc ? order[i] : order[f.P - 1u - (i - n_unc)]));
-    } else {  // the static share: 32-pixel block chunks dealt round-robin
-      const uint32_t base = lb * kPix + it * step;
-      if (base >= f.P) break;
-      l = base + threadIdx.x / kFoldLanes;
-    }
+    const uint32_t base = lb * kPix + it * step;
+    if (base >= f.P) break;
+    const uint32_t l = base + threadIdx.x / kFoldLanes;
     int x = 0, y = 0;
     const bool valid = l < f.P && local_pixel(f, l, x, y);
     const uint32_t ps = valid ? (uint32_t)(y * f.W + x) : 0u;
@@ -1680,7 +1655,7 @@ __device__ __forceinline__ bool walk_start(WideWalk& wk, const Staged& sc, uint3
                                            float& tfar, uint32_t& ref, Visits& vc) {
   return wide_start<kAny, kCount>(wk, root, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc);
 }
-template <bool kAny, bool kCount, bool kW4, bool kU = (SPTR_WALK_UNIFIED != 0), int N>
+template <bool kAny, bool kCount, bool kW4, bool kU = true, int N>
 __device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const uint4* top,
                                            uint32_t ntop, const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
                                            int steps) {
@@ -1704,10 +1679,6 @@ __device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, co
 #define SPTR_DYN_STEPS 8
 #endif
 constexpr int kDynSteps = SPTR_DYN_STEPS;
-#ifndef SPTR_DYN_LDS
-#define SPTR_DYN_LDS 0  // LDS-staged BVH2 bounces: refilling measured 2-3 % slower on C2 (short, even traversals)
-#endif
-constexpr bool kDynLds = SPTR_DYN_LDS != 0;
 __device__ __forceinline__ uint32_t block_items(const Sched& sd, uint32_t n) {
   if (sd.first >= sd.end) return 0u;
   const uint32_t rest = sd.end - sd.first, full = rest / sd.step, tail = rest - full * sd.step;
@@ -1827,9 +1798,6 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   bool have = false, done = false;
   uint32_t id = 0u, pid = 0u, ref = kNoHit;
   uint32_t v0 = 0u;  // kCount: the lane's node visits when its current ray started
-#ifdef SPTR_EXPERIMENT_STEP_CAP  // timing experiment only (wrong hits): a ray ends after this many refill rounds
-  uint32_t rounds = 0u;
-#endif
   float tfar = 0.0f;
   Ray r;
   WideWalk wk;
@@ -1872,9 +1840,6 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
         tfar = __builtin_huge_valf();
         ref = kNoHit;
         if (kCount) v0 = culled ? ~0u : vc.nodes;  // culled camera rays are not traversals
-#ifdef SPTR_EXPERIMENT_STEP_CAP
-        rounds = 0u;
-#endif
         done = walk_start<false, kCount, kW4>(wk, sc, culled ? kNoHit : (kW4 ? sv.root4 : sv.root), r, 0.0f, tfar, ref,
                                               vc);
         have = true;
@@ -1888,11 +1853,8 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     // the tree and the launches overlapped: C5 8.45 inline vs 8.22 ms/step unified, means of 3; r03x,
     // before both: 2.15 vs 2.37 ms for the bounce-0 trace)
     if (have && !done)
-      done = walk_steps<false, kCount, kW4, (!kPrimary || SPTR_PRIMARY_UNIFIED) && SPTR_WALK_UNIFIED>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
+      done = walk_steps<false, kCount, kW4, true>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
                                                                           kDynSteps);
-#ifdef SPTR_EXPERIMENT_STEP_CAP
-    if (have && !done && ++rounds >= (uint32_t)SPTR_EXPERIMENT_STEP_CAP) done = true;
-#endif
     // Straggler hand-off: the wave has no rays left to start and at most strag_lanes lanes are still
     // tracing (the long rays that would otherwise set the launch's length while the rest of the chip
     // idles).  Their rays are written to the bounce's straggler records and k_strag, beside the chain,
@@ -1960,175 +1922,6 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_depth_nodes(vc, w.tot, depth);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
-}
-
-// --------------------------------------------------------------------------------- two rays per lane
-// k_trace_dyn with two rays in flight per lane (SPTR_TRACE_PAIR; wide BVH from L2/HBM, timed passes):
-// each refill round fills the lane's two slots, and each walk step issues both slots' fetches
-// (walk_fetch) before either step proper (walk_apply), so a wave keeps twice the dependent loads in
-// flight at the occupancy two ray states allow.  Per ray the walk is the single-ray kernel's, step for
-// step (same hits, same records, same hand-off); only which lane and slot carries a ray differs.
-#ifndef SPTR_TRACE_PAIR
-#define SPTR_TRACE_PAIR 0  // r04x: bit-identical, but C5 7.9 -> 9.2 ms (4 waves/SIMD) / 10.0 (5 waves), C3 3.7 -> 3.9
-#endif
-#ifndef SPTR_TRACE2_WAVES
-#define SPTR_TRACE2_WAVES 4
-#endif
-template <bool kPrimary, bool kCube, bool kQueue>
-__global__ void __launch_bounds__(kBlock, SPTR_TRACE2_WAVES)
-    k_trace_dyn2(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
-  const FrameView f = frame_dyn(fin);
-  __shared__ LdsStackN<kLdsStackG> s_stack[2];
-  extern __shared__ float4 lds[];
-  __shared__ uint32_t s_cnt, s_next, s_taken;
-  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
-  if (threadIdx.x == 0) s_cnt = s_next = s_taken = 0u;
-  const Staged sc = stage_scene<false>(sv, lds);
-  const uint32_t ntop = sv.num_top4;
-  const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, false, kPrimary, nseg_in)) : nullptr;
-  uint32_t n, per_in = 0u, nlist = 0u;
-  if (kPrimary) {
-    nlist = f.plist ? f.plist[f.P] : 0u;
-    n = f.plist ? nlist * f.k : f.P * f.k;
-    __syncthreads();
-  } else {
-    n = seg_scan(w.segN, nseg_in, s_off, per_in);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    atomicAdd(&w.tot[kTotClosest], (unsigned long long)(kPrimary ? (unsigned long long)f.valid * f.k : n));
-    const unsigned long long t = kPrimary ? primary_traced(f) : (unsigned long long)n;
-    atomicAdd(&w.tot[kPrimary ? kTotTracedP : kTotTracedB], (unsigned long long)(t));
-    atomicAdd(&w.tot[kTotTracedD + stat_depth(depth)], (unsigned long long)(t));
-  }
-  const ImageDiv idiv = image_div(f);
-  const RayStream rs = w.rs[depth & 1];
-  Visits vc;
-  const Sched sd = block_sched(n);
-  const uint32_t nb = block_items(sd, n);
-  const uint32_t cap = kQueue ? 2u * sd.per : sd.per;
-  const uint32_t seg0 = logical_block() * cap;
-  XcdQueue xq = xcd_queue(w.work + kWorkTraceQueue, n);
-  TravStack<kLdsStackG> stack[2];
-  stack[0].lds = &s_stack[0].e[0][threadIdx.x];
-  stack[1].lds = &s_stack[1].e[0][threadIdx.x];
-  bool have[2] = {false, false}, done[2] = {false, false};
-  uint32_t id[2] = {0u, 0u}, pid[2] = {0u, 0u}, ref[2] = {kNoHit, kNoHit};
-  float tfar[2] = {0.0f, 0.0f};
-  Ray r[2];
-  WideWalk wk[2];
-  bool drained = false;
-  for (;;) {
-    bool more = false;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      uint32_t item = kNoHit;
-      if constexpr (kQueue) {
-        item = xcd_take(xq, !have[q], &s_taken, cap);
-        more = more || !xq.drained;
-        drained = xq.drained;
-      } else {
-        const uint32_t k = block_take(&s_next, !have[q]);
-        if (!have[q] && k < nb) item = block_item(sd, k);
-        more = more || (__ballot(!have[q] && k < nb) != 0ull);
-        if (__ballot(!have[q] && k >= nb) != 0ull) drained = true;
-      }
-      if (item != kNoHit) {
-        bool valid = true, culled = false;
-        vec3 o, d;
-        if (kPrimary) {
-          Primary pr;
-          uint32_t l, p = item;
-          if (f.plist) p = primary_item(f, nlist, item);
-          id[q] = pid[q] = p;
-          valid = primary_path(f, idiv, p, pr, l);
-          culled = !f.plist && pixel_culled(f, l);
-          o = f.cam_pos;
-          d = pr.d;
-        } else {
-          id[q] = seg_slot(s_off, nseg_in, per_in, item);
-          const float4 o4 = rs.o[id[q]], d4 = rs.d[id[q]];
-          o = xyz(o4);
-          d = xyz(d4);
-          pid[q] = __float_as_uint(d4.w);
-        }
-        if (valid) {
-          r[q] = make_ray(o, d);
-          tfar[q] = __builtin_huge_valf();
-          ref[q] = kNoHit;
-          done[q] = walk_start<false, false, true>(wk[q], sc, culled ? kNoHit : sv.root4, r[q], 0.0f, tfar[q], ref[q], vc);
-          have[q] = true;
-        }
-      }
-    }
-    if (__ballot(have[0] || have[1]) == 0ull) {
-      if (!more) break;
-      continue;
-    }
-    for (int it = 0; it < kDynSteps; ++it) {
-      const bool a0 = have[0] && !done[0], a1 = have[1] && !done[1];
-      if (__ballot(a0 || a1) == 0ull) break;
-      WalkItem i0, i1;
-      if (a0) i0 = walk_fetch(wk[0].cur, sc.nodes4, top, ntop, sc.tris, sc.sph);
-      if (a1) i1 = walk_fetch(wk[1].cur, sc.nodes4, top, ntop, sc.tris, sc.sph);
-      if (a0) done[0] = walk_apply<false, false>(wk[0], stack[0], i0, sc.prim_ref, sc.tris, sc.sph, r[0], 0.0f, tfar[0], ref[0], vc);
-      if (a1) done[1] = walk_apply<false, false>(wk[1], stack[1], i1, sc.prim_ref, sc.tris, sc.sph, r[1], 0.0f, tfar[1], ref[1], vc);
-    }
-    const bool defer = !kPrimary && w.defer_miss != 0u;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      // straggler hand-off, as in k_trace_dyn (counted over both slots of the wave's lanes)
-      if (w.strag_lanes != 0u && drained && (uint32_t)depth < kStragBounces) {
-        const unsigned long long act = __ballot((have[0] && !done[0]) || (have[1] && !done[1]));
-        if (act != 0ull && (uint32_t)__popcll(act) <= w.strag_lanes && have[q] && !done[q]) {
-          const uint32_t slot = atomicAdd(&w.work[kWorkStrag + (uint32_t)depth * 32u], 1u);
-          if (slot < w.strag_cap) {
-            float4* rec = w.strag + ((size_t)depth * w.strag_cap + slot) * kStragRec;
-            rec[3] = make_float4(__uint_as_float(wk[q].cur),
-                                 __uint_as_float((uint32_t)wk[q].sp | (wk[q].hit ? 0x10000u : 0u)), __uint_as_float(ref[q]),
-                                 tfar[q]);
-            uint32_t* st = reinterpret_cast<uint32_t*>(rec + 4);
-            for (int e = 0; e < wk[q].sp; ++e) st[e] = stack[q].get(e);
-            if (kPrimary) {
-              Primary pr;
-              (void)primary_path(f, idiv, pid[q], pr);
-              rec[0] = f4(f.cam_pos, __uint_as_float(pr.rng));
-              rec[1] = f4(r[q].d, __uint_as_float(pid[q]));
-              rec[2] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(0u));
-            } else {
-              rec[0] = rs.o[id[q]];
-              rec[1] = rs.d[id[q]];
-              rec[2] = f4(xyz(rs.thr[id[q]]), __uint_as_float((uint32_t)depth));
-            }
-            have[q] = false;
-          }
-        }
-      }
-      const bool fin = have[q] && done[q];
-      if (fin && !wk[q].hit) {
-        if (defer) {
-          if (sh.debug_mode != 1) rs.thr[id[q]] = f4(xyz(rs.thr[id[q]]) * env_color<kCube>(sh, renormalized_again(r[q].d)), 0.0f);
-        } else if (sh.debug_mode == 1) {
-          w.rad[pid[q]] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        } else {
-          const vec3 e = env_color<kCube>(sh, renormalized_again(r[q].d));
-          vec3 rv;
-          if (kPrimary) rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * e;
-          else rv = xyz(w.rad[pid[q]]) + xyz(rs.thr[id[q]]) * e;
-          w.rad[pid[q]] = f4(rv, 0.0f);
-        }
-      }
-      const bool rec = fin && (wk[q].hit || defer);
-      const uint32_t j = block_append(&s_cnt, rec);
-      if (rec) {
-        if (seg0 + j < w.hrec_cap)
-          w.hrec.put(seg0 + j, id[q], wk[q].hit ? __float_as_uint(tfar[q]) : pid[q], wk[q].hit ? ref[q] : kNoHit);
-        else w.tot[kTotOverflow] = 1ull;
-      }
-      if (fin) have[q] = false;
-    }
-  }
-  seg_publish(w.segH, &s_cnt, cap);
-  report_stack(vc, w.tot);
 }
 
 // --------------------------------------------------------------------------------- shading steps
@@ -2301,9 +2094,6 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
   __shared__ DevMaterial smat[32];
   __shared__ uint32_t s_cnt_n, s_cnt_s, s_rays;
   __shared__ LdsStackN<kFuse ? kFuseStack : 1> s_stack;
-#if SPTR_SORT_OCTANT
-  __shared__ uint32_t s_hist[16];
-#endif
   const uint32_t nm = stage_materials(sh, smat);
   if (threadIdx.x == 0) s_cnt_n = s_cnt_s = s_rays = 0u;
   if (blockIdx.x == 0 && threadIdx.x < kXcds) {
@@ -2405,11 +2195,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
     }
     if (active && sh.debug_mode != 1) cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
     if (!kFuse && active && dirty) w.rad[p] = f4(radv, 0.0f);
-#if SPTR_SORT_OCTANT
-    const uint32_t jn = block_append_key(&s_cnt_n, s_hist, cont, cont ? octant(nd.x, nd.y, nd.z) : 0u);
-#else
     const uint32_t jn = block_append(&s_cnt_n, cont);
-#endif
     if (cont && sd.seg0 + jn >= w.seg_cap) {
       cont = false;
       w.tot[kTotOverflow] = 1ull;
@@ -2681,7 +2467,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
     // per hit leaf (r03x A/B: C5 shadow 2.65 -> 2.12 ms/step); L2-resident scenes keep the leaf-inline
     // walk, whose serial leaf fetches are L2 hits (C3 0.30 inline vs 0.35 unified)
     if (have && !done)
-      done = wide_walk<true, kCount, kQueue && SPTR_WALK_UNIFIED>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris,
+      done = wide_walk<true, kCount, kQueue>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris,
                                                                    sv.sph, r, 1e-4f, tfar, ref, vc, kDynSteps);
     if (have && done) {
       if (kCount) hist_ray(s_hist, vc.nodes - v0);
@@ -2823,7 +2609,6 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
 // between.  A bounce-0 path starts from zero radiance, as k_shade<primary> does.  The handed-off ray
 // itself was counted by its trace launch; the later bounces' closest-hit and the any-hit queries are
 // added to the totals here (atomics: k_shadow_dyn may be updating the per-block tallies meanwhile).
-static_assert(SPTR_PRIMARY_UNIFIED == 1 || SPTR_WALK_UNIFIED == 0, "k_strag resumes camera and bounce rays with one walk kind");
 #ifndef SPTR_STRAG_WAVES
 #define SPTR_STRAG_WAVES SPTR_TAIL_WAVES
 #endif
@@ -2890,7 +2675,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_STRAG_WAVES) k_strag(SceneView sv
       if (first) {  // the handed-off ray: its walk resumes where k_trace_dyn left it (the same walk kind)
         tfar = tfar0;
         ref = ref0;
-        (void)walk_steps<false, true, kW4, SPTR_WALK_UNIFIED != 0>(wk, stack, sc, top, ntop, make_ray(ro, rd), 0.0f,
+        (void)walk_steps<false, true, kW4, true>(wk, stack, sc, top, ntop, make_ray(ro, rd), 0.0f,
                                                                   tfar, ref, vr, 0x7FFFFFFF);
         hit = wk.hit;
       } else {
@@ -2963,67 +2748,12 @@ __global__ void __launch_bounds__(kBlock, SPTR_STRAG_WAVES) k_strag(SceneView sv
 __device__ __forceinline__ bool sky_pixel(const FrameView& f, uint32_t l, int& x, int& y) {
   return pixel_culled(f, l) && local_pixel(f, l, x, y);
 }
-//
-// Work distribution (r04): a pixel's samples are one serial sum, so with a thread per pixel the
-// launch is made of units k samples long (C3: 256), dealt in blocks that also held the unculled pixels
-// (idle lanes) — and it ended on the last blocks' whole sample loops.  kLanes = 8: a lane group per
-// culled pixel, taken 8 pixels per wave from k_cull's list of culled pixels (plist[P - 1 - j]) through
-// a queue (FrameView::dyn[kDynSkyQueue], zeroed by k_frame_dyn and k_accum); lane q computes sample
-// r * 8 + q of round r, and the group adds the 8 radiances into the pixel's sum in sample order (the
-// fold of k_trace_wp), so every lane works and a unit is k / 8 samples long.  kLanes = 1 (batches of
-// fewer than 8 samples, or no list): a thread per pixel over the local pixels, the r03 kernel.
-template <bool kCube, uint32_t kLanes>
+// (r04 A/B: lane groups of 8 per culled pixel fed by per-XCD queues over a list of the culled pixels
+// cost C3 0.6 ms: the fold's shuffles and the queue grabs outweigh the idle lanes of mixed waves.)
+template <bool kCube>
 __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
   const FrameView f = frame_dyn(fin);
   const ImageDiv idiv = image_div(f);
-  if constexpr (kLanes > 1u) {
-    const uint32_t n_cull = f.plist[f.P + 1u];  // k_cull's other list: culled pixels and tile slots outside the image
-    // per-XCD counters (128 B apart): counter x hands out the 64-pixel chunks c = 8 u + x, a wave works
-    // through a chunk 8 pixels at a time (grids of fewer than 8 blocks use counter 0 for every chunk)
-    const uint32_t nq = gridDim.x >= kXcds ? kXcds : 1u, qx = blockIdx.x % nq;
-    uint32_t* queue = const_cast<uint32_t*>(f.dyn) + kDynSkyQueue + 32u * qx;
-    const uint32_t lane = lane_id(), q = lane & (kLanes - 1u), g0 = lane & ~(kLanes - 1u);
-    constexpr uint32_t kWavePix = 64u / kLanes;  // pixels per wave round
-    constexpr uint32_t kChunkPix = 64u;          // pixels per queue grab
-    const uint32_t rounds = (f.k + kLanes - 1u) / kLanes;
-    uint32_t cbase = 0u, cend = 0u;
-    for (;;) {
-      if (cbase >= cend) {
-        uint32_t u = 0u;
-        if (lane == 0u) u = atomicAdd(queue, 1u);
-        u = __shfl(u, 0);
-        cbase = (u * nq + qx) * kChunkPix;
-        if (cbase >= n_cull) break;
-        cend = min(cbase + kChunkPix, n_cull);
-      }
-      const uint32_t base = cbase;
-      cbase += kWavePix;
-      const uint32_t j = base + lane / kLanes;
-      const uint32_t l = j < cend ? f.plist[f.P - 1u - j] : kNoHit;
-      int x = 0, y = 0;
-      const bool valid = l < f.P && sky_pixel(f, l, x, y);
-      vec3 a = v3(0.0f, 0.0f, 0.0f);
-      if (valid && !f.reset) a = xyz(f.accum[l]);
-      const uint32_t ps = (uint32_t)(y * f.W + x);
-      for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t smp = r * kLanes + q;
-        vec3 rv = v3(0.0f, 0.0f, 0.0f);
-        if (valid && smp < f.k && sh.debug_mode != 1) {
-          Primary pr;
-          primary_at(f, idiv, x, y, ps, f.acc0 + smp, pr);
-          rv = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * env_color<kCube>(sh, renormalized_again(pr.d));
-        }
-        const uint32_t nact = min(kLanes, f.k - r * kLanes);
-#pragma unroll
-        for (uint32_t s = 0; s < kLanes; ++s) {
-          const float vx = __shfl(rv.x, (int)(g0 + s)), vy = __shfl(rv.y, (int)(g0 + s)), vz = __shfl(rv.z, (int)(g0 + s));
-          if (s < nact) a = v3(a.x + vx, a.y + vy, a.z + vz);
-        }
-      }
-      if (valid && q == 0u) f.accum[l] = make_float4(a.x, a.y, a.z, __uint_as_float(f.k));
-    }
-    return;
-  }
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
     int x, y;
     // only the culled pixels' words: k_accum sums the others (sky_pixel)
@@ -3103,11 +2833,8 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
                                                   uint8_t* image) {
   const FrameView f = frame_dyn(fin);
   const uint32_t n_total = f.dyn ? f.dyn[2] : 0u;  // total frames of the accumulation (kResolve)
-  // the next batch's bounce-0 trace (k_trace_pm, k_trace_wp, k_trace_dyn) and k_sky take their work
-  // from fresh queues
+  // the next batch's bounce-0 trace (k_trace_dyn) takes its work from fresh queues
   if (blockIdx.x == 0) {
-    if (f.dyn && threadIdx.x == 0) const_cast<uint32_t*>(f.dyn)[kDynPmQueue] = 0u;
-    if (f.dyn && threadIdx.x >= 64 && threadIdx.x < 64 + kXcds) const_cast<uint32_t*>(f.dyn)[kDynSkyQueue + 32u * (threadIdx.x - 64)] = 0u;
     if (threadIdx.x < kXcds) w.work[kWorkTraceQueue + threadIdx.x * 32u] = 0u;
     // the straggler counts of this batch's bounces (their k_strag launches were joined before this one)
     if (threadIdx.x >= 128 && threadIdx.x < 128 + kStragBounces) w.work[kWorkStrag + (threadIdx.x - 128) * 32u] = 0u;
@@ -3778,7 +3505,7 @@ SceneView scene_view(const Context& c) {
   s.lds_bytes = bytes <= kLdsSceneBytes ? (uint32_t)bytes : 0u;
   s.scene_bytes = bytes;
   // the refilling wide-BVH kernels of L2/HBM scenes stage the top levels (4-wide nodes only)
-  s.num_top4 = (SPTR_TOP_LDS && s.width == (uint32_t)kWide && kWide == 4 && s.lds_bytes == 0u) ? c.num_top4 : 0u;
+  s.num_top4 = (s.width == (uint32_t)kWide && kWide == 4 && s.lds_bytes == 0u) ? c.num_top4 : 0u;
   return s;
 }
 
@@ -3840,26 +3567,6 @@ static unsigned dispatch(Fn&& fn, Flags<B...>, bool first, Rest... rest) {
   return first ? dispatch(fn, Flags<B..., true>{}, rest...) : dispatch(fn, Flags<B..., false>{}, rest...);
 }
 
-// experiment knobs: SPTR_NO_DYN keeps the statically scheduled trace/shadow kernels for wide BVHs;
-// SPTR_DYN_LDS=0/1 selects the refilling trace for the later bounces of LDS-staged scenes
-static bool dyn_lds() {
-#ifdef SPTR_EXPERIMENT_KNOBS
-  static const bool v = getenv("SPTR_DYN_LDS") ? atoi(getenv("SPTR_DYN_LDS")) != 0 : kDynLds;
-  return v;
-#else
-  return kDynLds;
-#endif
-}
-// SPTR_TRACE_QUEUE=0 (A/B builds): k_trace_dyn keeps the block's static share
-static bool trace_queue() { return SPTR_TRACE_QUEUE != 0; }
-static bool no_dyn() {
-#ifdef SPTR_EXPERIMENT_KNOBS
-  static const bool v = getenv("SPTR_NO_DYN") != nullptr;
-  return v;
-#else
-  return false;
-#endif
-}
 
 unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                       bool count, uint32_t nseg, hipStream_t s) {
@@ -3899,36 +3606,19 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         },
         Flags<>{}, count, W, cube);
   }
-  if (((!L && W) || (L && !W && !P && dyn_lds())) && !no_dyn()) {  // refilling lanes
-    const unsigned lbd = lb + (!L && W ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
+  if (!L && W) {  // refilling lanes (scenes traversed from L2/HBM)
+    const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (as k_shadow_dyn)
-    const bool queue = !L && W && sv.scene_bytes > kL2BytesPerXcd && trace_queue();
-    if constexpr (SPTR_TRACE_PAIR != 0) {
-      if (!L && W && !count && kWide == 4) {  // two rays per lane (measured slower, off: DESIGN.md §8)
-      return dispatch(
-          [&](auto fl) -> unsigned {
-            return [&]<bool Pc, bool Cube, bool Q>(Flags<Pc, Cube, Q>) {
-              const unsigned g = resident_grid((const void*)&k_trace_dyn2<Pc, Cube, Q>, lbd);
-              hipLaunchKernelGGL((k_trace_dyn2<Pc, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
-              return g;
-            }(fl);
-          },
-          Flags<>{}, P, cube, queue);
-      }
-    }
+    const bool queue = trace_queue_applies(sv);
     return dispatch(
         [&](auto fl) -> unsigned {
-          return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube, bool Q>(Flags<Lc, C, Pc, Wc, Cube, Q>) {
-            if constexpr (Lc == Wc || (Q && Lc)) {
-              return 0u;  // not instantiated: LDS scenes traverse BVH2, L2/HBM scenes the wide BVH
-            } else {
-              const unsigned g = resident_grid((const void*)&k_trace_dyn<Lc, C, Pc, Wc, Cube, Q>, lbd);
-              hipLaunchKernelGGL((k_trace_dyn<Lc, C, Pc, Wc, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
-              return g;
-            }
+          return [&]<bool C, bool Pc, bool Cube, bool Q>(Flags<C, Pc, Cube, Q>) {
+            const unsigned g = resident_grid((const void*)&k_trace_dyn<false, C, Pc, true, Cube, Q>, lbd);
+            hipLaunchKernelGGL((k_trace_dyn<false, C, Pc, true, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
+            return g;
           }(fl);
         },
-        Flags<>{}, L, count, P, W, cube, queue);
+        Flags<>{}, count, P, cube, queue);
   }
   return dispatch(
       [&](auto fl) -> unsigned {
@@ -3944,7 +3634,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
 // the any-hit stage runs as k_shadow_dyn and the bounce traces as k_trace_dyn (scenes traversed from
 // L2/HBM, one light): the pair enqueue_wavefront overlaps (bounce traces defer their misses to k_shade)
 bool shadow_overlaps(const SceneView& sv, const WaveView& w) {
-  return sv.lds_bytes == 0 && sv.width == (uint32_t)kWide && w.L == 1u && !no_dyn();
+  return sv.lds_bytes == 0 && sv.width == (uint32_t)kWide && w.L == 1u;
 }
 
 bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count) {
@@ -3998,7 +3688,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   const bool W = sv.width == (uint32_t)kWide;
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
-  if (!L && W && w.L == 1u && !no_dyn()) {  // wide BVH from L2/HBM, one light: refilling lanes
+  if (!L && W && w.L == 1u) {  // wide BVH from L2/HBM, one light: refilling lanes
     const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (k_shadow_dyn kQueue)
     const bool queue = sv.scene_bytes > kL2BytesPerXcd;
@@ -4044,9 +3734,10 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
       Flags<>{}, L, sv.width == (uint32_t)kWide, sh.env.env != nullptr);
 }
 
-bool strag_applies(const SceneView& sv) {
-  return sv.lds_bytes == 0u && sv.width == (uint32_t)kWide && sv.scene_bytes > kL2BytesPerXcd && !no_dyn();
+bool trace_queue_applies(const SceneView& sv) {
+  return sv.lds_bytes == 0u && sv.width == (uint32_t)kWide && sv.scene_bytes > kL2BytesPerXcd;
 }
+bool strag_applies(const SceneView& sv) { return trace_queue_applies(sv); }
 
 // a fixed grid: the number of handed-off paths is known only on the device (k_strag reads it).  Small,
 // so that it holds few of the wave slots the chain's resident grids expect (r04k: 1024 blocks, 16 waves
@@ -4114,16 +3805,8 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
   constexpr unsigned cap = 16384u;
 #endif
   const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
-  if (SPTR_SKY_LANES && f.plist && f.dyn && f.k >= 8u) {  // lane groups over k_cull's culled-pixel list, resident grid
-    const bool cube = sh.env.env != nullptr;
-    const void* fn = cube ? (const void*)&k_sky<true, 8u> : (const void*)&k_sky<false, 8u>;
-    const unsigned gr = std::min<unsigned>(resident_grid(fn, 0u), std::max(1u, g));
-    if (cube) hipLaunchKernelGGL((k_sky<true, 8u>), dim3(gr), dim3(kBlock), 0, s, sh.env, f);
-    else hipLaunchKernelGGL((k_sky<false, 8u>), dim3(gr), dim3(kBlock), 0, s, sh.env, f);
-    return;
-  }
-  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_sky<true, 1u>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
-  else hipLaunchKernelGGL((k_sky<false, 1u>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_sky<true>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  else hipLaunchKernelGGL((k_sky<false>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
 }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,

@@ -108,19 +108,21 @@ inline bool host_local_pixel(const Context& c, uint32_t l, int& x, int& y) {
 // segment tables (3 x (kMaxSegs + 4) u32), per-block tallies (2 x kMaxSegs u64), work counters
 size_t seg_table_bytes() { return 3 * (kMaxSegs + 4) * 4 + 2 * kMaxSegs * 8 + kWorkWords * 4; }
 
-// device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record, radiance, and
-// L shadow tasks of ts float4s
-uint64_t wave_path_bytes(uint32_t L, uint32_t ts) { return 2 * 3 * 16 + kHrecQueueMult * kHitBytes + 16 + (uint64_t)L * ts * 16; }
+// device bytes per path slot of a wave: ray streams 2 x (o, d, thr), hit record(s), radiance, and
+// L shadow tasks of ts float4s.  hrec_mult: hit-record segments per static share (2 when the trace
+// takes its rays from the per-XCD queues, trace_queue_applies; else 1).
+uint64_t wave_path_bytes(uint32_t L, uint32_t ts, uint32_t hrec_mult) {
+  return 2 * 3 * 16 + hrec_mult * kHitBytes + 16 + (uint64_t)L * ts * 16;
+}
 // fixed segment slack of a wave's streams (see ensure_wave); k_slack = hit-record slack multiplier
-uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack) {
+uint64_t wave_slack_bytes(uint32_t L, uint32_t ts, uint32_t k_slack, uint32_t hrec_mult) {
   const uint64_t recs = (uint64_t)kMaxSegs * kBlock;
-  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + kHrecQueueMult * recs * k_slack * kHitBytes;
+  return recs * (2 * 3 * 16 + (uint64_t)(L ? L : 1u) * ts * 16) + hrec_mult * recs * k_slack * kHitBytes;
 }
 
 // k_slack: the pixel-major bounce-0 trace gives each block a hit-record segment of k records per
-// pixel slot it may take, twice its static share (k_trace_pm's work queue), so the hit records span
-// 2 (cap + kMaxSegs * kBlock * k) (k_slack = k); every other producer needs cap + kMaxSegs * kBlock
-// (k_slack = 1).
+// pixel slot of its static share, so the hit records span cap + kMaxSegs * kBlock * k (k_slack = k);
+// every other producer needs cap + kMaxSegs * kBlock (k_slack = 1).  hrec_mult: see wave_path_bytes.
 int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_slack, uint32_t hrec_mult) {
   WaveBufs& b = c.wb;
   L = L ? L : 1u;
@@ -165,12 +167,8 @@ WaveView wave_view(Context& c) {
     w.rs[b].thr = static_cast<float4*>(wb.rs[b][2].p);
   }
   const uint64_t hcap = std::min<uint64_t>(wb.hrec.bytes / kHitBytes, 0xFFFFFFFFull);
-#if SPTR_HREC16
-  w.hrec.r = static_cast<uint4*>(wb.hrec.p);
-#else
   w.hrec.tr = static_cast<uint2*>(wb.hrec.p);
   w.hrec.id = reinterpret_cast<uint32_t*>(static_cast<char*>(wb.hrec.p) + hcap * 8u);
-#endif
   w.rad = static_cast<float4*>(wb.rad.p);
   w.stask = static_cast<float4*>(wb.stask.p);
   uint32_t* seg = static_cast<uint32_t*>(wb.seg.p);  // 3 tables of kMaxSegs counts + 1 stride
@@ -237,7 +235,6 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   v.sky_fold = 0u;
   v.plist = nullptr;
   v.unculled = nullptr;
-  v.pm_order = nullptr;
   v.integrator = f.integrator;
   v.spf = f.samples_per_frame ? f.samples_per_frame : 4u;
   return v;
@@ -589,12 +586,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     fv.acc0 = done;                  // offset from the call's frame_begin (frame_dyn)
     fv.reset = done == 0 ? 1u : 0u;  // and the call's reset flag applies to its first batch only
     fv.pixel_major = bounce0_pixel_major(sv, fv);
-    // culled pixels summed by k_sky (beside the trace when launches overlap): path-major batches, and
-    // the thread-per-pixel bounce 0 (SPTR_PM_SKY: k_trace_pm then takes only k_cull's unculled pixels)
-    fv.sky_fold = (fv.cull != nullptr && (fv.pixel_major == kFoldNone ||
-                                          (SPTR_PM_SKY != 0 && fv.pixel_major == kFoldThread))) ? 1u : 0u;
+    // culled pixels summed by k_sky (beside the trace when launches overlap): path-major batches.
+    // (r04s: handing them to k_sky beside the thread-per-pixel bounce 0 too: C2 3.09-3.20 -> 3.54-3.57 ms)
+    fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
     fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
-    fv.pm_order = (fv.cull != nullptr && fv.pixel_major != kFoldNone) ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
     // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
     // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
     // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
@@ -832,7 +827,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   // with side-stream launches replays slower than it launches directly (r04h: C5 8.70 vs 8.18 ms,
   // C3 3.80 vs 3.75; C2, which forks nothing, 3.07 vs 3.10).  Mode 3 captures every repeated shape.
   const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && (!c.last_forked || samples <= kGraphForkedMaxSamples));
-  if (!graphable || timing || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) {
+  const bool bad = c.have_bad_key && same_key(key, c.bad_key);  // this shape failed to capture before
+  auto direct = [&]() -> int {
     c.last_forked = false;  // (set by the launch sequence if it forks)
     StageTimer tm{c, timing, trace_only, s};
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
@@ -840,10 +836,24 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     API_HIP(hipGetLastError());
     if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + tm.what + ": " + hipGetErrorString(tm.err));
     return SPTR_OK;
-  }
+  };
+  if (!graphable || timing || bad || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) return direct();
   if (!(c.graph.valid && same_key(key, c.graph.key))) {  // capture this shape
     drop_graph(c);
     GraphShape gshape;
+    // A shape that cannot be captured (the capture fails, leaves a forked stream capturing, or yields
+    // a graph check_graph rejects or the runtime cannot instantiate) is remembered and launched
+    // directly, this call and every later one: the direct launches are safe (the runtime faults
+    // only while ending a capture), and a failing shape re-captured per call would never render.
+    // graph_info / sptr_capture_error report why.
+    auto not_capturable = [&](hipError_t status, const std::string& why) -> int {
+      c.capture_status = (int32_t)(status != hipSuccess ? status : hipErrorUnknown);
+      c.capture_error = why;
+      c.bad_key = key;
+      c.have_bad_key = true;
+      (void)hipGetLastError();
+      return direct();
+    };
     API_HIP(hipStreamBeginCapture(c.cap_stream, hipStreamCaptureModeThreadLocal));
     StageTimer tm{c, false, false, c.cap_stream};
     tm.capturing = true;
@@ -851,34 +861,33 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(c.cap_stream, &g);
     // every stream the capture forked must have left capture mode with it (a stream still capturing
-    // would fold the next direct launches into a dead graph)
+    // would fold the next direct launches into a dead graph): end the capture on any that did not
+    bool stuck = false;
     for (hipStream_t st : {c.cap_stream, c.cap_side, c.cap_side2}) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-        if (g) (void)hipGraphDestroy(g);
-        return fail(c, SPTR_ERR_HIP, "render: graph capture: a forked stream is still capturing (internal error)");
+        stuck = true;
+        hipGraph_t gs = nullptr;
+        (void)hipStreamEndCapture(st, &gs);
+        if (gs) (void)hipGraphDestroy(gs);
       }
     }
-    if (ec == hipSuccess && tm.err == hipSuccess && g) {
+    if (stuck) {
+      if (g) (void)hipGraphDestroy(g);
+      return not_capturable(hipErrorStreamCaptureUnjoined, "graph capture: a forked stream was still capturing");
+    }
+    if (ec != hipSuccess || tm.err != hipSuccess || !g) {
+      if (g) (void)hipGraphDestroy(g);
+      return not_capturable(ec != hipSuccess ? ec : tm.err,
+                            ec != hipSuccess ? std::string("hipStreamEndCapture: ") + hipGetErrorString(ec)
+                                             : tm.what + ": " + hipGetErrorString(tm.err));
+    }
+    {
       std::string why;
       if (!check_graph(g, gshape, why)) {
         (void)hipGraphDestroy(g);
-        return fail(c, SPTR_ERR_HIP, "render: captured graph rejected: " + why);
+        return not_capturable(hipErrorInvalidValue, "captured graph rejected: " + why);
       }
-    }
-    if (ec != hipSuccess || tm.err != hipSuccess || !g) {
-      // not capturable: direct launches (graph_info reports why)
-      c.capture_status = (int32_t)(ec != hipSuccess ? ec : (tm.err != hipSuccess ? tm.err : hipErrorUnknown));
-      c.capture_error = ec != hipSuccess ? std::string("hipStreamEndCapture: ") + hipGetErrorString(ec)
-                                         : tm.what + ": " + hipGetErrorString(tm.err);
-      if (g) (void)hipGraphDestroy(g);
-      (void)hipGetLastError();
-      StageTimer td{c, timing, trace_only, s};
-      launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
-      waves = enqueue(s, td);
-      API_HIP(hipGetLastError());
-      if (td.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + td.what + ": " + hipGetErrorString(td.err));
-      return SPTR_OK;
     }
     GraphCache gc;
     gc.graph = g;
@@ -909,7 +918,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     const hipError_t ei = hipGraphInstantiate(&gc.exec, g, nullptr, nullptr, 0);
     if (ei != hipSuccess) {
       (void)hipGraphDestroy(g);
-      return fail(c, SPTR_ERR_HIP, std::string("render: graph instantiate: ") + hipGetErrorString(ei));
+      return not_capturable(ei, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
     }
     gc.valid = true;
     c.graph = gc;
@@ -1295,12 +1304,13 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       if (c.wb.cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
-          const uint64_t held = c.wb.cap ? c.wb.cap * wave_path_bytes(c.wb.L, c.wb.ts) : 0ull;
+          const uint32_t hm = trace_queue_applies(scene_view(c)) ? 2u : 1u;
+          const uint64_t held = c.wb.cap ? c.wb.cap * wave_path_bytes(c.wb.L, c.wb.ts, hm) : 0ull;
           const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
           // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
           const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
-                                (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u));
-          const uint64_t fit = budget > 0.0 ? (uint64_t)budget / wave_path_bytes(L, task_stride(c)) : 0ull;
+                                (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u), hm);
+          const uint64_t fit = budget > 0.0 ? (uint64_t)budget / wave_path_bytes(L, task_stride(c), hm) : 0ull;
           wave_paths = std::max<uint64_t>(1ull << 24, std::min<uint64_t>(wave_paths, fit));
         }
       }
@@ -1316,8 +1326,9 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
         probe.k = f->spp % k;
         pm = pm || bounce0_pixel_major(scene_view(c), probe) != 0u;
       }
-      // hit-record segments hold twice the static shares (the bounce-0 work queues, k_trace_dyn's per-XCD queues)
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u, kHrecQueueMult);
+      // hit-record segments hold twice the static shares when k_trace_dyn takes its rays from the per-XCD queues
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u,
+                       trace_queue_applies(scene_view(c)) ? 2u : 1u);
       if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));

@@ -44,14 +44,10 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;
 constexpr int kTile = 32;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kMaxLights = 8;
-// Collapsed ("wide") BVH: every kWideLevels-th level of the LBVH, kWide children per node.
-#ifndef SPTR_WIDE
-#define SPTR_WIDE 4
-#endif
-constexpr int kWide = SPTR_WIDE;
-static_assert(kWide == 4 || kWide == 8, "wide BVH: 4 or 8 children");
-constexpr int kWideLevels = kWide == 8 ? 3 : 2;  // BVH2 levels per wide level
-constexpr int kQWords = kWide / 4;         // u32 words per quantised plane, one byte per child
+// Collapsed ("wide") BVH: 4 children per node (8-wide measured slower: C5 22.5 -> 28.6 ms/step, spills).
+constexpr int kWide = 4;
+constexpr int kWideLevels = 2;  // BVH2 levels per wide level
+constexpr int kQWords = 1;      // u32 words per quantised plane, one byte per child
 // The wide BVH's top kTopLevels levels (at most 1 + 4 + 16 = 21 nodes, 1.3 KB) take wide indices
 // 0..num_top4-1, so a kernel can stage them in LDS and tell an LDS node by its index alone.
 constexpr int kTopLevels = 3;
@@ -61,7 +57,7 @@ constexpr int kMaxDepth = 32;
 // (wide) entries; build_lbvh records both bounds, scene_view never picks a width whose bound
 // exceeds kStack, and a push that would still overflow is dropped and reported
 // (kTotStackOverflow), never silent.
-constexpr int kStack = kWide == 8 ? 112 : 96;
+constexpr int kStack = 96;
 constexpr int kBlock = 256;
 #ifndef SPTR_TREELET_PASSES
 #define SPTR_TREELET_PASSES 3
@@ -77,7 +73,7 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "node size");
 
-// Wide BVH node (64 B for 4 children = half a 128-B cache line; 128 B for 8): the child boxes
+// Wide BVH node (64 B = half a 128-B cache line): the child boxes
 // quantised to 8 bits per plane on a per-node, per-axis power-of-two grid anchored at the node's
 // lower corner (org).  Child k's box is [org + qlo_k * 2^e, org + qhi_k * 2^e] per axis, rounded
 // outwards at build time (k_collapse_wide), so it contains the exact child box; traverse_wide
@@ -88,9 +84,9 @@ struct alignas(16) WideNode {
   uint32_t link[kWide];      // child: internal node index | leaf range (kLeafBit) | kNoHit
   uint32_t q[6][kQWords];    // planes lo x, hi x, lo y, hi y, lo z, hi z; byte k % 4 of word k / 4
   uint32_t parent;           // wide-node index (build bookkeeping, not traversed)
-  uint32_t pad[kWide == 8 ? 7 : 1];
+  uint32_t pad[1];
 };
-static_assert(sizeof(WideNode) == (kWide == 8 ? 128 : 64), "node size");
+static_assert(sizeof(WideNode) == 64, "node size");
 
 struct DevMaterial {  // == sptr_material
   float albedo[3];
@@ -169,32 +165,8 @@ struct FrameView {
   uint32_t cull_depth;   // BVH2 levels k_cull tests (<= kCullDepthMax)
   const uint32_t* plist; // with sky_fold: the unculled local pixels (count at plist[P]), bounce 0's paths
   const uint32_t* unculled;  // with cull: the number of unculled valid local pixels (k_cull's plist[P])
-  const uint32_t* pm_order;  // pixel-major bounce 0 with a cull mask: k_cull's list (unculled first), else null
 };
-// FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn), and the work queue of
-// the pixel-major bounce 0 (k_trace_pm), zeroed by k_frame_dyn and k_accum
-// r04 work distribution (A/B builds; measured r04f, DESIGN.md §8: the first two slower, so off):
-// SPTR_PM_QUEUE, the pixel-major bounce 0 takes 64-pixel chunks from a queue in k_cull's order;
-// SPTR_SKY_LANES, k_sky runs lane groups over k_cull's culled list through per-XCD queues;
-// SPTR_TRACE_QUEUE, k_trace_dyn of scenes beyond an XCD's L2 takes work from per-XCD queues: within
-// noise alone (r04f), on since the straggler hand-off (r04l: with k_strag's blocks resident beside it
-// a static share leaves late-starting blocks a tail; C5 8.68 -> 8.49 ms at 8 lanes, grid 128)
-#ifndef SPTR_PM_QUEUE
-#define SPTR_PM_QUEUE 0
-#endif
-#ifndef SPTR_SKY_LANES
-#define SPTR_SKY_LANES 0
-#endif
-#ifndef SPTR_PM_SKY
-#define SPTR_PM_SKY 0  // 1: the thread-per-pixel bounce 0 leaves its culled pixels to k_sky (r04s: C2 3.09-3.20 -> 3.54-3.57 ms, off)
-#endif
-#ifndef SPTR_TRACE_QUEUE
-#define SPTR_TRACE_QUEUE 1
-#endif
-// hit-record segments hold twice the static shares when a producer takes work from a queue
-constexpr uint32_t kHrecQueueMult = (SPTR_PM_QUEUE || SPTR_TRACE_QUEUE) ? 2u : 1u;
-constexpr uint32_t kDynPmQueue = 32;   // a 128-B line of its own
-constexpr uint32_t kDynSkyQueue = 64;  // k_sky's per-XCD work queues, 32 words (128 B) apart
+// FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn).
 constexpr size_t kDynBytes = 2048;
 constexpr uint64_t kGraphForkedMaxSamples = 1ull << 22;  // run_call: graphs for forked calls up to this size
 
@@ -261,25 +233,8 @@ struct SegTable {
 
 // Hit records: per hit of a trace stage, the ray's input slot (bounce 0: its path id), its t bits and
 // the primitive ref, 12 B in two dense arrays — {t, ref} (8 B, one dwordx2 per lane) and the slot (4 B,
-// one dword) — so every access is a naturally aligned coalesced stream.  SPTR_HREC16 = 1: one uint4
-// record (16 B, A/B builds).  (r03: a packed 12-B uint3 record, one dwordx3 per lane, was 2 % slower on
-// C2 than the 16-B record.)
-#ifndef SPTR_HREC16
-#define SPTR_HREC16 0
-#endif
-#if SPTR_HREC16
-constexpr size_t kHitBytes = 16;
-struct HitStream {
-  uint4* r;
-  __device__ __forceinline__ void put(uint32_t j, uint32_t id, uint32_t tb, uint32_t ref) const { r[j] = make_uint4(id, tb, ref, 0u); }
-  __device__ __forceinline__ void get(uint32_t j, uint32_t& id, uint32_t& tb, uint32_t& ref) const {
-    const uint4 v = r[j];
-    id = v.x;
-    tb = v.y;
-    ref = v.z;
-  }
-};
-#else
+// one dword) — so every access is a naturally aligned coalesced stream.  (r03: this split form replaced
+// a 16-B uint4 record; a packed 12-B uint3 record, one dwordx3 per lane, measured 2 % slower on C2.)
 constexpr size_t kHitBytes = 12;
 struct HitStream {
   uint2* tr;     // {t bits, prim ref}
@@ -295,7 +250,6 @@ struct HitStream {
     ref = v.y;
   }
 };
-#endif
 
 struct RayStream {
   float4* o;    // origin.xyz, rng state bits
@@ -396,6 +350,8 @@ struct Context {
   uint32_t captures = 0;             // graphs captured and instantiated
   GraphKey last_key{};               // the previous call's shape: a graph is captured when it repeats
   bool have_last_key = false;
+  GraphKey bad_key{};                // a shape whose capture failed or was rejected: launched directly from then on
+  bool have_bad_key = false;
   std::string err;
   int debug_mode = 0;
   uint64_t wave_paths = 0;  // 0 = default
@@ -481,6 +437,10 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
 void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s);
 // whether bounce traces of this scene hand their stragglers off (wide BVH beyond an XCD's L2)
+// k_trace_dyn of scenes beyond an XCD's L2 takes its rays from per-XCD work queues (r04l: with
+// k_strag's blocks resident beside it a static share leaves late-starting blocks a tail; C5 8.68 ->
+// 8.49 ms at 8 lanes, grid 128); its hit-record segments then hold twice the static shares.
+bool trace_queue_applies(const SceneView& sv);
 bool strag_applies(const SceneView& sv);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 // resolve: also tone-map the sums into tiles (+ image) in the same launch (the call's last batch)

@@ -18,11 +18,12 @@ for name, scene, p0, p1, W, H, S in (("mesh300", "sphere_mesh", 300, 600, 160, 1
     st = r.render(cam, W, H, spp=S)
     out[name] = r.read_accum().view(np.uint32).copy()
     out[name + "_counts"] = np.array([st.rays_closest, st.rays_shadow], np.uint64)
-wl = workloads.WORKLOADS["c3"]
-workloads.setup(r, wl)
-cam = workloads.camera(wl)
-st = r.render(cam, 320, 180, spp=32)
-out["c3"] = r.read_accum().view(np.uint32).copy()
-out["c3_counts"] = np.array([st.rays_closest, st.rays_shadow], np.uint64)
+for name, W, H, S in (("c2", 320, 180, 32), ("c3", 320, 180, 32), ("c5", 320, 180, 8)):
+    wl = workloads.WORKLOADS[name]
+    workloads.setup(r, wl)
+    cam = workloads.camera(wl)
+    st = r.render(cam, W, H, spp=S)
+    out[name] = r.read_accum().view(np.uint32).copy()
+    out[name + "_counts"] = np.array([st.rays_closest, st.rays_shadow], np.uint64)
 np.savez(sys.argv[1], **out)
 print("dumped", sys.argv[1], {k: v.shape for k, v in out.items()})
