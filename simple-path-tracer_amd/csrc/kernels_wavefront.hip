@@ -606,9 +606,22 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
 // leaves (leaf size > 1) are tested with leaf_test on their step.  Same hits: the closest hit is the
 // minimum over the same set of primitives tested against the same rays (ties at exactly equal t
 // may resolve to another primitive, as with any change of traversal order).
+// Walk forms: the leaf-inline walk (wide_walk_inl), the unified walk (one item per step) as r04's
+// branchy step (walk_fetch + walk_apply) or as the branch-free step (walk_step_bf, r05).  The two
+// unified forms visit the same items in the same order (k_strag resumes either's state).
+enum : int { kWalkInline = 0, kWalkUnified = 1, kWalkBranchFree = 2 };
 #ifndef SPTR_WALK_BF
-#define SPTR_WALK_BF 1  // r05: the unified step without divergent branches (walk_step_bf); 0: walk_fetch + walk_apply
+#define SPTR_WALK_BF 1  // the unified walk's form: 1 branch-free, 0 r04's step (A/B builds)
 #endif
+#ifndef SPTR_BF_PRIMARY
+#define SPTR_BF_PRIMARY 0  // 1: camera rays (k_trace_dyn<primary>) take the branch-free form too (r05d A/B: C5
+                           // bounce-0 trace 1.57-1.59 vs 1.46 ms with the r04 step: coherent waves rarely split,
+                           // and the branch-free step runs both the node and the triangle test)
+#endif
+constexpr int kWalkU = SPTR_WALK_BF ? kWalkBranchFree : kWalkUnified;
+constexpr int kWalkPrimary = SPTR_BF_PRIMARY ? kWalkU : kWalkUnified;
+// the branch-free step reads every node from L2/HBM, so kernels stage the LDS top levels only for the others
+__host__ __device__ constexpr bool walk_reads_top(int kind) { return kind != kWalkBranchFree; }
 // One step of the unified walk: its fetch (the 56 B of the item wk.cur names: a wide node from the
 // LDS top levels or L2/HBM, or a direct leaf's triangle / sphere record) and the step proper.
 struct WalkItem {
@@ -865,16 +878,17 @@ __device__ __forceinline__ bool wide_walk_bf(WideWalk& wk, TravStack<N>& stack, 
     if (walk_step_bf<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc)) return true;
   return false;
 }
-// kU: the unified walk; callers choose per ray class (see the kernels)
-template <bool kAny, bool kCount, bool kU = true, int N>
+// kKind: the walk form (kWalk*); callers choose per ray class (see the kernels)
+template <bool kAny, bool kCount, int kKind = kWalkU, int N>
 __device__ __forceinline__ bool wide_walk(WideWalk& wk, TravStack<N>& stack, const WideNode* nodes, const uint4* top,
                                           uint32_t ntop, const uint32_t* prim_ref, const float4* tris, const float4* sph,
                                           const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc, int steps) {
-  if constexpr (kU && SPTR_WALK_BF)
+  if constexpr (kKind == kWalkBranchFree)
     return wide_walk_bf<kAny, kCount>(wk, stack, nodes, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
-  else if constexpr (kU)
+  else if constexpr (kKind == kWalkUnified)
     return wide_walk_u<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
-  return wide_walk_inl<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
+  else
+    return wide_walk_inl<kAny, kCount>(wk, stack, nodes, top, ntop, prim_ref, tris, sph, r, tnear, tfar, ref, vc, steps);
 }
 // Starts a walk at root; true when it is already over (empty scene, or a root leaf tested here).
 template <bool kAny, bool kCount>
@@ -960,9 +974,6 @@ __device__ __forceinline__ bool traverse_w(const Staged& sc, const SceneView& sv
 
 // traverse_w with the wide BVH's top levels read from an LDS copy (stage_top; ntop = 0: none) — the
 // path-per-thread kernels of L2/HBM scenes (k_tail, k_strag), whose every ray starts at the root
-#ifndef SPTR_TAIL_TOP
-#define SPTR_TAIL_TOP 1
-#endif
 template <bool kW4, bool kAny, bool kCount, int N>
 __device__ __forceinline__ bool traverse_w_top(const Staged& sc, const SceneView& sv, const uint4* top, uint32_t ntop,
                                                const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
@@ -1655,12 +1666,12 @@ __device__ __forceinline__ bool walk_start(WideWalk& wk, const Staged& sc, uint3
                                            float& tfar, uint32_t& ref, Visits& vc) {
   return wide_start<kAny, kCount>(wk, root, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc);
 }
-template <bool kAny, bool kCount, bool kW4, bool kU = true, int N>
+template <bool kAny, bool kCount, bool kW4, int kKind = kWalkU, int N>
 __device__ __forceinline__ bool walk_steps(WideWalk& wk, TravStack<N>& stack, const Staged& sc, const uint4* top,
                                            uint32_t ntop, const Ray& r, float tnear, float& tfar, uint32_t& ref, Visits& vc,
                                            int steps) {
   if (kW4)
-    return wide_walk<kAny, kCount, kU>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
+    return wide_walk<kAny, kCount, kKind>(wk, stack, sc.nodes4, top, ntop, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref, vc,
                                    steps);
   return bvh2_walk<kAny, kCount>(wk.cur, wk.sp, wk.hit, stack, sc.nodes, sc.prim_ref, sc.tris, sc.sph, r, tnear, tfar, ref,
                                  vc, steps);
@@ -1769,7 +1780,8 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
   if (threadIdx.x == 0) s_cnt = s_next = s_hits = s_taken = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
-  const uint32_t ntop = (kW4 && !kLds) ? sv.num_top4 : 0u;
+  constexpr int kKind = kPrimary ? kWalkPrimary : kWalkU;
+  const uint32_t ntop = (kW4 && !kLds && walk_reads_top(kKind)) ? sv.num_top4 : 0u;
   const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, kLds, kPrimary, nseg_in)) : nullptr;
   uint32_t n, per_in = 0u, nlist = 0u;
   if (kPrimary) {
@@ -1853,7 +1865,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     // the tree and the launches overlapped: C5 8.45 inline vs 8.22 ms/step unified, means of 3; r03x,
     // before both: 2.15 vs 2.37 ms for the bounce-0 trace)
     if (have && !done)
-      done = walk_steps<false, kCount, kW4, true>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
+      done = walk_steps<false, kCount, kW4, kKind>(wk, stack, sc, top, ntop, r, 0.0f, tfar, ref, vc,
                                                                           kDynSteps);
     // Straggler hand-off: the wave has no rays left to start and at most strag_lanes lanes are still
     // tracing (the long rays that would otherwise set the launch's length while the rest of the chip
@@ -2408,7 +2420,8 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds);
   if (threadIdx.x == 0) s_rays = s_next = 0u;
   if (kCount) hist_init(s_hist);
-  const uint32_t ntop = sv.num_top4;
+  constexpr int kKind = kQueue ? kWalkU : kWalkInline;
+  const uint32_t ntop = walk_reads_top(kKind) ? sv.num_top4 : 0u;
   const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, false, false, nseg_in)) : nullptr;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segS, nseg_in, s_off, per_in);
@@ -2467,7 +2480,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
     // per hit leaf (r03x A/B: C5 shadow 2.65 -> 2.12 ms/step); L2-resident scenes keep the leaf-inline
     // walk, whose serial leaf fetches are L2 hits (C3 0.30 inline vs 0.35 unified)
     if (have && !done)
-      done = wide_walk<true, kCount, kQueue>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris,
+      done = wide_walk<true, kCount, kKind>(wk, stack, sv.nodes4, top, ntop, sv.prim_ref, sv.tris,
                                                                    sv.sph, r, 1e-4f, tfar, ref, vc, kDynSteps);
     if (have && done) {
       if (kCount) hist_ray(s_hist, vc.nodes - v0);
@@ -2508,7 +2521,7 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   if (threadIdx.x == 0u) s_next = 0u;
   const Staged sc = stage_scene<kLds>(sv, lds);
   // the wide BVH's top levels in LDS (L2/HBM scenes), published by seg_scan's barriers
-  const uint32_t ntop = (SPTR_TAIL_TOP && kW4 && !kLds) ? sv.num_top4 : 0u;
+  const uint32_t ntop = (walk_reads_top(kWalkU) && kW4 && !kLds) ? sv.num_top4 : 0u;
   const uint4* top = ntop ? stage_top(sv, lds + top_lds_offset(sv, kLds, false, nseg_in)) : nullptr;
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
@@ -2623,7 +2636,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_STRAG_WAVES) k_strag(SceneView sv
   if (threadIdx.x == 0u) s_next = 0u;
   const Staged sc = stage_scene<false>(sv, nullptr);
   extern __shared__ float4 lds[];
-  const uint32_t ntop = SPTR_TAIL_TOP ? sv.num_top4 : 0u;
+  const uint32_t ntop = walk_reads_top(kWalkU) ? sv.num_top4 : 0u;
   const uint4* top = ntop ? stage_top(sv, lds) : nullptr;
   __syncthreads();
   const uint32_t n = min(w.work[kWorkStrag + (uint32_t)depth0 * 32u], w.strag_cap);
@@ -2675,7 +2688,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_STRAG_WAVES) k_strag(SceneView sv
       if (first) {  // the handed-off ray: its walk resumes where k_trace_dyn left it (the same walk kind)
         tfar = tfar0;
         ref = ref0;
-        (void)walk_steps<false, true, kW4, true>(wk, stack, sc, top, ntop, make_ray(ro, rd), 0.0f,
+        (void)walk_steps<false, true, kW4>(wk, stack, sc, top, ntop, make_ray(ro, rd), 0.0f,
                                                                   tfar, ref, vr, 0x7FFFFFFF);
         hit = wk.hit;
       } else {
@@ -3607,7 +3620,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         Flags<>{}, count, W, cube);
   }
   if (!L && W) {  // refilling lanes (scenes traversed from L2/HBM)
-    const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
+    const unsigned lbd = lb + (walk_reads_top(P ? kWalkPrimary : kWalkU) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (as k_shadow_dyn)
     const bool queue = trace_queue_applies(sv);
     return dispatch(
@@ -3689,9 +3702,9 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
   const unsigned lb = trace_lds(sv, L, false, nseg);
   unsigned g = 0;
   if (!L && W && w.L == 1u) {  // wide BVH from L2/HBM, one light: refilling lanes
-    const unsigned lbd = lb + sv.num_top4 * (unsigned)sizeof(WideNode);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (k_shadow_dyn kQueue)
     const bool queue = sv.scene_bytes > kL2BytesPerXcd;
+    const unsigned lbd = lb + (walk_reads_top(queue ? kWalkU : kWalkInline) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
     return dispatch(
         [&](auto fl) -> unsigned {
           return [&]<bool C, bool Q>(Flags<C, Q>) {
@@ -3722,7 +3735,7 @@ unsigned launch_tail(const SceneView& sv, const ShadeView& sh, const FrameView& 
                      uint32_t nseg, hipStream_t s) {
   const bool L = sv.lds_bytes != 0;
   const bool W = sv.width == (uint32_t)kWide;
-  const unsigned lb = trace_lds(sv, L, false, nseg) + ((SPTR_TAIL_TOP && !L && W) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);
+  const unsigned lb = trace_lds(sv, L, false, nseg) + ((walk_reads_top(kWalkU) && !L && W) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);
   return dispatch(
       [&](auto fl) -> unsigned {
         return [&]<bool Lc, bool Wc, bool Cube>(Flags<Lc, Wc, Cube>) {
@@ -3749,7 +3762,7 @@ bool strag_applies(const SceneView& sv) { return trace_queue_applies(sv); }
 void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                   hipStream_t s) {
   constexpr unsigned kStragGrid = SPTR_STRAG_GRID;
-  const unsigned lb = SPTR_TAIL_TOP ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u;  // the top levels in LDS
+  const unsigned lb = walk_reads_top(kWalkU) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u;  // the top levels in LDS
   if (sh.env.env != nullptr) hipLaunchKernelGGL((k_strag<true, true>), dim3(kStragGrid), dim3(kBlock), lb, s, sv, sh, f, w, depth);
   else hipLaunchKernelGGL((k_strag<true, false>), dim3(kStragGrid), dim3(kBlock), lb, s, sv, sh, f, w, depth);
 }
