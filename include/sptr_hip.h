@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 6
+#define SPTR_ABI_VERSION 7
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -312,6 +312,20 @@ int sptr_occluded(sptr_ctx* ctx, const float* rays, uint32_t n, uint8_t* occlude
  * (W*H*3) and initial path RNG states (W*H), computed by the device kernel. */
 int sptr_primary_rays(sptr_ctx* ctx, const sptr_camera* cam, int32_t width, int32_t height, uint32_t acc,
                       float* dirs, uint32_t* rng);
+/* The LBVH build's device primitives (kernels_sort.hip), exposed for their own tests; they replace
+ * the rocPRIM calls Embree's replacement would otherwise make (EmbreeBackend.cpp:82-181 builds on the
+ * CPU).  Host arrays in and out, n entries each; every call allocates device scratch and waits.
+ *   sptr_sort_pairs_u64: stable ascending LSD radix sort of (keys, vals) (equal keys keep their order);
+ *   sptr_scan_u32: exclusive prefix sum of 32-bit counts (mod 2^32); out may equal in. */
+int sptr_sort_pairs_u64(sptr_ctx* ctx, const uint64_t* keys, const uint32_t* vals, uint32_t n, uint64_t* keys_out,
+                        uint32_t* vals_out);
+int sptr_scan_u32(sptr_ctx* ctx, const uint32_t* in, uint32_t n, uint32_t* out);
+/* The device's values of the wavefront path's two library calls, for the parity residue classifier:
+ * fn SPTR_MATH_COSINE_SINCOS: (sinf, cosf) of the cosine sample's phi = 2 pi r1 for every
+ *   r1 = k / 2^24 (wf_math.h:51-72), out = 2^25 floats, pairs by k; x and n are ignored;
+ * fn SPTR_MATH_GAMMA: powf(x[i], 1/2.2) as the resolve computes it (GLRenderer.cpp:416-430), n values. */
+enum { SPTR_MATH_COSINE_SINCOS = 0, SPTR_MATH_GAMMA = 1 };
+int sptr_eval_math(sptr_ctx* ctx, int fn, const float* x, uint32_t n, float* out);
 
 /* ---- host-side scene layer (the C++ SceneDesc / Camera / MaterialManager / LightManager mirror) ---- */
 typedef struct sptr_host_scene sptr_host_scene;

@@ -38,6 +38,7 @@ class Job(C.Structure):
         ("frame_begin", C.c_uint32), ("num_frames", C.c_uint32), ("max_depth", C.c_uint32),
         ("shard_rank", C.c_int32), ("shard_count", C.c_int32), ("threads", C.c_int32), ("use_bvh", C.c_int32),
         ("accum", C.POINTER(C.c_float)), ("rgb", C.POINTER(C.c_uint8)), ("counters", C.c_uint64 * 4),
+        ("pixels", C.POINTER(C.c_uint32)), ("num_pixels", C.c_uint32),
     ]
 
 
@@ -75,6 +76,8 @@ def lib():
             "oracle_render_pt": (C.c_int, [vp, C.POINTER(Job), C.c_uint32]),
             "oracle_render_optix": (C.c_int, [vp, C.POINTER(Job), fp]),
             "oracle_resolve": (None, [fp, C.c_uint32, C.c_uint32, bp]),
+            "oracle_set_device_math": (None, [fp, C.c_int]),
+            "oracle_path_rays": (C.c_int, [vp, C.POINTER(Job), C.c_int, C.c_int, C.c_uint32, fp, C.c_int]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -174,15 +177,41 @@ class Prepared:
         lib().oracle_occluded(self.h, _f(rays), len(rays), 1 if ub else 0, _b(out))
         return out
 
+    def path_rays(self, cam: np.ndarray, width: int, height: int, materials: np.ndarray, lights: np.ndarray,
+                  x: int, y: int, frame: int, max_depth: int = 6, env_faces: np.ndarray | None = None,
+                  env_intensity: float = 0.8, env_clamp: float = 5.0):
+        """The rays of pixel (x, y)'s wavefront path at accumulation index `frame`, in trace order:
+        (kinds (n,) 0 closest hit / 1 shadow, rays (n, 8) float32 o3 d3 tnear tfar) — residue diagnosis."""
+        mats = np.ascontiguousarray(materials, np.float32)
+        lts = np.ascontiguousarray(lights, np.float32)
+        j = Job()
+        j.materials, j.num_materials = _f(mats), len(mats)
+        j.lights, j.num_lights = _f(lts), len(lts)
+        if env_faces is not None:
+            ef = np.ascontiguousarray(env_faces, np.float32)
+            j.env_faces, j.env_size = _f(ef), ef.shape[1]
+        j.env_intensity, j.env_clamp = env_intensity, env_clamp
+        j.cam[:] = [float(v) for v in cam]
+        j.width, j.height, j.max_depth = width, height, max_depth
+        j.use_bvh = 1 if self.bvh else 0
+        out = np.zeros((64, 9), np.float32)
+        n = lib().oracle_path_rays(self.h, C.byref(j), x, y, frame, _f(out), 64)
+        if n < 0:
+            raise RuntimeError("oracle_path_rays")
+        out = out[:min(n, 64)]
+        return out[:, 0].astype(np.int32), np.ascontiguousarray(out[:, 1:9])
+
     def render(self, cam: np.ndarray, width: int, height: int, materials: np.ndarray, lights: np.ndarray,
                frames: int = 1, frame_begin: int = 1, max_depth: int = 6, shard_rank: int = 0,
                shard_count: int = 1, threads: int = 0, env_faces: np.ndarray | None = None,
                env_intensity: float = 0.8, env_clamp: float = 5.0, accum: np.ndarray | None = None,
-               pathtracer_spf: int = 0, optix: bool = False, accum_w: np.ndarray | None = None):
+               pathtracer_spf: int = 0, optix: bool = False, accum_w: np.ndarray | None = None,
+               pixels: np.ndarray | None = None):
         """Returns (accum (H,W,3) float32 sums, rgb8 (H,W,3), counters dict).  pathtracer_spf > 0 selects
         the PathTracer integrator (the reference's default CPU path) with that many samples per frame;
         optix=True the OptiX device-program shading (accum_w: the per-pixel sample counts, (H,W) float32,
-        returned as the 4th counters key "accum_w")."""
+        returned as the 4th counters key "accum_w").  pixels (wavefront only): render just these pixel
+        indices y * width + x; the other accum / rgb entries stay as given."""
         mats = np.ascontiguousarray(materials, np.float32)
         lts = np.ascontiguousarray(lights, np.float32)
         acc = np.zeros((height, width, 3), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32)
@@ -200,6 +229,9 @@ class Prepared:
         j.shard_rank, j.shard_count = shard_rank, shard_count
         j.threads, j.use_bvh = threads, 1 if self.bvh else 0
         j.accum, j.rgb = _f(acc), _b(rgb)
+        if pixels is not None:
+            pix = np.ascontiguousarray(pixels, np.uint32)
+            j.pixels, j.num_pixels = _u(pix), len(pix)
         aw = None
         if optix:
             aw = np.zeros((height, width), np.float32) if accum_w is None else np.ascontiguousarray(accum_w, np.float32)
@@ -215,6 +247,25 @@ class Prepared:
         if aw is not None:
             out["accum_w"] = aw
         return acc, rgb, out
+
+
+class device_math:
+    """Context manager for the residue diagnosis: the oracle's wavefront path takes the GPU's values
+    for the cosine sample's sin/cos (sin_cos: (2^24, 2) float32 from sptr.Renderer.cosine_sincos_table,
+    or None) and the GPU's double squaring chains for pow(x, 5/8/64) (pow_chains)."""
+
+    def __init__(self, sin_cos: np.ndarray | None = None, pow_chains: bool = False):
+        self.tab = None if sin_cos is None else np.ascontiguousarray(sin_cos, np.float32)
+        assert self.tab is None or self.tab.shape == (1 << 24, 2)
+        self.pow_chains = pow_chains
+
+    def __enter__(self):
+        lib().oracle_set_device_math(None if self.tab is None else _f(self.tab), 1 if self.pow_chains else 0)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_device_math(None, 0)
+        return False
 
 
 def primary(cam: np.ndarray, width: int, height: int, acc: int):

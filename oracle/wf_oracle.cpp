@@ -89,6 +89,40 @@ static inline float rand01(uint32_t& s) {
   return float(s & 0x00FFFFFFu) / float(0x01000000u);
 }
 
+// Residue diagnosis (parity tests only; off by default): the GPU's values in place of glibc's for the
+// operations of the wavefront path whose last bit depends on the math library or on its form —
+//   sin_cos : (sinf, cosf) of the cosine sample's phi for each of the 2^24 values r1 = k / 2^24 takes
+//             (wf_math.h:51-72), as the device computes them (sptr_eval_math);
+//   pow_chains: pow(x, 5) / pow(x, 8) / pow(x, 64) as the device's squaring chains in double (one
+//             rounding to float; glibc's powf is correctly rounded, the chains differ from it only
+//             within ~6 2^-53 of a rounding midpoint).
+// With both set, a GPU/oracle pixel difference that remains is not a math-library difference.
+struct DevMath {
+  const float* sin_cos = nullptr;  // 2^24 pairs
+  bool pow_chains = false;
+};
+static DevMath g_devmath;
+static inline void cosine_sincos(float r1, float& sp, float& cp) {
+  const float phi = 2.0f * 3.14159265358979323846f * r1;
+  if (g_devmath.sin_cos) {
+    const uint32_t k = uint32_t(r1 * 16777216.0f);  // exact: r1 = k / 2^24
+    sp = g_devmath.sin_cos[2u * k];
+    cp = g_devmath.sin_cos[2u * k + 1u];
+    return;
+  }
+  sp = std::sin(phi);
+  cp = std::cos(phi);
+}
+static inline float pow_int(float x, float e) {  // e in {5, 8, 64}
+  if (!g_devmath.pow_chains) return std::pow(x, e);
+  const double s = double(x), s2 = s * s, s4 = s2 * s2;
+  if (e == 5.0f) return float(s4 * s);
+  const double s8 = s4 * s4;
+  if (e == 8.0f) return float(s8);
+  const double s16 = s8 * s8, s32 = s16 * s16;
+  return float(s32 * s32);
+}
+
 // ----------------------------------------------------------------------------- scene description
 struct Mat4 {  // column-major, m[col][row]
   float m[4][4];
@@ -309,7 +343,7 @@ static V3 eval_brdf(const Material& m, V3 N, V3 V, V3 L) {
   float f0d = (m.ior - 1.0f) / (m.ior + 1.0f);
   f0d *= f0d;
   const V3 F0 = mix(mk(f0d, f0d, f0d), m.albedo, m.metallic);
-  const float pw = std::pow(gclamp(1.0f - HdotV, 0.0f, 1.0f), 5.0f);
+  const float pw = pow_int(gclamp(1.0f - HdotV, 0.0f, 1.0f), 5.0f);
   const V3 F = F0 + (1.0f - F0) * pw;
   const V3 numer = (D * G) * F;
   const float denom = 4.0f * NdotV * NdotL + 0.0001f;
@@ -354,8 +388,8 @@ static V3 sky(V3 d) {  // EnvironmentManager::getSkyColor (EnvironmentManager.cp
   V3 c = mix(mk(0.7f, 0.8f, 0.9f), mk(0.2f, 0.4f, 0.8f), t);
   const V3 sd = normalize(mk(0.3f, 0.6f, -0.8f));
   const float sdot = gmax(dot(d, sd), 0.0f);
-  const float si = std::pow(sdot, 64.0f);
-  const float sg = std::pow(sdot, 8.0f) * 0.3f;
+  const float si = pow_int(sdot, 64.0f);
+  const float sg = pow_int(sdot, 8.0f) * 0.3f;
   c = c + mk(1.0f, 0.9f, 0.7f) * (si + sg);
   return c * 0.8f;
 }
@@ -803,6 +837,13 @@ static const Material& material_of(const Ctx& x, uint32_t geom) {  // MaterialMa
   return M[geom % M.size()];
 }
 
+// Residue diagnosis: when set (one thread), trace_path appends every ray it traces — 9 floats: kind
+// (0 closest hit, 1 shadow), origin, direction, tnear, tfar — so a test can replay them on the GPU.
+static thread_local std::vector<float>* g_raylog = nullptr;
+static inline void log_ray(float kind, V3 o, V3 d, float tn, float tf) {
+  if (g_raylog) g_raylog->insert(g_raylog->end(), {kind, o.x, o.y, o.z, d.x, d.y, d.z, tn, tf});
+}
+
 // WavefrontPathTracerCPU::traceRay (wf_pt_cpu.cpp:61-255) for the tile task's {spp=1}
 static V3 trace_path(const Ctx& x, V3 origin, V3 direction, uint32_t pixel_seed, uint32_t spp, Counters& cnt) {
   V3 color = mk(0, 0, 0);
@@ -817,6 +858,7 @@ static V3 trace_path(const Ctx& x, V3 origin, V3 direction, uint32_t pixel_seed,
       HitRec h;
       ++cnt.closest;
       ++cnt.bounces;
+      log_ray(0.0f, ro, rd, 0.0f, inf);
       if (!closest_hit(*x.P, ro, rd, 0.0f, inf, h, x.bvh)) {
         rad = rad + thr * env_color(x.env, safe_normalize(rd));
         break;
@@ -838,6 +880,7 @@ static V3 trace_path(const Ctx& x, V3 origin, V3 direction, uint32_t pixel_seed,
           const float eps = 1e-4f * gmax(1.0f, gmax(gmax(std::fabs(p.x), std::fabs(p.y)), std::fabs(p.z)));
           const V3 so = p + n * eps;
           ++cnt.shadow;
+          log_ray(1.0f, so, ldir, 1e-4f, ldist - 1e-4f);
           if (occluded(*x.P, so, ldir, 1e-4f, ldist - 1e-4f, x.bvh)) continue;
           const V3 f = eval_brdf(m, n, view, ldir);
           rad = rad + thr * (f * Li * cs);
@@ -885,9 +928,10 @@ static V3 trace_path(const Ctx& x, V3 origin, V3 direction, uint32_t pixel_seed,
       {  // diffuse: cosine sample (wf_math.h:51-72), then RR draw
         const float r1 = rand01(rng);
         const float r2 = rand01(rng);
-        const float phi = 2.0f * kPiF * r1;
+        float sp, cp;
+        cosine_sincos(r1, sp, cp);  // phi = 2 pi r1
         const float rr = std::sqrt(r2);
-        const float lx = rr * std::cos(phi), ly = rr * std::sin(phi);
+        const float lx = rr * cp, ly = rr * sp;
         const float lz = std::sqrt(std::max(0.0f, 1.0f - r2));
         const V3 nn = safe_normalize(n);
         const V3 t = (std::fabs(nn.z) < 0.999f) ? normalize(cross(nn, mk(0, 0, 1))) : normalize(cross(nn, mk(0, 1, 0)));
@@ -1240,9 +1284,18 @@ struct oracle_job {
   float* accum;   // width*height*3, read-modify-write
   uint8_t* rgb;   // width*height*3 (shard pixels only), may be null
   uint64_t counters[4];  // closest-hit queries, shadow queries, samples, bounces
+  const uint32_t* pixels;  // oracle_render only: if not null, render just these pixels (y * width + x)
+  uint32_t num_pixels;
 };
 
-int oracle_version(void) { return 4; }
+int oracle_version(void) { return 5; }
+
+// Residue diagnosis (see DevMath): sin_cos = 2^24 (sin, cos) pairs or null; pow_chains 0/1.  Global,
+// set before a render and reset after it.
+void oracle_set_device_math(const float* sin_cos, int pow_chains) {
+  g_devmath.sin_cos = sin_cos;
+  g_devmath.pow_chains = pow_chains != 0;
+}
 
 uint32_t oracle_wang_hash(uint32_t a) { return wang_hash(a); }
 
@@ -1440,31 +1493,43 @@ int oracle_render(void* h, oracle_job* job) {
   const int G = job->shard_count > 0 ? job->shard_count : 1, R = job->shard_rank;
   std::atomic<int> next{0};
   std::atomic<uint64_t> c_closest{0}, c_shadow{0}, c_samples{0}, c_bounces{0};
+  auto pixel = [&](int xx, int y, Counters& cnt) {
+    const uint32_t ps = uint32_t(y * W + xx);
+    float* acc = job->accum + size_t(ps) * 3;
+    V3 a = mk(acc[0], acc[1], acc[2]);
+    for (uint32_t f = 0; f < job->num_frames; ++f) {
+      const uint32_t n = job->frame_begin + f;
+      uint32_t r = wang_hash(ps ^ n * 9781u);
+      const float jx = rand01(r), jy = rand01(r);
+      const V3 d = ray_dir(cam, (float(xx) + jx) / float(W), (float(y) + jy) / float(H));
+      const V3 c = trace_path(x, cam.pos, d, ps ^ n, 1, cnt);
+      a = a + c;
+      ++cnt.samples;
+    }
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z;
+    if (job->rgb) resolve_pixel(a, job->frame_begin + job->num_frames - 1, job->rgb + size_t(ps) * 3);
+  };
   auto worker = [&]() {
     Counters cnt;
-    for (;;) {
-      const int t = next.fetch_add(1);
-      if (t >= ntiles) break;
-      if (t % G != R) continue;
-      const int tx = t % ntx, ty = t / ntx;
-      const int x0 = tx * TS, y0 = ty * TS, x1 = std::min(x0 + TS, W), y1 = std::min(y0 + TS, H);
-      for (int y = y0; y < y1; ++y)
-        for (int xx = x0; xx < x1; ++xx) {
-          const uint32_t ps = uint32_t(y * W + xx);
-          float* acc = job->accum + size_t(ps) * 3;
-          V3 a = mk(acc[0], acc[1], acc[2]);
-          for (uint32_t f = 0; f < job->num_frames; ++f) {
-            const uint32_t n = job->frame_begin + f;
-            uint32_t r = wang_hash(ps ^ n * 9781u);
-            const float jx = rand01(r), jy = rand01(r);
-            const V3 d = ray_dir(cam, (float(xx) + jx) / float(W), (float(y) + jy) / float(H));
-            const V3 c = trace_path(x, cam.pos, d, ps ^ n, 1, cnt);
-            a = a + c;
-            ++cnt.samples;
-          }
-          acc[0] = a.x; acc[1] = a.y; acc[2] = a.z;
-          if (job->rgb) resolve_pixel(a, job->frame_begin + job->num_frames - 1, job->rgb + size_t(ps) * 3);
+    if (job->pixels) {  // a pixel list (residue diagnosis): 64 pixels per grab
+      for (;;) {
+        const uint32_t i0 = uint32_t(next.fetch_add(64));
+        if (i0 >= job->num_pixels) break;
+        for (uint32_t i = i0; i < std::min(i0 + 64u, job->num_pixels); ++i) {
+          const uint32_t ps = job->pixels[i];
+          if (ps < uint32_t(W) * uint32_t(H)) pixel(int(ps % uint32_t(W)), int(ps / uint32_t(W)), cnt);
         }
+      }
+    } else {
+      for (;;) {
+        const int t = next.fetch_add(1);
+        if (t >= ntiles) break;
+        if (t % G != R) continue;
+        const int tx = t % ntx, ty = t / ntx;
+        const int x0 = tx * TS, y0 = ty * TS, x1 = std::min(x0 + TS, W), y1 = std::min(y0 + TS, H);
+        for (int y = y0; y < y1; ++y)
+          for (int xx = x0; xx < x1; ++xx) pixel(xx, y, cnt);
+      }
     }
     c_closest += cnt.closest;
     c_shadow += cnt.shadow;
@@ -1482,6 +1547,48 @@ int oracle_render(void* h, oracle_job* job) {
   job->counters[2] = c_samples;
   job->counters[3] = c_bounces;
   return 0;
+}
+
+// Residue diagnosis: the rays of pixel (px, py)'s wavefront path at accumulation index `frame` (the job's
+// scene state, camera and frame size), in trace order, 9 floats each (see log_ray); returns the count
+// (at most cap are written).
+int oracle_path_rays(void* h, oracle_job* job, int px, int py, uint32_t frame, float* out, int cap) {
+  const Prepared& P = *static_cast<Prepared*>(h);
+  std::vector<Material> mats(job->num_materials);
+  for (uint32_t i = 0; i < job->num_materials; ++i) {
+    const float* m = job->materials + i * 12;
+    mats[i] = Material{mk(m[0], m[1], m[2]), m[3], m[4], mk(m[5], m[6], m[7]), m[8], int(m[9])};
+  }
+  std::vector<Light> lights(job->num_lights);
+  for (uint32_t i = 0; i < job->num_lights; ++i) {
+    const float* l = job->lights + i * 8;
+    lights[i] = Light{int(l[0]), mk(l[1], l[2], l[3]), mk(l[4], l[5], l[6]), l[7]};
+  }
+  if (mats.empty()) return -1;
+  Ctx x;
+  x.P = &P;
+  x.mats = &mats;
+  x.lights = &lights;
+  x.env.faces = job->env_faces;
+  x.env.size = job->env_size;
+  x.env.intensity = job->env_intensity;
+  x.env.max_clamp = job->env_clamp;
+  x.max_depth = job->max_depth;
+  x.bvh = job->use_bvh != 0;
+  const Camera cam = cam_from(job->cam);
+  const int W = job->width, H = job->height;
+  const uint32_t ps = uint32_t(py * W + px);
+  uint32_t r = wang_hash(ps ^ frame * 9781u);
+  const float jx = rand01(r), jy = rand01(r);
+  const V3 d = ray_dir(cam, (float(px) + jx) / float(W), (float(py) + jy) / float(H));
+  std::vector<float> log;
+  Counters cnt;
+  g_raylog = &log;
+  (void)trace_path(x, cam.pos, d, ps ^ frame, 1, cnt);
+  g_raylog = nullptr;
+  const int n = int(log.size() / 9);
+  for (int i = 0; i < std::min(n, cap) * 9; ++i) out[i] = log[size_t(i)];
+  return n;
 }
 
 // PathTracer-mode render (PathTracer::renderImage / renderTileTask / traceRay, PathTracer.cpp:280-389):

@@ -1244,6 +1244,18 @@ __device__ __forceinline__ bool pixel_culled(const FrameView& f, uint32_t l) {
 }
 
 // --------------------------------------------------------------------------------- shading math
+// The two library calls of the wavefront path whose last bit may differ from glibc's (the CPU
+// reference links glibc; this is ocml): the cosine sample's sin / cos of phi = 2 pi r1
+// (wf_math.h:51-72; r1 takes the 2^24 values k / 2^24) and the resolve's pow(c, 1/2.2)
+// (GLRenderer.cpp:416-430).  One definition each, shared by the kernels and by k_eval_math, which
+// tabulates them for the parity tests' residue classifier (tests/test_gpu_configs.py).
+__device__ __forceinline__ void cosine_sincos(float r1, float& s, float& c) {
+  const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
+  s = sinf(phi);
+  c = cosf(phi);
+}
+__device__ __forceinline__ float gamma_pow(float x) { return powf(x, 1.0f / 2.2f); }
+
 // Integer powers of x in [0,1] (the reference's pow(sun_dot, 64/8) and the Fresnel pow(.., 5)):
 // squaring chain in double, rounded once to float.  x^2 is exact in double; every later product
 // carries <= 2^-53 relative error, so the float result equals the correctly rounded pow except
@@ -2052,9 +2064,10 @@ __device__ __forceinline__ bool continue_path(const Surface& s, vec3 rd, uint32_
   }
   const float r1 = rand01(rng);
   const float r2 = rand01(rng);
-  const float phi = 2.0f * 3.14159265358979323846264338327950288f * r1;
+  float sp, cp;
+  cosine_sincos(r1, sp, cp);
   const float rr = sqrtf(r2);
-  const float lx = rr * cosf(phi), ly = rr * sinf(phi);
+  const float lx = rr * cp, ly = rr * sp;
   const float lz = sqrtf(fmax_g(0.0f, 1.0f - r2));
   const vec3 nn = renormalized_again(nrm);  // s.n: safe_normalize's output (or its negation)
   const vec3 tg = (fabsf(nn.z) < 0.999f) ? normalize_dir(cross(nn, v3(0.0f, 0.0f, 1.0f)))
@@ -2811,8 +2824,7 @@ __device__ __forceinline__ uint32_t pack_rgba(vec3 c) {
 // Wavefront tile task resolve (GLRenderer.cpp:411-431): mean -> ACES -> gamma -> clamp -> 8 bit
 __device__ __forceinline__ uint32_t resolve_rgba(vec3 acc, uint32_t n) {
   vec3 c = aces(acc / float(n));
-  const float g = 1.0f / 2.2f;
-  c = v3(powf(c.x, g), powf(c.y, g), powf(c.z, g));
+  c = v3(gamma_pow(c.x), gamma_pow(c.y), gamma_pow(c.z));
   return pack_rgba(clamp_g(c, 0.0f, 1.0f));
 }
 // PathTracer::renderTileTask resolve (PathTracer.cpp:364-384): the frames were tonemapped as they
@@ -3444,6 +3456,21 @@ __global__ void __launch_bounds__(kBlock) k_primary(FrameView f, float* dirs, ui
   }
 }
 
+// The device's values of the two library calls above (sptr_eval_math): fn 0, the cosine sample's
+// (sin, cos) for every r1 = k / 2^24 (out: 2^25 floats, pairs by k; x unused); fn 1, gamma_pow(x[i]).
+__global__ void __launch_bounds__(kBlock) k_eval_math(int fn, const float* x, uint32_t n, float* out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) {
+    if (fn == 0) {
+      float sp, cp;
+      cosine_sincos(float(i) / float(0x01000000u), sp, cp);
+      out[2u * i] = sp;
+      out[2u * i + 1u] = cp;
+    } else {
+      out[i] = gamma_pow(x[i]);
+    }
+  }
+}
+
 // --------------------------------------------------------------------------------- launchers
 static inline unsigned grid_for(uint64_t work) {
   const uint64_t blocks = (work + kBlock - 1) / kBlock;
@@ -3846,6 +3873,9 @@ void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t*
                      ref, t, ng, occ, stack_overflow);
 }
 
+void launch_eval_math(int fn, const float* x, uint32_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_eval_math, dim3(grid_for(n)), dim3(kBlock), 0, s, fn, x, n, out);
+}
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s) {
   hipLaunchKernelGGL(k_primary, dim3(grid_for((uint64_t)f.W * f.H)), dim3(kBlock), 0, s, f, dirs, rng);
 }

@@ -1582,4 +1582,86 @@ int sptr_primary_rays(sptr_ctx* x, const sptr_camera* cam, int32_t W, int32_t H,
   return SPTR_OK;
 }
 
+// scratch of the primitive tests: freed on every exit path
+struct DevScratch {
+  std::vector<void*> p;
+  ~DevScratch() {
+    for (void* q : p) (void)hipFree(q);
+  }
+  hipError_t alloc(void** q, size_t bytes) {
+    *q = nullptr;
+    const hipError_t e = hipMalloc(q, bytes ? bytes : 16);
+    if (e == hipSuccess) p.push_back(*q);
+    return e;
+  }
+};
+
+int sptr_sort_pairs_u64(sptr_ctx* x, const uint64_t* keys, const uint32_t* vals, uint32_t n, uint64_t* keys_out,
+                        uint32_t* vals_out) {
+  if (!x || (n && (!keys || !vals || !keys_out || !vals_out))) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  API_HIP(hipSetDevice(c.device));
+  DevScratch d;
+  void *ki = nullptr, *ko = nullptr, *vi = nullptr, *vo = nullptr, *tmp = nullptr;
+  size_t tb = 0;
+  API_HIP(radix_sort_pairs_u64(nullptr, tb, nullptr, nullptr, nullptr, nullptr, n, c.stream));
+  API_HIP(d.alloc(&ki, (size_t)n * 8));
+  API_HIP(d.alloc(&ko, (size_t)n * 8));
+  API_HIP(d.alloc(&vi, (size_t)n * 4));
+  API_HIP(d.alloc(&vo, (size_t)n * 4));
+  API_HIP(d.alloc(&tmp, tb));
+  if (n) {
+    API_HIP(hipMemcpy(ki, keys, (size_t)n * 8, hipMemcpyHostToDevice));
+    API_HIP(hipMemcpy(vi, vals, (size_t)n * 4, hipMemcpyHostToDevice));
+  }
+  API_HIP(radix_sort_pairs_u64(tmp, tb, static_cast<const uint64_t*>(ki), static_cast<uint64_t*>(ko),
+                               static_cast<const uint32_t*>(vi), static_cast<uint32_t*>(vo), n, c.stream));
+  API_HIP(hipStreamSynchronize(c.stream));
+  if (n) {
+    API_HIP(hipMemcpy(keys_out, ko, (size_t)n * 8, hipMemcpyDeviceToHost));
+    API_HIP(hipMemcpy(vals_out, vo, (size_t)n * 4, hipMemcpyDeviceToHost));
+  }
+  return SPTR_OK;
+}
+
+int sptr_eval_math(sptr_ctx* x, int fn, const float* in, uint32_t n, float* out) {
+  if (!x || !out || (fn != SPTR_MATH_COSINE_SINCOS && fn != SPTR_MATH_GAMMA) || (fn == SPTR_MATH_GAMMA && n && !in))
+    return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  API_HIP(hipSetDevice(c.device));
+  const uint32_t m = fn == SPTR_MATH_COSINE_SINCOS ? (1u << 24) : n;
+  const size_t out_n = fn == SPTR_MATH_COSINE_SINCOS ? 2u * (size_t)m : (size_t)m;
+  DevScratch d;
+  void *di = nullptr, *dout = nullptr;
+  API_HIP(d.alloc(&di, fn == SPTR_MATH_GAMMA ? (size_t)n * 4 : 16));
+  API_HIP(d.alloc(&dout, out_n * 4));
+  if (fn == SPTR_MATH_GAMMA && n) API_HIP(hipMemcpy(di, in, (size_t)n * 4, hipMemcpyHostToDevice));
+  if (m) launch_eval_math(fn, static_cast<const float*>(di), m, static_cast<float*>(dout), c.stream);
+  API_HIP(hipGetLastError());
+  API_HIP(hipStreamSynchronize(c.stream));
+  if (out_n) API_HIP(hipMemcpy(out, dout, out_n * 4, hipMemcpyDeviceToHost));
+  return SPTR_OK;
+}
+
+int sptr_scan_u32(sptr_ctx* x, const uint32_t* in, uint32_t n, uint32_t* out) {
+  if (!x || (n && (!in || !out))) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  API_HIP(hipSetDevice(c.device));
+  DevScratch d;
+  void *di = nullptr, *dout = nullptr, *tmp = nullptr;
+  size_t tb = 0;
+  API_HIP(scan_u32(nullptr, tb, nullptr, nullptr, n, c.stream));
+  API_HIP(d.alloc(&di, (size_t)n * 4));
+  API_HIP(d.alloc(&dout, (size_t)n * 4));
+  API_HIP(d.alloc(&tmp, tb));
+  if (n) API_HIP(hipMemcpy(di, in, (size_t)n * 4, hipMemcpyHostToDevice));
+  API_HIP(scan_u32(tmp, tb, static_cast<const uint32_t*>(di), static_cast<uint32_t*>(dout), n, c.stream));
+  API_HIP(hipStreamSynchronize(c.stream));
+  if (n) API_HIP(hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return SPTR_OK;
+}
+
 }  // extern "C"

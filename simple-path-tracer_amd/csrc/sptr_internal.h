@@ -466,6 +466,7 @@ void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
                   bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, uint32_t* stack_overflow, hipStream_t s);
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s);
+void launch_eval_math(int fn, const float* x, uint32_t n, float* out, hipStream_t s);
 // one wave spinning for `ticks` of the device wall clock (sptr_overlap_probe)
 void launch_spin(uint64_t ticks, hipStream_t s);
 

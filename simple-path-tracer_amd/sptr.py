@@ -114,6 +114,7 @@ EXPORTS = [
     "sptr_read_rgb8",
     "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
+    "sptr_sort_pairs_u64", "sptr_scan_u32", "sptr_eval_math",
     "sptr_host_builtin_scene", "sptr_host_scene_view", "sptr_host_scene_free", "sptr_host_camera_lookat",
     "sptr_host_preset_materials", "sptr_host_default_lights", "sptr_host_equirect_to_faces",
     "sptr_host_pack_tiles", "sptr_host_unpack_tiles", "sptr_host_load_hdr", "sptr_host_free",
@@ -161,6 +162,9 @@ def lib() -> C.CDLL:
         "sptr_intersect": (C.c_int, [vp, fp, u32, up, up, fp, fp]),
         "sptr_occluded": (C.c_int, [vp, fp, u32, bp]),
         "sptr_primary_rays": (C.c_int, [vp, C.POINTER(Camera), i32, i32, u32, fp, up]),
+        "sptr_sort_pairs_u64": (C.c_int, [vp, C.POINTER(C.c_uint64), up, u32, C.POINTER(C.c_uint64), up]),
+        "sptr_scan_u32": (C.c_int, [vp, up, u32, up]),
+        "sptr_eval_math": (C.c_int, [vp, C.c_int, fp, u32, fp]),
         "sptr_host_builtin_scene": (C.c_int, [C.c_char_p, u32, u32, C.POINTER(vp)]),
         "sptr_host_scene_view": (C.c_int, [vp, C.POINTER(Scene)]),
         "sptr_host_scene_free": (None, [vp]),
@@ -508,6 +512,38 @@ class Renderer:
         self._check(self._L.sptr_primary_rays(self._h, C.byref(cam), width, height, acc, _f(dirs), _u(rng)),
                     "primary_rays")
         return dirs, rng
+
+    def sort_pairs_u64(self, keys: np.ndarray, vals: np.ndarray):
+        """The LBVH build's stable device radix sort (kernels_sort.hip): (keys, vals) sorted by key."""
+        k = np.ascontiguousarray(keys, np.uint64)
+        v = np.ascontiguousarray(vals, np.uint32)
+        assert k.shape == v.shape and k.ndim == 1
+        ko, vo = np.empty_like(k), np.empty_like(v)
+        u64p = C.POINTER(C.c_uint64)
+        self._check(self._L.sptr_sort_pairs_u64(self._h, k.ctypes.data_as(u64p), _u(v), len(k),
+                                                ko.ctypes.data_as(u64p), _u(vo)), "sort_pairs_u64")
+        return ko, vo
+
+    def cosine_sincos_table(self) -> np.ndarray:
+        """(sin, cos) of the cosine sample's phi for every r1 = k / 2^24, as the device computes them:
+        (2^24, 2) float32 (sptr_eval_math, fn 0)."""
+        out = np.empty((1 << 24, 2), np.float32)
+        self._check(self._L.sptr_eval_math(self._h, 0, None, 0, _f(out)), "eval_math")
+        return out
+
+    def gamma_pow(self, x: np.ndarray) -> np.ndarray:
+        """powf(x, 1/2.2) as the device's resolve computes it (sptr_eval_math, fn 1)."""
+        a = np.ascontiguousarray(x, np.float32).ravel()
+        out = np.empty_like(a)
+        self._check(self._L.sptr_eval_math(self._h, 1, _f(a), len(a), _f(out)), "eval_math")
+        return out.reshape(np.shape(x))
+
+    def scan_u32(self, counts: np.ndarray) -> np.ndarray:
+        """The LBVH build's device exclusive prefix sum of u32 counts (mod 2^32)."""
+        a = np.ascontiguousarray(counts, np.uint32)
+        out = np.empty_like(a)
+        self._check(self._L.sptr_scan_u32(self._h, _u(a), len(a), _u(out)), "scan_u32")
+        return out
 
 
 def setup_default(r: Renderer, scene: str = "default", p0: int = 0, p1: int = 0, env_faces=None) -> FlatScene:

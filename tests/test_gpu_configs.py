@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 import oracle
+import residue
 import sptr
 import workloads
 
@@ -311,19 +312,12 @@ def _render_as_bench(renderer, cam, W, H, S):
     return runs[-1]
 
 
-def _full_size_parity(name, renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, flat=None, fan_aware=False):
-    """§8(c) at the timed size: >= 99.9 % identical RGB8 pixels and relative L1 <= 1e-3 over every finite
-    pixel.  With fan_aware (the 10M-triangle mesh), the pixels that differ are classified (any camera
-    sample's first hit on a pole fan row or a t tie, on either side) and the fractions are logged."""
-    exact = (rgb == orgb).all(axis=2)
-    fin = np.isfinite(acc).all(axis=2) & np.isfinite(oacc).all(axis=2)
-    assert (~fin).sum() <= max(3, 1e-6 * W * H), "non-finite pixels"
-    rel_all = float(np.abs(acc[fin] - oacc[fin]).sum() / max(1e-12, np.abs(oacc[fin]).sum()))
-    rec = {"pixels": W * H, "spp": S, "exact_all": float(exact.mean()), "rel_l1_all": rel_all,
-           "differing_pixels": int((~exact).sum())}
-    if fan_aware and rec["differing_pixels"]:
-        ys, xs = np.nonzero(~exact)
-        cls = np.zeros(len(ys), bool)
+def _full_size_parity(name, renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, flat=None, fan_aware=False,
+                      env_faces=None):
+    """residue.full_size_parity with, for the 10M-triangle mesh (fan_aware), its BVH tie class: a camera
+    sample's first hit on a pole fan row or a t tie between primitives, on either side."""
+    def tie_fn(ys, xs):
+        tie = np.zeros(len(ys), bool)
         for a in range(1, S + 1):
             d, _ = oracle.primary(cam.as_array(), W, H, a)
             rays = np.zeros((len(ys), 8), np.float32)
@@ -332,14 +326,12 @@ def _full_size_parity(name, renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, fla
             rays[:, 7] = np.inf
             g, pr, t, _ = renderer.intersect(rays)
             og, opr, ot, _ = P.intersect(rays)
-            tie = (g != 0xFFFFFFFF) & (og != 0xFFFFFFFF) & (t.view(np.uint32) == ot.view(np.uint32)) & (pr != opr)
-            cls |= _c5_fan_rows(flat, g, pr) | _c5_fan_rows(flat, og, opr) | tie
-        rec["differing_pixels_in_class"] = int(cls.sum())
-        rec["differing_pixels_outside_class"] = int((~cls).sum())
-    _log_parity(name, rec)
-    assert rec["exact_all"] >= 0.999, rec
-    assert rel_all <= 1e-3, rec
-    return rec
+            tt = (g != 0xFFFFFFFF) & (og != 0xFFFFFFFF) & (t.view(np.uint32) == ot.view(np.uint32)) & (pr != opr)
+            tie |= _c5_fan_rows(flat, g, pr) | _c5_fan_rows(flat, og, opr) | tt
+        return tie
+
+    return residue.full_size_parity(name, renderer, P, cam, W, H, S, rgb, acc, orgb, oacc,
+                                    tie_fn=tie_fn if fan_aware else None, env_faces=env_faces, log=_log_parity)
 
 
 def test_c5_full_size_vs_oracle(renderer, c5_scene):
@@ -358,10 +350,9 @@ def test_c5_full_size_vs_oracle(renderer, c5_scene):
     oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
                                 frames=S, threads=THREADS)
     assert st.samples == ocnt["samples"]
-    rec = _full_size_parity("c5_full_size", renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, flat, fan_aware=True)
+    _full_size_parity("c5_full_size", renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, flat, fan_aware=True)
     assert abs(int(st.rays_closest) - ocnt["rays_closest"]) <= 1e-3 * ocnt["rays_closest"], (st.rays_closest, ocnt)
     assert abs(int(st.rays_shadow) - ocnt["rays_shadow"]) <= 1e-3 * ocnt["rays_shadow"], (st.rays_shadow, ocnt)
-    assert rec.get("differing_pixels_outside_class", 0) <= 1e-3 * W * H, rec
 
 
 def test_c3_full_size_vs_oracle(renderer):
@@ -378,7 +369,7 @@ def test_c3_full_size_vs_oracle(renderer):
     P = oracle.Prepared(_flat_dict(flat), bvh=True)
     oacc, orgb, ocnt = P.render(cam.as_array(), W, H, oracle.preset_materials(False), oracle.default_lights(),
                                 frames=S, env_faces=faces, threads=THREADS)
-    _full_size_parity("c3_full_size", renderer, P, cam, W, H, S, rgb, acc, orgb, oacc)
+    _full_size_parity("c3_full_size", renderer, P, cam, W, H, S, rgb, acc, orgb, oacc, env_faces=faces)
     assert abs(int(st.rays_closest) - ocnt["rays_closest"]) <= 1e-3 * ocnt["rays_closest"]
     assert abs(int(st.rays_shadow) - ocnt["rays_shadow"]) <= 1e-3 * ocnt["rays_shadow"]
     renderer.set_environment(None)

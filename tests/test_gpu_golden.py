@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
+import residue
 import sptr
 
 pytestmark = pytest.mark.gpu
@@ -93,6 +94,8 @@ def test_c2_full_size_vs_oracle(renderer, c2_full):
     oacc, orgb, ocnt = P.render(cam.as_array(), 1920, 1080, oracle.preset_materials(True), oracle.default_lights(),
                                 frames=64, threads=min(16, os.cpu_count() or 1))
     _image_close(rgb, orgb, acc, oacc)
+    residue.full_size_parity("c2_full_size", renderer, P, cam, 1920, 1080, 64, rgb, acc, orgb, oacc,
+                             materials=oracle.preset_materials(True))
     assert st.samples == ocnt["samples"] == 1920 * 1080 * 64
     assert abs(int(st.rays_closest) - ocnt["rays_closest"]) <= 1e-4 * ocnt["rays_closest"]
     assert abs(int(st.rays_shadow) - ocnt["rays_shadow"]) <= 1e-4 * ocnt["rays_shadow"]
