@@ -365,16 +365,35 @@ def cpu_baseline(wl, flat, cam):
 def interactive(steps):
     """The reference's own usage: 1 spp per render() call, progressive accumulation, RGB8 read back
     every frame, as GLRenderer::renderLoop drives a backend (src/GLRenderer.cpp:161-176).  Runs the C++
-    harness (backends::HipBackend through the C ABI) as a child process."""
+    harness (backends::HipBackend through the C ABI) as a child process: the default scene at 800x600
+    and 1080p, and the L2/HBM scenes C3 (chair + HDR environment) and C5 (10M triangles) at 1080p; the
+    1080p legs in launch mode 0 (graph replay where it pays, the default) and 1 (direct launches)."""
+    import tempfile
+
     cli = os.path.join(ROOT, "simple-path-tracer_amd", "sptr_cli")
     out = []
-    for w, h in ((800, 600), (1920, 1080)):
-        r = subprocess.run([cli, "--scene", "default", "--w", str(w), "--h", str(h), "--spp", str(steps),
-                            "--warmup", "10", "--json", "--out", "/dev/null"], capture_output=True, text=True,
-                           timeout=300)
-        if r.returncode != 0:
-            raise RuntimeError(f"sptr_cli failed: {r.stderr[-2000:]}")
-        out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    with tempfile.TemporaryDirectory() as d:
+        sky = os.path.join(d, "sky.hdr")
+        workloads.write_hdr(sky, workloads.synthetic_sky_equirect())
+        c3, c5 = workloads.WORKLOADS["c3"], workloads.WORKLOADS["c5"]
+        legs = [(["--scene", "default"], 800, 600, 0)]
+        for mode in (0, 1):
+            legs.append((["--scene", "default"], 1920, 1080, mode))
+        for mode in (0, 1):
+            legs.append((["--scene", c3.scene, "--env", sky], 1920, 1080, mode))
+            legs.append((["--scene", f"sphere_mesh:{c5.p0}:{c5.p1}"], 1920, 1080, mode))
+        for extra, w, h, mode in legs:
+            r = subprocess.run([cli, *extra, "--w", str(w), "--h", str(h), "--spp", str(steps), "--warmup", "10",
+                                "--launch-mode", str(mode), "--json", "--out", "/dev/null"], capture_output=True,
+                               text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"sptr_cli failed: {r.stderr[-2000:]}")
+            rec = json.loads(r.stdout.strip().splitlines()[-1])
+            if rec["scene"].startswith("gltf:"):
+                rec["scene"] = "c3 (gltf chair + synthetic HDR env)"
+            elif rec["scene"].startswith("sphere_mesh"):
+                rec["scene"] = "c5 (" + rec["scene"] + ")"
+            out.append(rec)
     return out
 
 

@@ -822,11 +822,15 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   const bool repeat = c.have_last_key && same_key(key, c.last_key);
   c.last_key = key;
   c.have_last_key = true;
-  // mode 0 captures a call whose direct launches forked nothing, or a small one (launch-bound): the
-  // runtime's graph executor does not run a graph's parallel branches concurrently, so a large call
-  // with side-stream launches replays slower than it launches directly (r04h: C5 8.70 vs 8.18 ms,
-  // C3 3.80 vs 3.75; C2, which forks nothing, 3.07 vs 3.10).  Mode 3 captures every repeated shape.
-  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && (!c.last_forked || samples <= kGraphForkedMaxSamples));
+  // mode 0 captures a call whose launches fork nothing to the side streams: the runtime's graph executor
+  // does not run a graph's parallel branches concurrently, so a call with side-stream launches replays
+  // slower than it launches directly, at every size measured (r04h: C5 8.70 vs 8.18 ms, C3 3.80 vs 3.75;
+  // r05i, 1-spp frames, C5 at 256x144 / 512x288 / 960x540 / 1920x1080: 1.87 / 2.21 / 2.52 / 3.11 vs
+  // 1.23 / 1.50 / 1.72 / 2.22 ms, C3 0.46 / 0.61 / 0.78 / 0.96 vs 0.44 / 0.57 / 0.73 / 0.92 ms; r05k, the
+  // default scene's 1-spp 1080p frame, which forks only k_sky: 0.47 vs 0.41 ms).  C2's 64-spp call forks
+  // nothing: 3.07 graph vs 3.10 ms direct.  Mode 3 captures every repeated shape.
+  (void)samples;
+  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && !c.last_forked);
   const bool bad = c.have_bad_key && same_key(key, c.bad_key);  // this shape failed to capture before
   auto direct = [&]() -> int {
     c.last_forked = false;  // (set by the launch sequence if it forks)

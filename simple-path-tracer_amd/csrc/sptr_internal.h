@@ -168,7 +168,6 @@ struct FrameView {
 };
 // FrameView::dyn words: {frame_begin, reset, total} of the call (k_frame_dyn).
 constexpr size_t kDynBytes = 2048;
-constexpr uint64_t kGraphForkedMaxSamples = 1ull << 22;  // run_call: graphs for forked calls up to this size
 
 // Bounce-0 modes (FrameView::pixel_major): path-major (thread per path slot, every miss writes
 // rad[p]); thread per pixel (k_trace_pm); wave per pixel (k_trace_wp).  The last two fold each

@@ -109,6 +109,10 @@ bool HipBackend::renderInternal(int w, int h, const Camera& camera) {
   fr.shard_count = 1;
   fr.integrator = settings_.integrator;
   fr.samples_per_frame = settings_.samples_per_frame;
+  if (sptr_set_launch_mode(ctx_, settings_.launch_mode) != SPTR_OK) {
+    err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);
+    return false;
+  }
   const int rc = sptr_render(ctx_, &fr, nullptr, &stats_);
   if (rc != SPTR_OK) {
     err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);

@@ -25,6 +25,9 @@ class HipBackend {
     // SPTR_INTEGRATOR_PATHTRACER (the default key's PathTracer semantics, src/GLRenderer.cpp:172-176)
     uint32_t integrator = SPTR_INTEGRATOR_WAVEFRONT;
     uint32_t samples_per_frame = 4;  // PathTracer::Settings::samples_per_pixel (src/main.cpp:107)
+    // sptr_set_launch_mode: 0 = replay a captured graph for repeated call shapes (default), 1 = direct
+    // launches, 2 = direct on one stream, 3 = a graph for every repeated shape
+    uint32_t launch_mode = 0;
   };
 
   explicit HipBackend(int device = 0);

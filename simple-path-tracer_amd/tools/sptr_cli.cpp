@@ -4,7 +4,7 @@
 // one render() per frame, progressive accumulation.
 //   sptr_cli [--scene default|default_emitter|test_triangle|sphere_mesh:STACKS:SLICES|gltf:PATH]
 //            [--w 800] [--h 600] [--spp 4] [--depth 6] [--env sky|FILE.hdr] [--out image.ppm]
-//            [--warmup N] [--json] [--integrator wavefront|pathtracer|optix] [--spf 4]
+//            [--warmup N] [--json] [--integrator wavefront|pathtracer|optix] [--spf 4] [--launch-mode 0-3]
 // --spp N renders N progressive frames of 1 spp each (GLRenderer's m_accumulated_samples loop);
 // --warmup N renders N untimed frames first (then restarts the accumulation by a camera change);
 // --json prints one line with per-frame wall-clock statistics (render + RGB8 read back, as the
@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
   int w = 800, h = 600, spp = 4, depth = 6, warmup = 0;
   bool json = false;
   std::string integrator = "wavefront";
-  int spf = 4;
+  int spf = 4, launch_mode = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto next = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
     else if (a == "--json") json = true;
     else if (a == "--integrator") integrator = next();
     else if (a == "--spf") spf = std::atoi(next());
+    else if (a == "--launch-mode") launch_mode = std::atoi(next());
     else {
       std::fprintf(stderr, "usage: %s [--scene S] [--w W] [--h H] [--spp N] [--depth D] [--env sky|F.hdr] [--out F] [--warmup N] [--json]\n",
                    argv[0]);
@@ -91,6 +92,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   st.samples_per_frame = uint32_t(spf);
+  st.launch_mode = uint32_t(launch_mode);
   be.setSettings(st);
   if (!be.build(sd)) {
     std::fprintf(stderr, "%s\n", be.lastError().c_str());
@@ -118,11 +120,11 @@ int main(int argc, char** argv) {
     std::vector<double> s = frame_ms;
     std::sort(s.begin(), s.end());
     auto pct = [&](double q) { return s.empty() ? 0.0 : s[std::min(s.size() - 1, size_t(q * double(s.size())))]; };
-    std::printf("{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"frames\": %d, \"spp_per_frame\": 1, "
+    std::printf("{\"scene\": \"%s\", \"launch_mode\": %d, \"width\": %d, \"height\": %d, \"frames\": %d, \"spp_per_frame\": 1, "
                 "\"depth\": %d, \"ms_per_frame_wall\": %.4f, \"ms_per_frame_p50\": %.4f, \"ms_per_frame_p99\": %.4f, "
                 "\"ms_per_frame_device\": %.4f, \"fps\": %.1f, \"mrays_per_s_wall\": %.1f, "
                 "\"path\": \"backends::HipBackend::render (sptr_render + sptr_read_rgb8 per frame)\"}\n",
-                scene_name.c_str(), w, h, spp, depth, wall / spp, pct(0.5), pct(0.99), ms / spp,
+                scene_name.c_str(), launch_mode, w, h, spp, depth, wall / spp, pct(0.5), pct(0.99), ms / spp,
                 wall > 0 ? 1e3 * spp / wall : 0.0, wall > 0 ? rays / (wall * 1e3) : 0.0);
   } else {
     std::printf("scene=%s %dx%d spp=%d depth=%d: %.2f ms device, %.2f ms wall, %.1f Mrays/s (device)\n",

@@ -404,17 +404,19 @@ def test_wave_fold_vs_oracle(renderer):
 
 @pytest.mark.parametrize("integrator", [0, 1, 2])
 def test_launch_graph_replay_equals_direct(renderer, integrator):
-    """Repeated call shapes are captured into a hipGraph and replayed (sptr_set_launch_mode 0): the
+    """Repeated call shapes are captured into a hipGraph and replayed (sptr_set_launch_mode 3): the
     accumulation and the stats must match direct launches call for call — including progressive
     continuation (the per-call frame index is a graph-node argument), a camera change (new shape:
-    direct launches again, then a second capture) and asynchronous calls.  Calls with stage timing run
+    direct launches again, then a second capture) and asynchronous calls.  The default mode 0 captures
+    only shapes whose launches fork nothing to the side streams (the wavefront call of this size forks
+    k_sky beside bounce 0; the path-per-thread integrators fork nothing).  Calls with stage timing run
     as direct launches in every mode (no capture)."""
     W, H = 96, 64
     sptr.setup_default(renderer, "default_emitter")
     cams = [sptr.camera_lookat(aspect=W / H), sptr.camera_lookat(pos=(0.5, 3.0, 8.0), aspect=W / H)]
     out = {}
     try:
-        for mode in (1, 0):
+        for mode in (1, 3):
             renderer.set_launch_mode(mode)
             g0 = renderer.graph_info()
             seq = []
@@ -429,10 +431,25 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
             seq.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow, None, 0, st.ms_total))
             out[mode] = seq
             g = renderer.graph_info()
-            if mode == 0:  # one capture per camera, the asynchronous calls replay the first camera's again
+            if mode == 3:  # one capture per camera, the asynchronous calls replay the first camera's again
                 assert g["valid"] == 1 and g["captures"] == g0["captures"] + 3, (g0, g)
             else:
                 assert g["captures"] == g0["captures"], (g0, g)
+        # mode 0 (the default) on a new shape (another frame width): captured unless it forks
+        W0 = 80
+        cam0 = sptr.camera_lookat(aspect=W0 / H)
+        ref = []
+        renderer.set_launch_mode(1)
+        for fb in (1, 3, 5):
+            renderer.render(cam0, W0, H, spp=2, frame_begin=fb, integrator=integrator)
+            ref.append(renderer.read_accum().copy())
+        renderer.set_launch_mode(0)
+        g0 = renderer.graph_info()
+        for i, fb in enumerate((1, 3, 5)):
+            renderer.render(cam0, W0, H, spp=2, frame_begin=fb, integrator=integrator)
+            assert np.array_equal(renderer.read_accum().view(np.uint32), ref[i].view(np.uint32))
+        forks = integrator == 0
+        assert renderer.graph_info()["captures"] == g0["captures"] + (0 if forks else 1)
         # stage timing: direct launches however often the shape repeats
         g0 = renderer.graph_info()
         for _ in range(3):
@@ -441,7 +458,7 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
         assert renderer.graph_info()["captures"] == g0["captures"]
     finally:
         renderer.set_launch_mode(0)
-    for a, b in zip(out[1], out[0]):
+    for a, b in zip(out[1], out[3]):
         assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
         assert (a[1], a[2]) == (b[1], b[2])
         assert b[5] > 0.0  # the call span's events were re-pointed and recorded on replay
@@ -675,7 +692,7 @@ def test_graph_replay_after_camera_switch(renderer, scene, p0, p1):
             "B": sptr.camera_lookat(pos=(4.0, 2.0, 6.0), target=(-1.0, 1.0, 0.0), aspect=W / H)}
     out = {}
     try:
-        for mode in (1, 0):
+        for mode in (1, 3):
             renderer.set_launch_mode(mode)
             out[mode] = []
             for name in "AABAA":
@@ -684,7 +701,7 @@ def test_graph_replay_after_camera_switch(renderer, scene, p0, p1):
     finally:
         renderer.set_launch_mode(0)
     assert not np.array_equal(out[1][0][0], out[1][2][0])  # the two cameras see different images
-    for a, b in zip(out[1], out[0]):
+    for a, b in zip(out[1], out[3]):
         assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
         assert a[1:] == b[1:]
 
