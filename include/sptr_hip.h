@@ -228,16 +228,18 @@ int sptr_set_leaf_size(sptr_ctx* ctx, uint32_t max_prims);
 int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
 /* Straggler hand-off (ABI 6) for scenes traversed from HBM (a wide BVH beyond an XCD's L2): once a
  * wave of a bounce trace has no rays left to start and at most `lanes` of its 64 lanes are still
- * tracing, those rays are handed to a path-per-thread kernel beside the launch chain, which traces
- * them again and finishes their paths, so the launch no longer lasts as long as its longest ray.
+ * tracing, those rays are handed to a path-per-thread kernel beside the launch chain, which resumes
+ * each walk from the state the trace saved (node, stack, closest hit so far) and finishes the path,
+ * so the launch no longer lasts as long as its longest ray.
  * 0 = off, 1..64 (default 12).  Results do not depend on it (each path makes the same operations in
  * the same order wherever it runs); sptr_stats::paths_handed_off counts the paths. */
 int sptr_set_stragglers(sptr_ctx* ctx, uint32_t lanes);
 /* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
  * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
  * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument —
- * except a call of more than 2^22 samples whose launches fork to the side streams (the graph executor
- * runs a graph's branches one after another: such calls launch directly);
+ * except a call whose launches fork to the side streams (the graph executor runs a graph's branches
+ * one after another, so such calls launch directly; a shape whose capture fails or is rejected also
+ * launches directly from then on);
  * 1: direct kernel launches for every call; 2: direct launches, all on the render stream (no launch
  * overlapped on the context's second stream); 3: as 0 for every repeated shape, whatever its size.
  * Calls with stage timing (SPTR_FRAME_TIMING*) launch directly in every mode.  Results are identical
@@ -247,7 +249,8 @@ int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
  * node count, dependency edges and the nodes on its longest path; captures = graphs captured so far;
  * capture_status = the hipError_t of the last capture attempt that fell back to direct launches (0:
  * none).  Every captured graph is checked to be acyclic before it is instantiated (a rejected capture
- * fails the call with SPTR_ERR_HIP).  Any pointer may be NULL. */
+ * falls back to direct launches for that shape, reported here and by sptr_capture_error).  Any
+ * pointer may be NULL. */
 int sptr_graph_info(const sptr_ctx* ctx, uint32_t* valid, uint32_t* nodes, uint32_t* edges, uint32_t* depth,
                     uint32_t* captures, int32_t* capture_status);
 /* The call that made the last capture attempt fall back to direct launches, with its error text ("" if none). */

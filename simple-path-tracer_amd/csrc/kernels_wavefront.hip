@@ -1881,8 +1881,9 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
                                                                           kDynSteps);
     // Straggler hand-off: the wave has no rays left to start and at most strag_lanes lanes are still
     // tracing (the long rays that would otherwise set the launch's length while the rest of the chip
-    // idles).  Their rays are written to the bounce's straggler records and k_strag, beside the chain,
-    // traces each again from the root and carries its path to the end; no hit record is written here.
+    // idles).  Their rays and walk states (node, stack, closest hit so far) are written to the bounce's
+    // straggler records; k_strag, beside the chain, resumes each walk where it stopped and carries its
+    // path to the end.  No hit record is written here.
     if (!kCount && w.strag_lanes != 0u && drained && (uint32_t)depth < kStragBounces) {
       const unsigned long long act = __ballot(have && !done);
       if (act != 0ull && (uint32_t)__popcll(act) <= w.strag_lanes && have && !done) {
@@ -2627,7 +2628,8 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
 
 // --------------------------------------------------------------------------------- k_strag
 // The paths whose bounce-`depth0` ray k_trace_dyn handed off (WaveView::strag), one thread per path,
-// refilled per bounce as in k_tail: the ray is traced again from the root, then the path is carried to
+// refilled per bounce as in k_tail: the handed-off walk resumes from the state k_trace_dyn saved (the same
+// walk form, node order, stack and closest hit so far — kStragRec), then the path is carried to
 // its end with k_tail's per-bounce steps — the operations and radiance-update order of k_trace + k_shade
 // + k_shadow — so a handed-off path adds exactly what the wavefront stages would have added.  The host
 // launches it after the trace and after the shadow launch of the previous bounce (which may still add to

@@ -1393,15 +1393,24 @@ int sptr_overlap_probe(sptr_ctx* x, double* ms) {
   API_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c.device));
   if (rate_khz <= 0) return fail(c, SPTR_ERR_HIP, "overlap probe: no wall clock rate");
   const uint64_t ticks = (uint64_t)rate_khz / 5u;  // 200 us per spin
-  hipEvent_t e0 = nullptr, e1 = nullptr, fk = nullptr, jn = nullptr;
-  API_HIP(hipEventCreate(&e0));
-  API_HIP(hipEventCreate(&e1));
-  API_HIP(hipEventCreateWithFlags(&fk, hipEventDisableTiming));
-  API_HIP(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+  // the events are destroyed on every exit path (Probe's destructor)
+  struct Probe {
+    hipEvent_t e0 = nullptr, e1 = nullptr, fk = nullptr, jn = nullptr;
+    ~Probe() {
+      for (hipEvent_t e : {e0, e1, fk, jn})
+        if (e) (void)hipEventDestroy(e);
+    }
+  } pe;
   hipError_t err = hipSuccess;
   auto ck = [&](hipError_t e) {
     if (e != hipSuccess && err == hipSuccess) err = e;
   };
+  ck(hipEventCreate(&pe.e0));
+  ck(hipEventCreate(&pe.e1));
+  ck(hipEventCreateWithFlags(&pe.fk, hipEventDisableTiming));
+  ck(hipEventCreateWithFlags(&pe.jn, hipEventDisableTiming));
+  if (err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("overlap probe: ") + hipGetErrorString(err));
+  hipEvent_t e0 = pe.e0, e1 = pe.e1, fk = pe.fk, jn = pe.jn;
   const hipStream_t s = c.stream;
   launch_spin(ticks / 8u, s);  // warm the kernel
   ck(hipStreamSynchronize(s));
@@ -1425,7 +1434,6 @@ int sptr_overlap_probe(sptr_ctx* x, double* ms) {
     ck(hipEventElapsedTime(&t, e0, e1));
     ms[i] = t;
   }
-  for (hipEvent_t e : {e0, e1, fk, jn}) (void)hipEventDestroy(e);
   if (err != hipSuccess) return fail(c, SPTR_ERR_HIP, std::string("overlap probe: ") + hipGetErrorString(err));
   return SPTR_OK;
 }

@@ -186,6 +186,7 @@ constexpr uint32_t kWorkWords = kWorkStrag + 32u * kStragBounces;
 // default lane threshold (a drained wave hands its rays off once this few lanes are still busy)
 constexpr uint32_t kStragCap = 1u << 17;
 constexpr uint32_t kStragRec = 4u + (uint32_t)kStack / 4u;
+static_assert(kStragRec * 4u - 16u >= (uint32_t)kStack, "a straggler record holds the whole traversal stack");
 constexpr uint32_t kStragLanesDefault = 12;  // C5, grid 256, bounce 0: r04n 0/8/16/32 lanes 8.03/7.76/7.95/8.48 ms; r04zb 4/8/12 lanes 7.96/7.83/7.73
 // bounces whose traces hand off (<= kStragBounces): a handed-off path must be finished before the
 // batch's k_accum, so the later a bounce, the less time its stragglers have beside the chain (r04n,
