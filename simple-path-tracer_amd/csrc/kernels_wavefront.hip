@@ -2203,6 +2203,11 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       shadow = false;
       w.tot[kTotOverflow] = 1ull;
     }
+    // shadow carry (WaveView::carry_depth, one light): the task's tag is written once the continuation
+    // is known — 0 (k_shadow_dyn skips it; k_tail traces it) for a path that continues to the tail
+    const bool carry = !kFuse && (uint32_t)depth == w.carry_depth;
+    bool lit0 = false;
+    vec3 c0 = v3(0.0f, 0.0f, 0.0f);
     if (shadow) {
       // direct light: shadow tasks carry the precomputed contribution, added if unoccluded
       float4* task = w.stask + (size_t)(sd.seg0 + js) * L * ts;
@@ -2215,8 +2220,13 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
           continue;
         }
         task[0] = f4(so, tfar);
-        task[1] = f4(contrib, __uint_as_float(p + 1u));
         if (ts > 2u) task[2] = f4(ldir, 0.0f);
+        if (carry) {
+          lit0 = true;
+          c0 = contrib;
+        } else {
+          task[1] = f4(contrib, __uint_as_float(p + 1u));
+        }
       }
     }
     if (active && sh.debug_mode != 1) cont = continue_path(sf, rd, (uint32_t)depth, thr, rng, no, nd) && !last;
@@ -2226,10 +2236,11 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
       cont = false;
       w.tot[kTotOverflow] = 1ull;
     }
+    if (lit0) w.stask[(size_t)(sd.seg0 + js) * ts + 1u] = f4(c0, __uint_as_float(cont ? 0u : p + 1u));
     if (cont) {
       rout.o[sd.seg0 + jn] = f4(no, __uint_as_float(rng));
       rout.d[sd.seg0 + jn] = f4(nd, __uint_as_float(p));
-      rout.thr[sd.seg0 + jn] = f4(thr, 0.0f);
+      rout.thr[sd.seg0 + jn] = f4(thr, __uint_as_float(lit0 ? sd.seg0 + js + 1u : 0u));
     }
     if (kFuse) {
       if (lit) {
@@ -2409,7 +2420,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
   for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
   if (lane_id() == 0u) atomicAdd(&s_rays, rays);
   __syncthreads();
-  if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
+  if (threadIdx.x == 0) atomicAdd(&w.bstat[blockIdx.x], (unsigned long long)s_rays);  // (k_tail may run beside: shadow carry)
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotShNodes);
@@ -2505,7 +2516,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
   for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
   if (lane_id() == 0u) atomicAdd(&s_rays, rays);
   __syncthreads();
-  if (threadIdx.x == 0) w.bstat[blockIdx.x] += s_rays;
+  if (threadIdx.x == 0) atomicAdd(&w.bstat[blockIdx.x], (unsigned long long)s_rays);  // (k_tail may run beside: shadow carry)
   report_stack(vc, w.tot);
   if (kCount) {
     flush_visits(vc, w.tot, kTotShNodes);
@@ -2550,14 +2561,17 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   bool have = false, loaded = false;  // loaded: rad[p] is read at the first update
   vec3 ro, rd, thr, radv;
   uint32_t rng = 0u, p = 0u, depth = 0u;
+  uint32_t cslot = 0u;  // the path's carried shadow task (slot + 1; WaveView::carry_depth), 0: none
+  const bool carried = w.carry_depth != kNoHit && (uint32_t)depth0 == w.carry_depth + 1u;
   for (;;) {
     const uint32_t k = block_take(&s_next, !have);
     if (!have && k < nb) {
       const uint32_t id = seg_slot(s_off, nseg_in, per_in, block_item(sd, k));
-      const float4 o4 = rin.o[id], d4 = rin.d[id];
+      const float4 o4 = rin.o[id], d4 = rin.d[id], t4 = rin.thr[id];
       ro = xyz(o4);
       rd = xyz(d4);
-      thr = xyz(rin.thr[id]);
+      thr = xyz(t4);
+      cslot = carried ? __float_as_uint(t4.w) : 0u;
       rng = __float_as_uint(o4.w);
       p = __float_as_uint(d4.w);
       radv = v3(0.0f, 0.0f, 0.0f);
@@ -2569,6 +2583,23 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
     if (!have) continue;
     bool fin = true;
     do {  // one bounce of this lane's path; fin = false when it continues
+      if (cslot) {  // the shadow ray of the path's previous bounce, handed over by k_shade: first, as k_shadow would
+        const float4* task = w.stask + (size_t)(cslot - 1u) * w.tstride;
+        const float4 a = task[0], c = task[1];
+        const vec3 sdir = (w.tstride > 2u && sh.lights[0].type != 0) ? xyz(task[2])
+                                                                    : v3(sh.lights[0].v[0], sh.lights[0].v[1], sh.lights[0].v[2]);
+        ++n_shadow;
+        float st = a.w;
+        uint32_t sref = kNoHit;
+        if (!traverse_w_top<kW4, true, false>(sc, sv, top, ntop, make_ray(xyz(a), sdir), 1e-4f, st, sref, vc, s_stack)) {
+          if (!loaded) {
+            radv = xyz(w.rad[p]);
+            loaded = true;
+          }
+          radv = radv + xyz(c);
+        }
+        cslot = 0u;
+      }
       ++n_closest;
       float tfar = __builtin_huge_valf();
       uint32_t ref = kNoHit;
@@ -2620,8 +2651,9 @@ __global__ void __launch_bounds__(kBlock, kLds ? SPTR_TAIL_WAVES_LDS : SPTR_TAIL
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    w.bstat_closest[blockIdx.x] += s_rays[0];
-    w.bstat[blockIdx.x] += s_rays[1];
+    // atomics: with the shadow carry k_shadow_dyn of the previous bounce runs beside (same tallies)
+    atomicAdd(&w.bstat_closest[blockIdx.x], (unsigned long long)s_rays[0]);
+    atomicAdd(&w.bstat[blockIdx.x], (unsigned long long)s_rays[1]);
   }
   report_stack(vc, w.tot);
 }

@@ -187,6 +187,7 @@ WaveView wave_view(Context& c) {
   w.strag = static_cast<float4*>(wb.strag.p);
   w.strag_cap = wb.strag.p ? kStragCap : 0u;
   w.strag_lanes = 0u;  // set per trace launch (enqueue_wavefront)
+  w.carry_depth = kNoHit;
   return w;
 }
 
@@ -578,6 +579,14 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
   const bool shadow_side = overlap && !fuse && shadow_overlaps(sv, w);
   const bool strag = c.strag_lanes != 0u && !count && w.strag != nullptr && strag_applies(sv);
   w.defer_miss = shadow_side ? 1u : 0u;
+  // shadow carry (WaveView::carry_depth): the last wavefront bounce before the tail hands its continuing
+  // paths' shadow rays to k_tail, so that the tail need not wait for that bounce's shadow launch (which
+  // then traces only the shadow rays of paths ending there, beside the tail, joined before k_accum).
+  // Not in the visit-count pass (its k_shadow tallies every query).  Only for scenes resident in an
+  // XCD's L2 (r05p/q: C3 3.70 -> 3.57 ms/step; C5, traversed from HBM, 7.38-7.44 -> 7.46-7.52: there the
+  // tail, path per thread at 4 waves/SIMD, traces the carried rays slower than the refilling
+  // k_shadow_dyn, 816 -> 1318 us, and the launch it shortens was 374 us).
+  w.carry_depth = (shadow_side && !count && T < D && w.L == 1u && !trace_queue_applies(sv)) ? (uint32_t)(T - 1) : kNoHit;
   StageTimer tside{c, tm.on, tm.trace_only, ss};
   tside.capturing = tm.capturing;
   while (done < f.spp) {
@@ -604,9 +613,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     SegTable rays_tab = w.segN, spare_tab = w.segH;
     for (int d = 0; d < D; ++d) {
       if (d >= T) {  // the remaining bounces, path per thread
-        // (shadow(d - 1) adds to rad[], which the tail reads; k_sky only to the culled pixels' accum,
-        // joined before k_accum, so the tail runs beside it: C3's k_sky outlasts the whole bounce chain)
-        join_shadow();
+        // (shadow(d - 1) adds to rad[], which the tail reads — unless the tail carries those shadow rays
+        // itself (w.carry_depth); k_sky only to the culled pixels' accum, joined before k_accum, so the
+        // tail runs beside it: C3's k_sky outlasts the whole bounce chain)
+        if (w.carry_depth == kNoHit) join_shadow();
         WaveView wt = w;
         wt.segN = rays_tab;
         tm.begin(7);

@@ -281,6 +281,12 @@ struct WaveView {
   // strag_lanes = 0: no hand-off
   float4* strag;
   uint32_t strag_cap, strag_lanes;
+  // shadow carry (r05; scenes whose shadow rays have launches of their own, one light, a path-per-thread
+  // tail): k_shade(carry_depth) hands the shadow task of every path that continues to the tail's
+  // kernel (the continuation's thr.w = task slot + 1, the task's tag 0 so k_shadow_dyn skips it); k_tail
+  // traces that shadow ray before the path's next bounce, so shadow(carry_depth) no longer has to end
+  // before the tail starts.  kNoHit: no carry.
+  uint32_t carry_depth;
 };
 
 struct DevBuf {
