@@ -609,6 +609,10 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
+#ifndef SPTR_SKY_LATE
+#define SPTR_SKY_LATE 0
+#endif
+    const bool sky_late = SPTR_SKY_LATE && fv.sky_fold && overlap && shadow_side && T < D && trace_queue_applies(sv);
     // fused bounces alternate the ray tables: the table holding the current rays, and the other
     SegTable rays_tab = w.segN, spare_tab = w.segH;
     for (int d = 0; d < D; ++d) {
@@ -619,6 +623,12 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         if (w.carry_depth == kNoHit) join_shadow();
         WaveView wt = w;
         wt.segN = rays_tab;
+        if (sky_late) {  // k_sky beside the tail, on the (joined) shadow stream, joined before k_accum
+          fork_to(ss);
+          launch_sky(sh, fv, ss);
+          check(hipEventRecord(ev.join, ss), "sky join record");
+          join = true;
+        }
         tm.begin(7);
         launch_tail(sv, sh, fv, wt, d, g_shade, s);
         tm.end();
@@ -634,7 +644,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         std::swap(rays_tab, spare_tab);
         continue;
       }
-      const bool sky = d == 0 && fv.sky_fold;  // the culled pixels' environment sums: accumulation, not k_trace
+      const bool sky = d == 0 && fv.sky_fold && !sky_late;  // the culled pixels' environment sums: accumulation, not k_trace
       const bool sky_side = sky && overlap;
       if (sky && !sky_side) {
         tm.begin(4);
@@ -1023,11 +1033,17 @@ int sptr_create(int device, sptr_ctx** out) {
   sptr_ctx* x = new sptr_ctx();
   Context& c = x->c;
   c.device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess ||
+#ifndef SPTR_MAIN_PRIO_HI
+#define SPTR_MAIN_PRIO_HI 0
+#endif
+  if (hipSetDevice(device) != hipSuccess ||
       // the side streams at the lowest priority: a priority of its own puts a stream on a hardware
       // queue of its own, so that its launches can run beside the main sequence's
       hipDeviceGetStreamPriorityRange(&c.prio_lo, &c.prio_hi) != hipSuccess ||
+      (SPTR_MAIN_PRIO_HI ? hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, c.prio_hi)
+                         : hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking)) != hipSuccess ||
+      (SPTR_MAIN_PRIO_HI ? hipStreamCreateWithPriority(&c.cap_stream, hipStreamNonBlocking, c.prio_hi)
+                         : hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking)) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.cap_side, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side2_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
@@ -1318,7 +1334,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       if (c.wb.cap < std::min<uint64_t>(wave_paths, (uint64_t)f->spp * c.P)) {  // would (re)allocate
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
-          const uint32_t hm = trace_queue_applies(scene_view(c)) ? 2u : 1u;
+          const uint32_t hm = hrec_mult(scene_view(c));
           const uint64_t held = c.wb.cap ? c.wb.cap * wave_path_bytes(c.wb.L, c.wb.ts, hm) : 0ull;
           const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
           // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
@@ -1342,7 +1358,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       }
       // hit-record segments hold twice the static shares when k_trace_dyn takes its rays from the per-XCD queues
       rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u,
-                       trace_queue_applies(scene_view(c)) ? 2u : 1u);
+                       hrec_mult(scene_view(c)));
       if (rc != SPTR_OK) return rc;
     }
     const int T = std::max(1, (int)(c.tail_depth ? c.tail_depth : auto_tail_depth((uint64_t)k * c.P, scene_view(c))));

@@ -447,6 +447,8 @@ void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
 // k_strag's blocks resident beside it a static share leaves late-starting blocks a tail; C5 8.68 ->
 // 8.49 ms at 8 lanes, grid 128); its hit-record segments then hold twice the static shares.
 bool trace_queue_applies(const SceneView& sv);
+uint32_t hrec_mult(const SceneView& sv);
+bool primary_queue_applies(const SceneView& sv);
 bool strag_applies(const SceneView& sv);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 // resolve: also tone-map the sums into tiles (+ image) in the same launch (the call's last batch)
