@@ -566,13 +566,16 @@ def main():
                  flags=flags | sptr.SPTR_FRAME_ASYNC, stream=stream, integrator=integ, samples_per_frame=4)
         ptr, nbytes = r.tiles_device()
         local_tiles = torch.as_tensor(_DevArray(ptr, nbytes), device=dev)
-        send[: local_tiles.numel()].copy_(local_tiles)
+        src = local_tiles
+        if local_tiles.numel() != send.numel():  # a rank with fewer tiles: padded to the common size
+            send[: local_tiles.numel()].copy_(local_tiles)
+            src = send
         if ev:
             ev[1].record()
         if distributed:
-            gather_tiles(send, gathered, world, rank)
+            gather_tiles(src, gathered, world, rank)
         else:
-            gathered[: send.numel()].copy_(send)
+            gathered[: src.numel()].copy_(src)
         if rank == 0:
             r.unpack_tiles(gathered.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
         if ev:
@@ -608,6 +611,13 @@ def main():
     stats = [r.collect_stats()]  # the K timed steps' counters and stage events, summed
     render_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     gather_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+
+    # one untimed step with events around every stage (the timed steps record them around the trace and
+    # shadow launches only: each record between two launches idles the GPU for several microseconds)
+    step(sptr.SPTR_FRAME_TIMING | sptr.SPTR_FRAME_RECULL)
+    st_full = r.collect_stats()
+    stage_full = {k: round(getattr(st_full, "ms_" + k), 3)
+                  for k in ("total", "cull", "trace0", "trace", "shade0", "shade", "shadow", "tail", "accum")}
 
     # untimed one-stream pass (launch mode 2) for scenes whose launches overlap on the side streams: the
     # trace and shadow launches' own durations, with nothing beside them (roofline_serial)
@@ -674,7 +684,7 @@ def main():
     if rank == 0:
         stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
                     for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum", "cull")
-                              if args.stage_timing else ("trace0", "trace", "shadow", "cull"))}
+                              if args.stage_timing else ("trace0", "trace", "shadow"))}
         knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
         if args.launch_mode:
             knobs["launch_mode"] = args.launch_mode
@@ -707,7 +717,9 @@ def main():
             "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
             "overlap_probe": probe,
             "stage_ms_per_step": stage_ms,
-            "cull_ms": round(sum(s.ms_cull for s in stats) / args.steps, 4),
+            # all stages of one untimed step, events around each (stage spans overlap on L2/HBM scenes)
+            "stage_ms_untimed_step": stage_full,
+            "cull_ms": stage_full["cull"],
             "cull_launches_per_step": sum(s.cull_launches for s in stats) / args.steps,
             "tail_rays_per_step": int(sum(s.rays_tail for s in stats) / args.steps),
             # paths the bounce traces handed to the straggler kernel (sptr_set_stragglers)

@@ -108,9 +108,9 @@ enum sptr_frame_flags {
   SPTR_FRAME_COUNT_VISITS = 4u, /* one instrumented trace pass: count BVH node / primitive fetches */
   SPTR_FRAME_ASYNC = 8u, /* enqueue only: return without waiting; stats are left zero and the call's
                             counters and stage times accumulate until sptr_collect_stats */
-  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace, shadow and cull launches only (ms_trace,
-                                   ms_trace0, trace_launches, ms_shadow, shadow_launches, ms_cull): the
-                                   other stages run back to back */
+  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace and shadow launches only (ms_trace,
+                                   ms_trace0, trace_launches, ms_shadow, shadow_launches): the other
+                                   stages run back to back, and ms_total / ms_cull stay 0 */
   SPTR_FRAME_NO_CULL = 32u, /* diagnostic: bounce 0 traverses every camera ray, without the pixel-frustum
                                cull (the image is the same either way) */
   SPTR_FRAME_RECULL = 64u /* recompute the bounce-0 pixel-frustum cull mask in this call even when the
@@ -163,7 +163,7 @@ typedef struct sptr_stats {
   uint64_t rays_shadow;  /* any-hit queries = rtcOccluded1 calls */
   uint64_t samples;      /* pixel samples completed */
   uint64_t waves;        /* wavefront batches launched */
-  double ms_total;       /* wall time of the call on the device stream */
+  double ms_total;       /* SPTR_FRAME_TIMING: wall time of the call on the device stream */
   double ms_raygen, ms_trace, ms_shade, ms_shadow, ms_accum; /* SPTR_FRAME_TIMING only; raygen is fused
                                                                 into the bounce-0 trace (ms_raygen = 0);
                                                                 ms_accum includes the culled pixels'
@@ -182,7 +182,7 @@ typedef struct sptr_stats {
   uint64_t node_visits_primary, tri_tests_primary, sphere_tests_primary; /* SPTR_FRAME_COUNT_VISITS: the
                                                                            bounce-0 part of node_visits,
                                                                            tri_tests, sphere_tests */
-  double ms_cull;              /* SPTR_FRAME_TIMING / _TIMING_TRACE: the pixel-cull launches (k_cull) */
+  double ms_cull;              /* SPTR_FRAME_TIMING: the pixel-cull launches (k_cull) */
   uint64_t cull_launches;      /* calls whose cull mask was (re)computed */
   uint64_t shadow_launches;    /* SPTR_FRAME_TIMING / _TIMING_TRACE: shadow-stage launches (ms_shadow) */
   /* Per bounce d (index 7: bounces >= 7): rays the wavefront trace kernels traversed (every call) and

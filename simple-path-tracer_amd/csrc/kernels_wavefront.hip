@@ -3683,7 +3683,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
   if (!L && W) {  // refilling lanes (scenes traversed from L2/HBM)
     const unsigned lbd = lb + (walk_reads_top(P ? kWalkPrimary : kWalkU) ? sv.num_top4 * (unsigned)sizeof(WideNode) : 0u);  // + top levels
     // per-XCD work queues for scenes larger than an XCD's L2 (as k_shadow_dyn)
-    const bool queue = trace_queue_applies(sv) || (P && primary_queue_applies(sv));
+    const bool queue = trace_queue_applies(sv);
     return dispatch(
         [&](auto fl) -> unsigned {
           return [&]<bool C, bool Pc, bool Cube, bool Q>(Flags<C, Pc, Cube, Q>) {
@@ -3812,13 +3812,9 @@ bool trace_queue_applies(const SceneView& sv) {
   return sv.lds_bytes == 0u && sv.width == (uint32_t)kWide && sv.scene_bytes > kL2BytesPerXcd;
 }
 bool strag_applies(const SceneView& sv) { return trace_queue_applies(sv); }
-#ifndef SPTR_Q_PRIMARY
-#define SPTR_Q_PRIMARY 0
-#endif
-bool primary_queue_applies(const SceneView& sv) {
-  return SPTR_Q_PRIMARY && sv.lds_bytes == 0u && sv.width == (uint32_t)kWide;
-}
-uint32_t hrec_mult(const SceneView& sv) { return (trace_queue_applies(sv) || primary_queue_applies(sv)) ? 2u : 1u; }
+// hit-record segments per static share: twice the share where k_trace_dyn takes its rays from the per-XCD
+// queues.  (r05t: the queues for C3's bounce-0 trace too, beside k_sky: 3.53-3.55 vs 3.55-3.57 ms, noise.)
+uint32_t hrec_mult(const SceneView& sv) { return trace_queue_applies(sv) ? 2u : 1u; }
 
 // a fixed grid: the number of handed-off paths is known only on the device (k_strag reads it).  Small,
 // so that it holds few of the wave slots the chain's resident grids expect (r04k: 1024 blocks, 16 waves

@@ -265,7 +265,7 @@ constexpr int kStages = 9;
 struct StageTimer {
   Context& c;
   bool on;                  // SPTR_FRAME_TIMING or SPTR_FRAME_TIMING_TRACE
-  bool trace_only;          // SPTR_FRAME_TIMING_TRACE alone: stages 1 and 5 only
+  bool trace_only;          // SPTR_FRAME_TIMING_TRACE alone: the trace (1, 5) and shadow (3) launches only
   hipStream_t s;
   hipError_t err = hipSuccess;
   std::string what;         // the call that set err
@@ -296,7 +296,9 @@ struct StageTimer {
     return i;
   }
   void begin(int stage) {
-    if (!on || capturing || (trace_only && stage != 1 && stage != 5 && stage != 3 && stage != 8)) return;
+    // (an event record between two launches idles the GPU for ~5-10 us: r05 8-way C2 shard, 6 records per
+    // step -> 2 without the cull and call spans)
+    if (!on || capturing || (trace_only && stage != 1 && stage != 5 && stage != 3)) return;
     open = c.marks.size();
     c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
@@ -306,7 +308,7 @@ struct StageTimer {
     open = SIZE_MAX;
   }
   void begin_call() {  // (a replayed graph's call span is recorded around its launch: run_call)
-    if (capturing) return;
+    if (capturing || (on && trace_only)) return;  // SPTR_FRAME_TIMING_TRACE: the trace spans only
     call = c.marks.size();
     c.marks.push_back(StageMark{0, next(), SIZE_MAX});
   }
@@ -609,10 +611,11 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     // segment-table chain: trace(d) -> shade(d) -> {shadow(d), trace(d+1)}; each launcher returns
     // its grid size = the number of segments its consumers scan
     uint32_t g_shade = 0;
-#ifndef SPTR_SKY_LATE
-#define SPTR_SKY_LATE 0
-#endif
-    const bool sky_late = SPTR_SKY_LATE && fv.sky_fold && overlap && shadow_side && T < D && trace_queue_applies(sv);
+    // k_sky beside the tail instead of beside the bounce-0 trace, for scenes beyond an XCD's L2: there the
+    // chain's traces are long and latency-bound, and the sky's VALU-bound grid beside bounce 0 took the
+    // wave slots of the trace on the critical path (r05t: C5 7.34-7.37 -> 7.08-7.13 ms/step).  C3's
+    // cubemap sky outlasts the whole chain (2.5 of 3.6 ms), so it keeps forking at bounce 0.
+    const bool sky_late = fv.sky_fold && overlap && shadow_side && T < D && trace_queue_applies(sv);
     // fused bounces alternate the ray tables: the table holding the current rays, and the other
     SegTable rays_tab = w.segN, spare_tab = w.segH;
     for (int d = 0; d < D; ++d) {
@@ -654,7 +657,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       // k_sky forks at the same point as the bounce-0 trace (it writes only the culled pixels' accum
       // words, which nothing reads before this batch's k_accum, the join point): its VALU-bound blocks
       // fill the CUs the latency-bound trace leaves idle, above all in the trace's tail.  Enqueued
-      // after the trace, so that the trace's grid is dispatched first.
+      // after the trace, so that the trace's grid is dispatched first.  (sky_late: beside the tail.)
       if (sky_side) {
         if (!cap) c.last_forked = true;
         check(hipEventRecord(ev.fork, s), "sky fork record");
@@ -1033,17 +1036,12 @@ int sptr_create(int device, sptr_ctx** out) {
   sptr_ctx* x = new sptr_ctx();
   Context& c = x->c;
   c.device = device;
-#ifndef SPTR_MAIN_PRIO_HI
-#define SPTR_MAIN_PRIO_HI 0
-#endif
-  if (hipSetDevice(device) != hipSuccess ||
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess ||
       // the side streams at the lowest priority: a priority of its own puts a stream on a hardware
-      // queue of its own, so that its launches can run beside the main sequence's
+      // queue of its own, so that its launches can run beside the main sequence's.  (r05t: the main
+      // streams at the highest priority instead of the default changed nothing, C3 and C5.)
       hipDeviceGetStreamPriorityRange(&c.prio_lo, &c.prio_hi) != hipSuccess ||
-      (SPTR_MAIN_PRIO_HI ? hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, c.prio_hi)
-                         : hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking)) != hipSuccess ||
-      (SPTR_MAIN_PRIO_HI ? hipStreamCreateWithPriority(&c.cap_stream, hipStreamNonBlocking, c.prio_hi)
-                         : hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking)) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.cap_side, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||
       hipStreamCreateWithPriority(&c.side2_stream, hipStreamNonBlocking, c.prio_lo) != hipSuccess ||

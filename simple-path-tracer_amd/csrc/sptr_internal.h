@@ -331,8 +331,9 @@ struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t cap_stream = nullptr;  // launch-graph capture
-  // side streams for launches that overlap the main sequence: the shadow launches (side) and k_sky
-  // (side2), for direct launches and inside a capture (cap_*).  Star-shaped fork/join only: a side
+  // side streams for launches that overlap the main sequence: the shadow launches (side) and k_sky /
+  // k_strag (side2; k_sky beside the tail of scenes beyond an XCD's L2 runs on side after the last
+  // shadow join), for direct launches and inside a capture (cap_*).  Star-shaped fork/join only: a side
   // stream waits on events of the call's main stream and the main stream on the side streams', never
   // one side stream on another (enqueue_wavefront, DESIGN.md §3 "Launch graphs").
   hipStream_t side_stream = nullptr, cap_side = nullptr, side2_stream = nullptr, cap_side2 = nullptr;
@@ -343,8 +344,8 @@ struct Context {
     hipEvent_t fork = nullptr, join = nullptr, sky = nullptr;
   } dev[2];
   int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
-  // 0: replay a captured graph for repeated call shapes (large calls with side-stream launches
-  // excepted, run_call); 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
+  // 0: replay a captured graph for repeated call shapes that fork no side-stream launch (run_call);
+  // 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
   uint32_t launch_mode = 0;
   bool last_forked = false;          // the last direct launch sequence forked launches to a side stream
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
@@ -448,7 +449,6 @@ void launch_strag(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
 // 8.49 ms at 8 lanes, grid 128); its hit-record segments then hold twice the static shares.
 bool trace_queue_applies(const SceneView& sv);
 uint32_t hrec_mult(const SceneView& sv);
-bool primary_queue_applies(const SceneView& sv);
 bool strag_applies(const SceneView& sv);
 uint32_t bounce0_pixel_major(const SceneView& sv, const FrameView& f);
 // resolve: also tone-map the sums into tiles (+ image) in the same launch (the call's last batch)

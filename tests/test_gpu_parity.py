@@ -454,7 +454,11 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
         g0 = renderer.graph_info()
         for _ in range(3):
             st = renderer.render(cams[0], W, H, spp=2, integrator=integrator, flags=sptr.SPTR_FRAME_TIMING_TRACE)
-            assert st.ms_total > 0.0
+            if integrator == 0:  # the trace launches' spans only: no call span, no cull span
+                assert st.ms_total == 0.0 and st.ms_cull == 0.0
+                assert st.trace_launches > 0 and st.ms_trace > 0.0
+            else:  # path per thread: no trace stage; the call span
+                assert st.ms_total > 0.0
         assert renderer.graph_info()["captures"] == g0["captures"]
     finally:
         renderer.set_launch_mode(0)
