@@ -2810,8 +2810,24 @@ __device__ __forceinline__ bool sky_pixel(const FrameView& f, uint32_t l, int& x
 }
 // (r04 A/B: lane groups of 8 per culled pixel fed by per-XCD queues over a list of the culled pixels
 // cost C3 0.6 ms: the fold's shuffles and the queue grabs outweigh the idle lanes of mixed waves.)
-template <bool kCube>
+// k_sky's occupancy beside the launch chain (kCapped): it claims registers up to v<SPTR_SKY_VGPR> (128
+// of 512 per lane: at most 4 of its waves per SIMD), so that the latency-bound launches beside it keep
+// wave slots.  Its 43 registers admit 8 waves/SIMD, and a grid that wide took every slot from C3's
+// bounce chain, which then ran after the sky rather than beside it.  r05za: C3 3.54-3.55 -> 3.31-3.33
+// ms/step (5 waves 3.48, 3 waves 3.50, 6 waves 3.50-3.57); C5, whose sky runs beside the tail, 7.20-7.28
+// either way.  (r05zc/zd: a capped launch beside the chain plus a full-occupancy one after it, sharing
+// per-XCD pixel queues, 3.38-3.39: a 64-pixel chunk is ~0.3 ms of one wave's work, so the two launches'
+// last chunks end late.)  Uncapped when nothing runs beside it.
+#ifndef SPTR_SKY_VGPR
+#define SPTR_SKY_VGPR 127
+#endif
+#define SPTR_STR2(x) #x
+#define SPTR_STR(x) SPTR_STR2(x)
+template <bool kCube, bool kCapped>
 __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
+#if SPTR_SKY_VGPR
+  if constexpr (kCapped) asm volatile("; k_sky occupancy cap" ::: "v" SPTR_STR(SPTR_SKY_VGPR));
+#endif
   const FrameView f = frame_dyn(fin);
   const ImageDiv idiv = image_div(f);
   for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < f.P; l += grid_threads()) {
@@ -3874,7 +3890,7 @@ __global__ void k_spin(uint64_t ticks) {
 }
 void launch_spin(uint64_t ticks, hipStream_t s) { hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks); }
 
-void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
+void launch_sky(const ShadeView& sh, const FrameView& f, bool capped, hipStream_t s) {
 #ifdef SPTR_EXPERIMENT_KNOBS
   // SPTR_SKY_BLOCKS (A/B): a smaller grid-stride grid, leaving wave slots to the launches overlapped with it
   static const unsigned cap = getenv("SPTR_SKY_BLOCKS") ? (unsigned)atoi(getenv("SPTR_SKY_BLOCKS")) : 16384u;
@@ -3882,8 +3898,12 @@ void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s) {
   constexpr unsigned cap = 16384u;
 #endif
   const unsigned g = std::max(1u, std::min<unsigned>((f.P + kBlock - 1u) / kBlock, cap ? cap : 16384u));
-  if (sh.env.env != nullptr) hipLaunchKernelGGL((k_sky<true>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
-  else hipLaunchKernelGGL((k_sky<false>), dim3(g), dim3(kBlock), 0, s, sh.env, f);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(kBlock), 0, s, sh.env, f); };
+  if (sh.env.env != nullptr) {
+    if (capped) go(k_sky<true, true>); else go(k_sky<true, false>);
+  } else {
+    if (capped) go(k_sky<false, true>); else go(k_sky<false, false>);
+  }
 }
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,

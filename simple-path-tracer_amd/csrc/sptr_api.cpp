@@ -628,7 +628,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         wt.segN = rays_tab;
         if (sky_late) {  // k_sky beside the tail, on the (joined) shadow stream, joined before k_accum
           fork_to(ss);
-          launch_sky(sh, fv, ss);
+          launch_sky(sh, fv, true, ss);
           check(hipEventRecord(ev.join, ss), "sky join record");
           join = true;
         }
@@ -651,7 +651,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       const bool sky_side = sky && overlap;
       if (sky && !sky_side) {
         tm.begin(4);
-        launch_sky(sh, fv, s);
+        launch_sky(sh, fv, false, s);
         tm.end();
       }
       // k_sky forks at the same point as the bounce-0 trace (it writes only the culled pixels' accum
@@ -670,7 +670,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
       tm.end();
       if (sky_side) {
         check(hipStreamWaitEvent(ks, ev.fork, 0), "sky fork wait");
-        launch_sky(sh, fv, ks);
+        launch_sky(sh, fv, true, ks);
         check(hipEventRecord(ev.sky, ks), "sky join record");
         join_sky = true;
       }

@@ -457,7 +457,8 @@ void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uin
 // BVH2 levels the bounce-0 pixel cull tests for a call of spp samples per pixel
 uint32_t cull_depth_for(uint32_t spp);
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s);
-void launch_sky(const ShadeView& sh, const FrameView& f, hipStream_t s);
+// capped: at most 4 waves per SIMD (beside the launch chain); else full occupancy
+void launch_sky(const ShadeView& sh, const FrameView& f, bool capped, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.
