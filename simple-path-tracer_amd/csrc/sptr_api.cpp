@@ -839,6 +839,7 @@ void drop_graph(Context& c) {
 // timing (SPTR_FRAME_TIMING*) always run as direct launches: a stage span inside a graph would need
 // external event-record nodes, which torch's HIP 7.0 runtime (the one bench.py and any process that
 // imports torch first binds libsptr_hip to) refuses inside a capture (hipErrorInvalidValue, r04g).
+constexpr uint64_t kGraphMinSamples = 1ull << 24;  // launch mode 0 captures calls of at least this many samples
 template <class Enqueue>
 int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t reset, uint32_t total, uint64_t samples, uint32_t* clear,
              bool timing, bool trace_only, hipStream_t s, Enqueue&& enqueue, uint32_t& waves) {
@@ -852,8 +853,12 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   // 1.23 / 1.50 / 1.72 / 2.22 ms, C3 0.46 / 0.61 / 0.78 / 0.96 vs 0.44 / 0.57 / 0.73 / 0.92 ms; r05k, the
   // default scene's 1-spp 1080p frame, which forks only k_sky: 0.47 vs 0.41 ms).  C2's 64-spp call forks
   // nothing: 3.07 graph vs 3.10 ms direct.  Mode 3 captures every repeated shape.
-  (void)samples;
-  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && !c.last_forked);
+  // Nor does mode 0 capture small calls: the default scene's 1-spp frames (r05zh, sptr_cli, 400 frames,
+  // two repetitions; mean wall / device ms, graph vs direct) 640x360 0.42/0.18 and 0.31/0.18 vs 0.38/0.19
+  // and 0.30/0.20; 800x600 0.33/0.21 vs 0.31/0.22; 1280x720 0.37-0.38/0.22 vs 0.35/0.24; 1920x1080 (whose
+  // pixel-major bounce 0 forks nothing) 0.46/0.25 vs 0.41-0.42/0.23 — the replays' device time is at best
+  // 10 us shorter and their wall time has spikes.  Calls from kGraphMinSamples on (C2: 2.98 vs 3.02 ms).
+  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && !c.last_forked && samples >= kGraphMinSamples);
   const bool bad = c.have_bad_key && same_key(key, c.bad_key);  // this shape failed to capture before
   auto direct = [&]() -> int {
     c.last_forked = false;  // (set by the launch sequence if it forks)

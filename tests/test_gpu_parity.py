@@ -408,9 +408,8 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
     accumulation and the stats must match direct launches call for call — including progressive
     continuation (the per-call frame index is a graph-node argument), a camera change (new shape:
     direct launches again, then a second capture) and asynchronous calls.  The default mode 0 captures
-    only shapes whose launches fork nothing to the side streams (the wavefront call of this size forks
-    k_sky beside bounce 0; the path-per-thread integrators fork nothing).  Calls with stage timing run
-    as direct launches in every mode (no capture)."""
+    only shapes of at least 2^24 samples whose launches fork nothing to the side streams (small calls,
+    forking or not, run direct; 1024x256x64 calls of the LDS scene fork nothing and are captured).  Calls with stage timing run as direct launches in every mode (no capture)."""
     W, H = 96, 64
     sptr.setup_default(renderer, "default_emitter")
     cams = [sptr.camera_lookat(aspect=W / H), sptr.camera_lookat(pos=(0.5, 3.0, 8.0), aspect=W / H)]
@@ -435,21 +434,24 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
                 assert g["valid"] == 1 and g["captures"] == g0["captures"] + 3, (g0, g)
             else:
                 assert g["captures"] == g0["captures"], (g0, g)
-        # mode 0 (the default) on a new shape (another frame width): captured unless it forks
-        W0 = 80
-        cam0 = sptr.camera_lookat(aspect=W0 / H)
-        ref = []
-        renderer.set_launch_mode(1)
-        for fb in (1, 3, 5):
-            renderer.render(cam0, W0, H, spp=2, frame_begin=fb, integrator=integrator)
-            ref.append(renderer.read_accum().copy())
-        renderer.set_launch_mode(0)
-        g0 = renderer.graph_info()
-        for i, fb in enumerate((1, 3, 5)):
-            renderer.render(cam0, W0, H, spp=2, frame_begin=fb, integrator=integrator)
-            assert np.array_equal(renderer.read_accum().view(np.uint32), ref[i].view(np.uint32))
-        forks = integrator == 0
-        assert renderer.graph_info()["captures"] == g0["captures"] + (0 if forks else 1)
+        # mode 0 (the default) on new shapes (other frame sizes): a small call runs direct; a large one
+        # that forks nothing is captured on its second call
+        for W0, H0, spp0, captured in ((80, H, 2, False), (1024, 256, 64, True)):
+            cam0 = sptr.camera_lookat(aspect=W0 / H0)
+            ref = []
+            renderer.set_launch_mode(1)
+            for fb in (1, 1 + spp0, 1 + 2 * spp0):
+                renderer.render(cam0, W0, H0, spp=spp0, frame_begin=fb, integrator=integrator)
+                ref.append(renderer.read_accum().copy())
+            renderer.set_launch_mode(0)
+            g0 = renderer.graph_info()
+            for i, fb in enumerate((1, 1 + spp0, 1 + 2 * spp0)):
+                renderer.render(cam0, W0, H0, spp=spp0, frame_begin=fb, integrator=integrator)
+                assert np.array_equal(renderer.read_accum().view(np.uint32), ref[i].view(np.uint32))
+            g = renderer.graph_info()
+            assert g["captures"] == g0["captures"] + (1 if captured else 0), (W0, g0, g)
+            if captured:
+                assert g["valid"] == 1
         # stage timing: direct launches however often the shape repeats
         g0 = renderer.graph_info()
         for _ in range(3):
@@ -507,17 +509,18 @@ def test_pixel_cull_invisible(renderer, scene, p0, p1, spp, W, H):
 def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
     """Scenes traversed from L2/HBM run k_shadow_dyn(d) on a second stream beside k_trace_dyn(d + 1)
     (bounce-trace misses deferred to k_shade) and k_sky beside the bounce-0 trace, in captured graphs
-    (launch mode 0) and direct launches (1); mode 2 keeps every launch on one stream.  The images and
-    ray counts must be equal bit for bit, and repeated renders too."""
+    (launch mode 3) and direct launches (modes 1 and 0, which runs forking calls directly); mode 2 keeps
+    every launch on one stream.  The images and ray counts must be equal bit for bit, and repeated
+    renders too."""
     W, H = 160, 96
     sptr.setup_default(renderer, scene, p0, p1)
     cam = sptr.camera_lookat(aspect=W / H)
     out = {}
     try:
-        for mode in (2, 1, 0):
+        for mode in (2, 1, 0, 3):
             renderer.set_launch_mode(mode)
             runs = []
-            for _ in range(3):  # mode 0: direct, then captured and replayed where a call is captured
+            for _ in range(3):  # mode 3: direct, then captured and replayed
                 st = renderer.render(cam, W, H, spp=spp, frame_begin=1)
                 runs.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow))
             out[mode] = runs
@@ -525,17 +528,18 @@ def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
         renderer.set_launch_mode(0)
     ref = out[2][0]
     assert ref[2] > 0  # shadow rays traced
-    for mode in (2, 1, 0):
+    for mode in (2, 1, 0, 3):
         for a in out[mode]:
             assert np.array_equal(a[0].view(np.uint32), ref[0].view(np.uint32)), mode
             assert a[1:] == ref[1:], mode
 
 
-@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("mode", [1, 3])
 def test_many_calls_without_collect(renderer, mode):
     """1500 asynchronous calls of an L2-scene frame with no collection in between, each forking k_sky
-    and the shadow launches to the side streams and joining them back: direct launches (mode 1), and
-    one captured graph replayed (mode 0).  No state may accumulate in the runtime (r03 saw a host stack
+    and the shadow launches to the side streams and joining them back: direct launches (mode 1, as the
+    default mode 0 runs a forking call), and one captured graph replayed (mode 3).  No state may
+    accumulate in the runtime (r03 saw a host stack
     overflow inside libamdhip64 in this suite — the recursion of hipStreamEndCapture over a cyclic
     capture-stream list, DESIGN.md §6 "Launch graphs"), and every call must give the same image."""
     W, H = 96, 64
@@ -543,15 +547,18 @@ def test_many_calls_without_collect(renderer, mode):
     cam = sptr.camera_lookat(aspect=W / H)
     try:
         renderer.set_launch_mode(mode)
+        g0 = renderer.graph_info()
         renderer.render(cam, W, H, spp=4, frame_begin=1)
         ref = renderer.read_accum().copy()
         for _ in range(1500):
             renderer.render(cam, W, H, spp=4, frame_begin=1, flags=sptr.SPTR_FRAME_ASYNC)
         renderer.collect_stats()
         assert np.array_equal(ref.view(np.uint32), renderer.read_accum().view(np.uint32))
-        if mode == 0:
-            g = renderer.graph_info()
-            assert g["valid"] == 1, g
+        g = renderer.graph_info()
+        if mode == 3:
+            assert g["valid"] == 1 and g["captures"] == g0["captures"] + 1, (g0, g)
+        else:
+            assert g["captures"] == g0["captures"], (g0, g)
     finally:
         renderer.set_launch_mode(0)
 
@@ -641,9 +648,9 @@ def test_large_forked_call_launches_direct(renderer):
 def test_multibatch_overlapped_graph_replay(renderer, scene, p0, p1, spp):
     """A call of several sample batches (set_wave_paths: 8 samples per batch -> 3 batches) with the
     overlapped side-stream launches (k_sky beside each bounce-0 trace, k_shadow_dyn(d) beside the next
-    bounce's trace, on the L2/HBM scene) captured into one graph (launch mode 0, call 2) and replayed
-    (calls 3-4): the graph passes the DAG check, and every call is bit-identical to the serial one-stream
-    direct launches (mode 2)."""
+    bounce's trace, on the L2/HBM scene) captured into one graph (launch mode 3, call 2; mode 0 would run
+    a forking call directly) and replayed (calls 3-4): the graph passes the DAG check, and every call is
+    bit-identical to the serial one-stream direct launches (mode 2)."""
     W, H = 96, 64
     sptr.setup_default(renderer, scene, p0, p1)
     cam = sptr.camera_lookat(aspect=W / H)
@@ -651,17 +658,18 @@ def test_multibatch_overlapped_graph_replay(renderer, scene, p0, p1, spp):
     out = {}
     try:
         renderer.set_wave_paths(P * 8)
-        for mode in (2, 0):
+        for mode in (2, 3):
             renderer.set_launch_mode(mode)
+            g0 = renderer.graph_info()
             runs = []
             for _ in range(4):
                 st = renderer.render(cam, W, H, spp=spp, frame_begin=1)
                 assert st.waves == spp // 8
                 runs.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow))
             out[mode] = runs
-            if mode == 0:
+            if mode == 3:
                 g = renderer.graph_info()
-                assert g["valid"] == 1, g
+                assert g["valid"] == 1 and g["captures"] == g0["captures"] + 1, (g0, g)
                 # a DAG whose longest path runs through every batch's sequence
                 assert 3 * spp // 8 < g["depth"] <= g["nodes"] <= 4096, g
                 assert g["edges"] >= g["nodes"] - 1, g
@@ -669,7 +677,7 @@ def test_multibatch_overlapped_graph_replay(renderer, scene, p0, p1, spp):
         renderer.set_wave_paths(0)
         renderer.set_launch_mode(0)
     ref = out[2][0]
-    for mode in (2, 0):
+    for mode in (2, 3):
         for a in out[mode]:
             assert np.array_equal(a[0].view(np.uint32), ref[0].view(np.uint32)), mode
             assert a[1:] == ref[1:], mode
