@@ -234,18 +234,20 @@ int sptr_set_split_refs(sptr_ctx* ctx, uint32_t max_pieces);
  * 0 = off, 1..64 (default 12).  Results do not depend on it (each path makes the same operations in
  * the same order wherever it runs); sptr_stats::paths_handed_off counts the paths. */
 int sptr_set_stragglers(sptr_ctx* ctx, uint32_t lanes);
-/* 0 (default): a render-call shape seen twice in a row (same frame parameters except frame_begin,
- * same state) is captured into a hipGraph once and replayed from then on — one graph launch per call
- * instead of ~20 kernel launches, the per-call accumulation index passed as a kernel-node argument —
- * except a call whose launches fork to the side streams (the graph executor runs a graph's branches
- * one after another, so such calls launch directly; a shape whose capture fails or is rejected also
- * launches directly from then on);
+/* 0 (default): a render-call shape of at least 2^24 samples seen twice in a row (same frame parameters
+ * except frame_begin, same state) is captured into a hipGraph once and replayed from then on — one
+ * graph launch per call instead of ~20 kernel launches, the per-call accumulation index passed as a
+ * kernel-node argument — except a call whose launches fork to the side streams (the graph executor
+ * runs a graph's branches one after another, so such calls launch directly; a shape whose capture
+ * fails or is rejected also launches directly from then on).  Smaller calls (the 1-spp interactive
+ * frames) launch directly: their replays were no faster and had wall-time spikes;
  * 1: direct kernel launches for every call; 2: direct launches, all on the render stream (no launch
- * overlapped on the context's second stream); 3: as 0 for every repeated shape, whatever its size.
+ * overlapped on the context's second stream); 3: as 0 for every repeated shape, whatever its size or
+ * side-stream launches.
  * Calls with stage timing (SPTR_FRAME_TIMING*) launch directly in every mode.  Results are identical
  * in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
-/* The launch graph the context holds (launch mode 0): valid = 1 once a call shape was captured; its
+/* The launch graph the context holds (launch modes 0 and 3): valid = 1 once a call shape was captured; its
  * node count, dependency edges and the nodes on its longest path; captures = graphs captured so far;
  * capture_status = the hipError_t of the last capture attempt that fell back to direct launches (0:
  * none).  Every captured graph is checked to be acyclic before it is instantiated (a rejected capture
