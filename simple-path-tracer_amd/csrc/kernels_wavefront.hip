@@ -58,6 +58,8 @@
 #ifndef SPTR_SKY_ILP
 #define SPTR_SKY_ILP 4  // independent samples per step of k_sky's per-pixel loop
 #endif
+#define SPTR_STR2(x) #x
+#define SPTR_STR(x) SPTR_STR2(x)  // a register name for an occupancy cap's clobber list
 #ifndef SPTR_SHADOW4_WAVES
 #define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
@@ -2821,8 +2823,6 @@ __device__ __forceinline__ bool sky_pixel(const FrameView& f, uint32_t l, int& x
 #ifndef SPTR_SKY_VGPR
 #define SPTR_SKY_VGPR 127
 #endif
-#define SPTR_STR2(x) #x
-#define SPTR_STR(x) SPTR_STR2(x)
 template <bool kCube, bool kCapped>
 __global__ void __launch_bounds__(kBlock) k_sky(EnvView sh, FrameView fin) {
 #if SPTR_SKY_VGPR
