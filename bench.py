@@ -468,6 +468,8 @@ def main():
     ap.add_argument("--stragglers", type=int, default=-1,
                     help="straggler hand-off lane threshold (-1 = library default, 0 = off; HBM scenes)")
     ap.add_argument("--tail-depth", type=int, default=0, help="first bounce traced path-per-thread (0 = library default)")
+    ap.add_argument("--pixel-lanes", type=int, default=0, choices=[0, 1, 2],
+                    help="sptr_set_pixel_lanes: 0 automatic (default), 1 one launch chain, 2 two lanes")
     ap.add_argument("--launch-mode", type=int, default=0, choices=[0, 1, 2, 3],
                     help="0: replay captured launch graphs where they pay (default); 1: direct launches; 2: direct "
                          "launches on one stream, no overlap (timing studies); 3: graphs for every repeated shape")
@@ -532,6 +534,8 @@ def main():
         r.set_tail_depth(args.tail_depth)
     if args.launch_mode:
         r.set_launch_mode(args.launch_mode)
+    if args.pixel_lanes:
+        r.set_pixel_lanes(args.pixel_lanes)
     # does the library's side stream run beside the render stream on this device (its own hardware
     # queue)?  Two 200-us one-wave spins, serial vs forked (sptr_overlap_probe)
     probe = r.overlap_probe()
@@ -619,6 +623,24 @@ def main():
     stage_full = {k: round(getattr(st_full, "ms_" + k), 3)
                   for k in ("total", "cull", "trace0", "trace", "shade0", "shade", "shadow", "tail", "accum")}
 
+    # pixel lanes (sptr_set_pixel_lanes): the timed calls' two launch chains share the GPU, so their launch
+    # durations include each other's time; an untimed pass of the same steps as one chain gives the
+    # launches' own durations (roofline_one_chain)
+    lanes_info = r.pixel_lanes_info()
+    stats_one = None
+    if lanes_info["active"] and not args.no_serial_pass and args.integrator == "wavefront":
+        r.set_pixel_lanes(1)
+        step(timing)
+        r.collect_stats()
+        torch.cuda.synchronize()
+        to0 = time.perf_counter()
+        for i in range(args.steps):
+            step(timing)
+        torch.cuda.synchronize()
+        one_elapsed = time.perf_counter() - to0
+        stats_one = [r.collect_stats()]
+        r.set_pixel_lanes(args.pixel_lanes)
+
     # untimed one-stream pass (launch mode 2) for scenes whose launches overlap on the side streams: the
     # trace and shadow launches' own durations, with nothing beside them (roofline_serial)
     stats_serial = None
@@ -692,6 +714,8 @@ def main():
             knobs["split_refs"] = args.split_refs
         if args.stragglers >= 0:
             knobs["stragglers"] = args.stragglers
+        if args.pixel_lanes:
+            knobs["pixel_lanes"] = args.pixel_lanes
         line = {
             "metric": "Mrays/sec + Msamples/sec, default scene 1920x1080, 1/2/4/8 MI355X",
             "value": round(rays / elapsed / 1e6, 2),
@@ -753,6 +777,17 @@ def main():
                 "trace": {k: rs[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")},
                 "shadow": {k: ss[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")}
                 if ss else None}
+        line["pixel_lanes"] = {"requested": lanes_info["requested"], "active": lanes_info["active"],
+                               "note": "two lanes: the shard's even and odd tiles as two concurrent launch chains "
+                                       "(each launch's duration includes the other chain's time)"
+                               if lanes_info["active"] else "one launch chain"}
+        if stats_one:
+            ro = roofline(cnt, stats_one, layout, wl.name, args.steps, env_bytes=env_bytes)
+            line["roofline_one_chain"] = {
+                "note": "untimed pass of the same steps as one launch chain (sptr_set_pixel_lanes 1): the trace "
+                        "launches' own durations; the headline value is the two-lane run's",
+                "ms_per_step": round(one_elapsed / args.steps * 1e3, 3),
+                "trace": {k: ro[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")}}
         if graph_replay:
             line["graph_replay"] = graph_replay
         if knobs:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 7
+#define SPTR_ABI_VERSION 8
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -247,6 +247,16 @@ int sptr_set_stragglers(sptr_ctx* ctx, uint32_t lanes);
  * Calls with stage timing (SPTR_FRAME_TIMING*) launch directly in every mode.  Results are identical
  * in every mode. */
 int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
+/* Pixel lanes (ABI 8): 2 = a wavefront call renders the even and the odd half of its shard's tiles as
+ * two launch chains on two streams of the same GPU, each with its own buffers (the context holds a
+ * second, internal context with a copy of the scene), so that each chain's launch tails run beside the
+ * other's work; 1 = one chain; 0 (default) = two lanes for calls of >= 2^24 samples on scenes staged into
+ * LDS, one chain otherwise.  An accumulation keeps the lane mode of its first call (frame_begin 1).
+ * Results are identical either way (each pixel's samples are the same operations in the same order);
+ * sptr_tiles_device, sptr_read_rgb8 and sptr_read_accum return the shard as one chain would. */
+int sptr_set_pixel_lanes(sptr_ctx* ctx, uint32_t lanes);
+/* The pixel-lane setting (0, 1 or 2) and whether the current accumulation runs in two lanes (0 / 1). */
+int sptr_pixel_lanes_info(const sptr_ctx* ctx, uint32_t* requested, uint32_t* active);
 /* The launch graph the context holds (launch modes 0 and 3): valid = 1 once a call shape was captured; its
  * node count, dependency edges and the nodes on its longest path; captures = graphs captured so far;
  * capture_status = the hipError_t of the last capture attempt that fell back to direct launches (0:

@@ -3906,6 +3906,24 @@ void launch_sky(const ShadeView& sh, const FrameView& f, bool capped, hipStream_
   }
 }
 
+__global__ void __launch_bounds__(kBlock) k_interleave_tiles(const uint4* a, uint32_t na, const uint4* b, uint32_t nb,
+                                                             uint4* dst, uint32_t n) {
+  constexpr uint32_t kQuads = kTilePixels / 4u;  // uint4 words per tile
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n * kQuads; q += grid_threads()) {
+    const uint32_t t = q / kQuads, r = q - t * kQuads, h = t >> 1;
+    const uint4* src = (t & 1u) ? b : a;
+    const uint32_t ns = (t & 1u) ? nb : na;
+    dst[q] = h < ns ? src[h * kQuads + r] : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+void launch_interleave_tiles(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* dst,
+                             uint32_t n, hipStream_t s) {
+  if (n == 0u) return;
+  hipLaunchKernelGGL(k_interleave_tiles, dim3(grid_for(n * (kTilePixels / 4u))), dim3(kBlock), 0, s,
+                     reinterpret_cast<const uint4*>(a), na, reinterpret_cast<const uint4*>(b), nb,
+                     reinterpret_cast<uint4*>(dst), n);
+}
+
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,
                        bool resolve, hipStream_t s) {
   if (resolve) hipLaunchKernelGGL(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);

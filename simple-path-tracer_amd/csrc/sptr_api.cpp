@@ -22,6 +22,18 @@
 
 struct sptr_ctx {
   sptr::Context c;
+  // Pixel lanes (sptr_set_pixel_lanes): a second context, with its own buffers and streams, renders the
+  // odd half of this context's tiles beside this one's launch chain, so that each chain's launch tails
+  // run beside the other's work.  Only for scenes staged into LDS (the lane holds a copy of the scene).
+  sptr_ctx* lane = nullptr;
+  bool is_lane = false;
+  uint32_t lanes_req = 0;   // 0: automatic, 1: one chain, 2: two lanes
+  bool lane_scene = false;  // the lane context holds this context's scene
+  bool split = false;       // the current accumulation runs in two lanes
+  hipEvent_t lane_fork = nullptr, lane_join = nullptr;
+  sptr::DevBuf tiles_full;  // with split: this context's tiles, interleaved from the two lanes'
+  uint32_t full_tiles = 0;
+  int full_G = 1, full_R = 0;
 };
 
 namespace sptr {
@@ -484,7 +496,7 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
   if (!(f.flags & SPTR_FRAME_NO_RESOLVE)) {
     tm.begin(4);
     launch_resolve(fv, static_cast<const float4*>(c.accum.p), 0u, static_cast<uint32_t*>(c.tiles.p),
-                   static_cast<uint8_t*>(c.image.p), s);
+                   c.image_out ? c.image_out : static_cast<uint8_t*>(c.image.p), s);
     tm.end();
   }
   tm.end_call();
@@ -711,7 +723,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     join_sky = false;
     tm.begin(4);
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
-                      static_cast<uint8_t*>(c.image.p), resolve, s);
+                      c.image_out ? c.image_out : static_cast<uint8_t*>(c.image.p), resolve, s);
     tm.end();
     done += kk;
     ++waves;
@@ -998,6 +1010,8 @@ using namespace sptr;
 
 extern "C" {
 
+static void add_stats(sptr_stats& a, const sptr_stats& b);  // (pixel lanes, below)
+
 int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
 
 
@@ -1031,7 +1045,26 @@ static void install_segv_trace() {
   });
 }
 
+static int create_one(int device, sptr_ctx** out);
 int sptr_create(int device, sptr_ctx** out) {
+  const int rc = create_one(device, out);
+  if (rc != SPTR_OK) return rc;
+  sptr_ctx* x = *out;
+  // the pixel lane: a context of its own (created now, given a scene only when it is staged into LDS)
+  if (create_one(device, &x->lane) != SPTR_OK) x->lane = nullptr;
+  if (x->lane) {
+    x->lane->is_lane = true;
+    if (hipEventCreateWithFlags(&x->lane_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->lane_join, hipEventDisableTiming) != hipSuccess) {
+      (void)sptr_destroy(x);
+      *out = nullptr;
+      return SPTR_ERR_HIP;
+    }
+  }
+  return SPTR_OK;
+}
+
+static int create_one(int device, sptr_ctx** out) {
   if (!out) return SPTR_ERR_INVALID;
   install_segv_trace();
   *out = nullptr;
@@ -1066,6 +1099,11 @@ int sptr_create(int device, sptr_ctx** out) {
 
 int sptr_destroy(sptr_ctx* x) {
   if (!x) return SPTR_ERR_INVALID;
+  if (x->lane) (void)sptr_destroy(x->lane);
+  x->lane = nullptr;
+  for (hipEvent_t e : {x->lane_fork, x->lane_join})
+    if (e) (void)hipEventDestroy(e);
+  free_buf(x->tiles_full);
   Context& c = x->c;
   (void)hipSetDevice(c.device);
   if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
@@ -1094,14 +1132,14 @@ int sptr_destroy(sptr_ctx* x) {
 
 const char* sptr_last_error(const sptr_ctx* x) { return x ? x->c.err.c_str() : "null context"; }
 
-int sptr_set_debug_mode(sptr_ctx* x, int mode) {
+static int set_debug_mode_one(sptr_ctx* x, int mode) {
   if (!x) return SPTR_ERR_INVALID;
   x->c.debug_mode = mode;
   ++x->c.epoch;
   return SPTR_OK;
 }
 
-int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
+static int set_leaf_size_one(sptr_ctx* x, uint32_t n) {
   if (!x) return SPTR_ERR_INVALID;
   if (n > kMaxLeafSize) return fail(x->c, SPTR_ERR_INVALID, "leaf size must be 0 (automatic) or 1..16");
   x->c.leaf_size = n;
@@ -1109,7 +1147,7 @@ int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   return SPTR_OK;
 }
 
-int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
+static int set_bvh_width_one(sptr_ctx* x, uint32_t width) {
   if (!x) return SPTR_ERR_INVALID;
   if (width != 0 && width != 2 && width != (uint32_t)kWide)
     return fail(x->c, SPTR_ERR_INVALID, "bvh width must be 0 (auto), 2 or " + std::to_string(kWide));
@@ -1118,7 +1156,7 @@ int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
   return SPTR_OK;
 }
 
-int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
+static int set_tail_depth_one(sptr_ctx* x, uint32_t depth) {
   if (!x) return SPTR_ERR_INVALID;
   if (depth > (uint32_t)kMaxDepth) return fail(x->c, SPTR_ERR_INVALID, "tail depth must be 0 (automatic) or 1..32");
   x->c.tail_depth = depth;
@@ -1126,7 +1164,7 @@ int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
   return SPTR_OK;
 }
 
-int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
+static int set_split_refs_one(sptr_ctx* x, uint32_t max_pieces) {
   if (!x) return SPTR_ERR_INVALID;
   if (max_pieces == 0u) max_pieces = 1u;
   if (max_pieces > 32u || (max_pieces & (max_pieces - 1u)))
@@ -1136,7 +1174,7 @@ int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
   return SPTR_OK;
 }
 
-int sptr_set_stragglers(sptr_ctx* x, uint32_t lanes) {
+static int set_stragglers_one(sptr_ctx* x, uint32_t lanes) {
   if (!x) return SPTR_ERR_INVALID;
   if (lanes > 64u) return fail(x->c, SPTR_ERR_INVALID, "straggler lanes: 0 (no hand-off) to 64");
   x->c.strag_lanes = lanes;
@@ -1144,7 +1182,7 @@ int sptr_set_stragglers(sptr_ctx* x, uint32_t lanes) {
   return SPTR_OK;
 }
 
-int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
+static int set_wave_paths_one(sptr_ctx* x, uint64_t max_paths) {
   if (!x) return SPTR_ERR_INVALID;
   if (max_paths > (1ull << 30)) return fail(x->c, SPTR_ERR_INVALID, "wave paths above 2^30");
   x->c.wave_paths = max_paths;
@@ -1152,7 +1190,7 @@ int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
   return SPTR_OK;
 }
 
-int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
+static int upload_scene_one(sptr_ctx* x, const sptr_scene* s) {
   if (!x || !s) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
@@ -1214,7 +1252,7 @@ int sptr_scene_layout_info(const sptr_ctx* x, sptr_scene_layout* out) {
   return SPTR_OK;
 }
 
-int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
+static int set_materials_one(sptr_ctx* x, const sptr_material* m, uint32_t n) {
   if (!x || (n && !m)) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
@@ -1228,7 +1266,7 @@ int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
   return resolve_geom_materials(c);
 }
 
-int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
+static int set_lights_one(sptr_ctx* x, const sptr_light* l, uint32_t n) {
   if (!x || (n && !l)) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (n > (uint32_t)kMaxLights) return fail(c, SPTR_ERR_INVALID, "too many lights");
@@ -1252,7 +1290,7 @@ int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
   return SPTR_OK;
 }
 
-int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
+static int set_environment_one(sptr_ctx* x, const sptr_environment* e) {
   if (!x) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;  // a pending render may still read the old state
@@ -1285,7 +1323,7 @@ int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
   return SPTR_OK;
 }
 
-int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
+static int render_one(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
   if (!x || !f) return SPTR_ERR_INVALID;
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
@@ -1467,7 +1505,7 @@ int sptr_overlap_probe(sptr_ctx* x, double* ms) {
   return SPTR_OK;
 }
 
-int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
+static int set_launch_mode_one(sptr_ctx* x, uint32_t mode) {
   if (!x) return SPTR_ERR_INVALID;
   if (mode > 3)
     return fail(x->c, SPTR_ERR_INVALID,
@@ -1480,13 +1518,22 @@ int sptr_collect_stats(sptr_ctx* x, sptr_stats* stats) {
   if (!x) return SPTR_ERR_INVALID;
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
-  return collect_pending(c, stats);
+  if (!x->lane || x->lane->c.pending == 0) return collect_pending(c, stats);
+  sptr_stats a{}, b{};
+  int rc = collect_pending(c, &a);
+  if (rc != SPTR_OK) return rc;
+  rc = collect_pending(x->lane->c, &b);
+  if (rc != SPTR_OK) return fail(c, rc, std::string("pixel lane: ") + x->lane->c.err);
+  add_stats(a, b);
+  if (stats) *stats = a;
+  return SPTR_OK;
 }
 
 int sptr_read_rgb8(sptr_ctx* x, uint8_t* rgb) {
   if (!x || !rgb) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (sync_pending(c) != SPTR_OK) return SPTR_ERR_HIP;
+  if (x->split && sync_pending(x->lane->c) != SPTR_OK) return SPTR_ERR_HIP;  // (it resolves into this image)
   if (!c.image.p) return fail(c, SPTR_ERR_NO_SCENE, "read_rgb8: nothing rendered");
   API_HIP(hipSetDevice(c.device));
   API_HIP(hipMemcpy(rgb, c.image.p, (size_t)c.W * c.H * 3, hipMemcpyDeviceToHost));
@@ -1502,13 +1549,23 @@ int sptr_read_accum(sptr_ctx* x, float* out) {
   std::vector<float> a((size_t)c.P * 4);
   API_HIP(hipMemcpy(a.data(), c.accum.p, a.size() * 4, hipMemcpyDeviceToHost));
   std::memset(out, 0, (size_t)c.W * c.H * 3 * 4);
-  for (uint32_t l = 0; l < c.P; ++l) {
-    int px, py;
-    if (!host_local_pixel(c, l, px, py)) continue;
-    float* o = out + ((size_t)py * c.W + px) * 3;
-    o[0] = a[(size_t)l * 4 + 0];
-    o[1] = a[(size_t)l * 4 + 1];
-    o[2] = a[(size_t)l * 4 + 2];
+  auto scatter = [&](const Context& cc, const std::vector<float>& acc) {
+    for (uint32_t l = 0; l < cc.P; ++l) {
+      int px, py;
+      if (!host_local_pixel(cc, l, px, py)) continue;
+      float* o = out + ((size_t)py * cc.W + px) * 3;
+      o[0] = acc[(size_t)l * 4 + 0];
+      o[1] = acc[(size_t)l * 4 + 1];
+      o[2] = acc[(size_t)l * 4 + 2];
+    }
+  };
+  scatter(c, a);
+  if (x->split) {  // the odd half of the tiles, from the lane
+    Context& cy = x->lane->c;
+    if (sync_pending(cy) != SPTR_OK) return SPTR_ERR_HIP;
+    std::vector<float> b((size_t)cy.P * 4);
+    API_HIP(hipMemcpy(b.data(), cy.accum.p, b.size() * 4, hipMemcpyDeviceToHost));
+    scatter(cy, b);
   }
   return SPTR_OK;
 }
@@ -1517,6 +1574,11 @@ int sptr_tiles_device(sptr_ctx* x, void** dptr, size_t* bytes) {
   if (!x || !dptr || !bytes) return SPTR_ERR_INVALID;
   Context& c = x->c;
   if (!c.tiles.p) return fail(c, SPTR_ERR_NO_SCENE, "tiles_device: nothing rendered");
+  if (x->split) {  // the two lanes' tiles, interleaved into this context's shard order by sptr_render
+    *dptr = x->tiles_full.p;
+    *bytes = (size_t)x->full_tiles * kTilePixels * 4;
+    return SPTR_OK;
+  }
   *dptr = c.tiles.p;
   *bytes = (size_t)c.P * 4;
   return SPTR_OK;
@@ -1703,6 +1765,240 @@ int sptr_scan_u32(sptr_ctx* x, const uint32_t* in, uint32_t n, uint32_t* out) {
   API_HIP(hipStreamSynchronize(c.stream));
   if (n) API_HIP(hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost));
   return SPTR_OK;
+}
+
+
+// ---- pixel lanes -------------------------------------------------------------------------------
+// A setter applied to the lane context too: its failure is reported through this context's error text.
+static int lane_forward(sptr_ctx* x, int rc_lane) {
+  if (!x || !x->lane || rc_lane == SPTR_OK) return SPTR_OK;
+  return fail(x->c, rc_lane, std::string("pixel lane: ") + x->lane->c.err);
+}
+
+int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
+  const int rc = upload_scene_one(x, s);
+  if (rc != SPTR_OK) return rc;
+  x->split = false;
+  x->lane_scene = false;
+  // the lane gets a copy only of scenes staged into LDS (small by construction): the two chains of a
+  // larger scene traversed from L2/HBM compete for the same memory latency (r05zs: C5 8.0 -> 7.6-7.7 ms,
+  // but a second copy of a 10M-triangle scene), and C3's VALU-bound sky gains nothing (3.55-3.63 -> 3.65)
+  if (x->lane && scene_view(x->c).lds_bytes != 0) {
+    const int r1 = upload_scene_one(x->lane, s);
+    if (r1 != SPTR_OK) return lane_forward(x, r1);
+    x->lane_scene = true;
+  }
+  return SPTR_OK;
+}
+
+int sptr_set_pixel_lanes(sptr_ctx* x, uint32_t lanes) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (lanes > 2u) return fail(x->c, SPTR_ERR_INVALID, "pixel lanes: 0 (automatic), 1 or 2");
+  if (x->is_lane) return fail(x->c, SPTR_ERR_INVALID, "pixel lanes: not on a lane context");
+  if (lanes == 2u && !x->lane) return fail(x->c, SPTR_ERR_INVALID, "pixel lanes: no lane context");
+  if (sync_pending(x->c) != SPTR_OK) return SPTR_ERR_HIP;
+  if (x->lane && sync_pending(x->lane->c) != SPTR_OK) return SPTR_ERR_HIP;
+  x->lanes_req = lanes;
+  x->split = false;  // the next call starts an accumulation of its own (frame_begin 1)
+  x->c.last_samples = 0;
+  return SPTR_OK;
+}
+
+int sptr_pixel_lanes_info(const sptr_ctx* x, uint32_t* requested, uint32_t* active) {
+  if (!x) return SPTR_ERR_INVALID;
+  if (requested) *requested = x->lanes_req;
+  if (active) *active = x->split ? 1u : 0u;
+  return SPTR_OK;
+}
+
+// Two lanes for this call: an accumulation continues in the mode it started in; a new one (frame_begin 1)
+// runs in two lanes when the scene is staged into LDS, the integrator is the wavefront one and the call
+// is large (>= 2^24 samples: r05zs, two contexts on one GPU, C2 3.0 -> 2.47 ms, C4 158.5 -> 137.5 ms, the
+// 8-way C2 shard 0.49-0.51 -> 0.46 ms; 1-spp frames keep one chain), or when asked for (lanes_req 2).
+static bool lanes_for(const sptr_ctx* x, const sptr_frame* f) {
+  if (!x->lane || !x->lane_scene || x->lanes_req == 1u || f->integrator != SPTR_INTEGRATOR_WAVEFRONT) return false;
+  const int G = f->shard_count > 0 ? f->shard_count : 1, R = f->shard_count > 0 ? f->shard_rank : 0;
+  const int ntiles = ((f->width + kTile - 1) / kTile) * ((f->height + kTile - 1) / kTile);
+  if (R < 0 || R >= G || R + G >= ntiles) return false;  // the second lane would hold no tile
+  if (f->frame_begin != 1) return x->split;
+  if (x->lanes_req == 2u) return true;
+  const uint64_t px = (uint64_t)shard_tiles(f->width, f->height, G, R) * kTilePixels;
+  return px * f->spp >= (1ull << 24);
+}
+
+static void add_stats(sptr_stats& a, const sptr_stats& b) {
+  // the counters add, and so do the stage times (sums of launch durations); the call spans overlap
+  const double total = std::max(a.ms_total, b.ms_total);
+  a.rays_closest += b.rays_closest;
+  a.rays_shadow += b.rays_shadow;
+  a.samples += b.samples;
+  a.waves += b.waves;
+  a.ms_raygen += b.ms_raygen;
+  a.ms_trace += b.ms_trace;
+  a.ms_shade += b.ms_shade;
+  a.ms_shadow += b.ms_shadow;
+  a.ms_accum += b.ms_accum;
+  a.trace_launches += b.trace_launches;
+  a.node_visits += b.node_visits;
+  a.tri_tests += b.tri_tests;
+  a.sphere_tests += b.sphere_tests;
+  a.shadow_node_visits += b.shadow_node_visits;
+  a.shadow_prim_tests += b.shadow_prim_tests;
+  a.ms_trace0 += b.ms_trace0;
+  a.ms_shade0 += b.ms_shade0;
+  a.rays_tail += b.rays_tail;
+  a.ms_tail += b.ms_tail;
+  a.traced_primary += b.traced_primary;
+  a.traced_bounce += b.traced_bounce;
+  a.node_visits_primary += b.node_visits_primary;
+  a.tri_tests_primary += b.tri_tests_primary;
+  a.sphere_tests_primary += b.sphere_tests_primary;
+  a.ms_cull += b.ms_cull;
+  a.cull_launches += b.cull_launches;
+  a.shadow_launches += b.shadow_launches;
+  for (int i = 0; i < 8; ++i) {
+    a.traced_by_depth[i] += b.traced_by_depth[i];
+    a.nodes_by_depth[i] += b.nodes_by_depth[i];
+  }
+  for (int i = 0; i < 16; ++i) {
+    a.trace_visit_hist[i] += b.trace_visit_hist[i];
+    a.shadow_visit_hist[i] += b.shadow_visit_hist[i];
+  }
+  a.hits_primary += b.hits_primary;
+  a.hits_bounce += b.hits_bounce;
+  a.paths_handed_off += b.paths_handed_off;
+  for (int i = 0; i < 3; ++i) a.strag_visits[i] += b.strag_visits[i];
+  a.ms_total = total;
+}
+
+int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
+  if (!x || !f) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  if (!lanes_for(x, f)) {
+    if (x->split) {  // leaving a two-lane accumulation: this call must start a new one
+      if (f->frame_begin != 1) return fail(c, SPTR_ERR_INVALID, "render: frame_begin must be 1 after a two-lane accumulation");
+      if (sync_pending(x->lane->c) != SPTR_OK) return SPTR_ERR_HIP;
+      x->split = false;
+      c.W = 0;  // the pixel buffers describe the even lane: re-laid out for the whole shard
+    }
+    return render_one(x, f, stream, stats);
+  }
+  // two lanes: this context renders shard (R, 2G) — the even half of shard (R, G)'s tiles — and the
+  // lane shard (R + G, 2G), the odd half, on its own stream, forked after everything enqueued on s so far
+  // and joined back into s
+  API_HIP(hipSetDevice(c.device));
+  sptr_ctx* y = x->lane;
+  Context& cy = y->c;
+  const int G = f->shard_count > 0 ? f->shard_count : 1, R = f->shard_count > 0 ? f->shard_rank : 0;
+  sptr_frame f0 = *f, f1 = *f;
+  f0.shard_count = f1.shard_count = 2 * G;
+  f0.shard_rank = R;
+  f1.shard_rank = R + G;
+  f0.flags |= SPTR_FRAME_ASYNC;
+  f1.flags |= SPTR_FRAME_ASYNC;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
+  const bool serial = c.launch_mode == 2u;  // one stream: the lanes one after the other
+  hipStream_t sy = serial ? s : cy.stream;
+  if (c.pending && s != c.pending_stream)
+    return fail(c, SPTR_ERR_INVALID, "render: asynchronous renders must stay on one stream until sptr_collect_stats");
+  if (!x->split || c.W != f->width || c.H != f->height || x->full_G != G || x->full_R != R) {
+    if (f->frame_begin != 1) return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
+    if (sync_pending(c) != SPTR_OK || sync_pending(cy) != SPTR_OK) return SPTR_ERR_HIP;
+    x->full_G = G;
+    x->full_R = R;
+    x->full_tiles = shard_tiles(f->width, f->height, G, R);
+    API_HIP(ensure_buf(x->tiles_full, (size_t)x->full_tiles * kTilePixels * 4));
+    API_HIP(hipMemsetAsync(x->tiles_full.p, 0, (size_t)x->full_tiles * kTilePixels * 4, s));
+  }
+  x->split = true;
+  // this context's pixel buffers first (the image both lanes resolve into is cleared on s before the fork)
+  bool resized = false;
+  int rc = ensure_pixels(c, f->width, f->height, 2 * G, R, s, resized);
+  if (rc != SPTR_OK) return rc;
+  cy.image_out = static_cast<uint8_t*>(c.image.p);
+  if (!serial) {
+    API_HIP(hipEventRecord(x->lane_fork, s));
+    API_HIP(hipStreamWaitEvent(sy, x->lane_fork, 0));
+  }
+  rc = render_one(x, &f0, s, nullptr);
+  if (rc != SPTR_OK) return rc;
+  rc = render_one(y, &f1, sy, nullptr);
+  if (rc != SPTR_OK) return fail(c, rc, std::string("pixel lane: ") + cy.err);
+  if (!serial) {
+    API_HIP(hipEventRecord(x->lane_join, sy));
+    API_HIP(hipStreamWaitEvent(s, x->lane_join, 0));
+  }
+  // this context's tiles (the multi-GPU gather's send buffer): the lanes' tiles interleaved
+  launch_interleave_tiles(static_cast<const uint32_t*>(c.tiles.p), c.local_tiles, static_cast<const uint32_t*>(cy.tiles.p),
+                          cy.local_tiles, static_cast<uint32_t*>(x->tiles_full.p), x->full_tiles, s);
+  API_HIP(hipGetLastError());
+  if (f->flags & SPTR_FRAME_ASYNC) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    return SPTR_OK;
+  }
+  sptr_stats a{}, b{};
+  rc = collect_pending(c, &a);
+  if (rc != SPTR_OK) return rc;
+  rc = collect_pending(cy, &b);
+  if (rc != SPTR_OK) return fail(c, rc, std::string("pixel lane: ") + cy.err);
+  add_stats(a, b);
+  if (stats) *stats = a;
+  return SPTR_OK;
+}
+
+int sptr_set_debug_mode(sptr_ctx* x, int mode) {
+  const int rc = set_debug_mode_one(x, mode);
+  return rc == SPTR_OK ? lane_forward(x, set_debug_mode_one(x ? x->lane : nullptr, mode)) : rc;
+}
+
+int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
+  const int rc = set_leaf_size_one(x, n);
+  return rc == SPTR_OK ? lane_forward(x, set_leaf_size_one(x ? x->lane : nullptr, n)) : rc;
+}
+
+int sptr_set_bvh_width(sptr_ctx* x, uint32_t width) {
+  const int rc = set_bvh_width_one(x, width);
+  return rc == SPTR_OK ? lane_forward(x, set_bvh_width_one(x ? x->lane : nullptr, width)) : rc;
+}
+
+int sptr_set_tail_depth(sptr_ctx* x, uint32_t depth) {
+  const int rc = set_tail_depth_one(x, depth);
+  return rc == SPTR_OK ? lane_forward(x, set_tail_depth_one(x ? x->lane : nullptr, depth)) : rc;
+}
+
+int sptr_set_split_refs(sptr_ctx* x, uint32_t max_pieces) {
+  const int rc = set_split_refs_one(x, max_pieces);
+  return rc == SPTR_OK ? lane_forward(x, set_split_refs_one(x ? x->lane : nullptr, max_pieces)) : rc;
+}
+
+int sptr_set_stragglers(sptr_ctx* x, uint32_t lanes) {
+  const int rc = set_stragglers_one(x, lanes);
+  return rc == SPTR_OK ? lane_forward(x, set_stragglers_one(x ? x->lane : nullptr, lanes)) : rc;
+}
+
+int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
+  const int rc = set_wave_paths_one(x, max_paths);
+  return rc == SPTR_OK ? lane_forward(x, set_wave_paths_one(x ? x->lane : nullptr, max_paths)) : rc;
+}
+
+int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
+  const int rc = set_materials_one(x, m, n);
+  return rc == SPTR_OK ? lane_forward(x, set_materials_one(x ? x->lane : nullptr, m, n)) : rc;
+}
+
+int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
+  const int rc = set_lights_one(x, l, n);
+  return rc == SPTR_OK ? lane_forward(x, set_lights_one(x ? x->lane : nullptr, l, n)) : rc;
+}
+
+int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
+  const int rc = set_environment_one(x, e);
+  return rc == SPTR_OK ? lane_forward(x, set_environment_one(x ? x->lane : nullptr, e)) : rc;
+}
+
+int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
+  const int rc = set_launch_mode_one(x, mode);
+  return rc == SPTR_OK ? lane_forward(x, set_launch_mode_one(x ? x->lane : nullptr, mode)) : rc;
 }
 
 }  // extern "C"

@@ -347,6 +347,7 @@ struct Context {
   // 0: replay a captured graph for repeated call shapes that fork no side-stream launch (run_call);
   // 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
   uint32_t launch_mode = 0;
+  uint8_t* image_out = nullptr;  // a pixel lane's resolve target: its parent context's image (sptr_render)
   bool last_forked = false;          // the last direct launch sequence forked launches to a side stream
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
@@ -459,6 +460,10 @@ uint32_t cull_depth_for(uint32_t spp);
 void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32_t* plist, hipStream_t s);
 // capped: at most 4 waves per SIMD (beside the launch chain); else full occupancy
 void launch_sky(const ShadeView& sh, const FrameView& f, bool capped, hipStream_t s);
+// dst local tile i <- a's tile i / 2 (i even) or b's tile i / 2 (i odd): two pixel lanes' tiles in the
+// tile order of the shard they split
+void launch_interleave_tiles(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* dst,
+                             uint32_t n, hipStream_t s);
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.

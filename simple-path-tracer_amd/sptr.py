@@ -109,7 +109,7 @@ _lib = None
 # every symbol include/sptr_hip.h declares
 EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
-    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_stragglers", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
+    "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_pixel_lanes", "sptr_pixel_lanes_info", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_stragglers", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
     "sptr_read_rgb8",
     "sptr_read_accum",
@@ -139,6 +139,8 @@ def lib() -> C.CDLL:
         "sptr_set_debug_mode": (C.c_int, [vp, C.c_int]),
         "sptr_set_wave_paths": (C.c_int, [vp, u64]),
         "sptr_set_launch_mode": (C.c_int, [vp, u32]),
+        "sptr_set_pixel_lanes": (C.c_int, [vp, u32]),
+        "sptr_pixel_lanes_info": (C.c_int, [vp, C.POINTER(u32), C.POINTER(u32)]),
         "sptr_graph_info": (C.c_int, [vp, up, up, up, up, up, C.POINTER(C.c_int32)]),
         "sptr_capture_error": (C.c_char_p, [vp]),
         "sptr_overlap_probe": (C.c_int, [vp, C.POINTER(C.c_double)]),
@@ -423,10 +425,21 @@ class Renderer:
                 "side_has_own_queue": bool(ms[1] < 0.75 * ms[0]), "sky_side_has_own_queue": bool(ms[2] < 0.75 * ms[0])}
 
     def set_launch_mode(self, mode: int):
-        """0: replay captured launch graphs for repeated call shapes (default; large calls with
-        side-stream launches excepted); 1: direct launches; 2: direct launches, all on the render
-        stream (no overlap); 3: launch graphs for every repeated shape."""
+        """0: replay captured launch graphs for large repeated call shapes that fork nothing (default);
+        1: direct launches; 2: direct launches, all on the render stream (no overlap); 3: launch graphs
+        for every repeated shape."""
         self._check(self._L.sptr_set_launch_mode(self._h, mode), "set_launch_mode")
+
+    def set_pixel_lanes(self, lanes: int):
+        """0: automatic (two lanes for large calls on LDS-staged scenes); 1: one launch chain; 2: the
+        shard's even and odd tiles as two concurrent launch chains (include/sptr_hip.h)."""
+        self._check(self._L.sptr_set_pixel_lanes(self._h, lanes), "set_pixel_lanes")
+
+    def pixel_lanes_info(self) -> dict:
+        """{"requested": 0/1/2, "active": whether the current accumulation runs in two lanes}."""
+        r, a = C.c_uint32(), C.c_uint32()
+        self._check(self._L.sptr_pixel_lanes_info(self._h, C.byref(r), C.byref(a)), "pixel_lanes_info")
+        return {"requested": r.value, "active": bool(a.value)}
 
     def set_tail_depth(self, n: int):
         self._check(self._L.sptr_set_tail_depth(self._h, n), "set_tail_depth")

@@ -435,7 +435,9 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
             else:
                 assert g["captures"] == g0["captures"], (g0, g)
         # mode 0 (the default) on new shapes (other frame sizes): a small call runs direct; a large one
-        # that forks nothing is captured on its second call
+        # that forks nothing is captured on its second call (as one launch chain: two pixel lanes would
+        # halve each chain's samples)
+        renderer.set_pixel_lanes(1)
         for W0, H0, spp0, captured in ((80, H, 2, False), (1024, 256, 64, True)):
             cam0 = sptr.camera_lookat(aspect=W0 / H0)
             ref = []
@@ -464,6 +466,7 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
         assert renderer.graph_info()["captures"] == g0["captures"]
     finally:
         renderer.set_launch_mode(0)
+        renderer.set_pixel_lanes(0)
     for a, b in zip(out[1], out[3]):
         assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
         assert (a[1], a[2]) == (b[1], b[2])
@@ -804,3 +807,55 @@ def test_setter_argument_checks(renderer):
     sptr.setup_default(renderer, "default")
     st = renderer.render(sptr.camera_lookat(aspect=W / H), W, H, spp=1)
     assert st.samples == W * H
+
+
+class _DevWords:
+    """A device buffer of 32-bit words seen by torch (__cuda_array_interface__)."""
+
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes // 4,), "typestr": "<i4", "data": (ptr, False),
+                                         "version": 3}
+
+
+@pytest.mark.parametrize("shard", [(0, 1), (1, 3)])
+def test_pixel_lanes_equal_one_chain(renderer, shard):
+    """Pixel lanes (sptr_set_pixel_lanes 2): the shard's even and odd tiles rendered as two concurrent
+    launch chains by the context and its internal lane context.  The accumulation (read_accum), the
+    resolved image, the shard's tile buffer (sptr_tiles_device, the multi-GPU gather's send buffer) and
+    the query counts must equal the one-chain render bit for bit — also across a progressive
+    continuation, asynchronous calls collected once, and a return to one chain."""
+    import torch
+
+    W, H = 320, 200
+    R, G = shard
+    sptr.setup_default(renderer, "default_emitter")
+    cam = sptr.camera_lookat(aspect=W / H)
+
+    def run(lanes):
+        renderer.set_pixel_lanes(lanes)
+        st1 = renderer.render(cam, W, H, spp=6, shard_rank=R, shard_count=G)
+        st2 = renderer.render(cam, W, H, spp=5, frame_begin=7, shard_rank=R, shard_count=G)
+        acc = renderer.read_accum().copy()
+        rgb = renderer.read_rgb8().copy()
+        ptr, nbytes = renderer.tiles_device()
+        tiles = torch.as_tensor(_DevWords(ptr, nbytes), device="cuda").cpu().numpy().copy()
+        for fb in (1, 4, 7):  # asynchronous calls, one collection
+            renderer.render(cam, W, H, spp=3, frame_begin=fb, shard_rank=R, shard_count=G, flags=sptr.SPTR_FRAME_ASYNC)
+        st3 = renderer.collect_stats()
+        acc3 = renderer.read_accum().copy()
+        counts = [(s.rays_closest, s.rays_shadow, s.samples) for s in (st1, st2, st3)]
+        return acc, rgb, tiles, acc3, counts
+
+    try:
+        one = run(1)
+        two = run(2)
+        back = run(1)
+    finally:
+        renderer.set_pixel_lanes(0)
+    for a, b in ((one, two), (one, back)):
+        assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+        assert np.array_equal(a[1], b[1])
+        assert np.array_equal(a[3].view(np.uint32), b[3].view(np.uint32))
+        assert a[4] == b[4]
+        assert np.array_equal(a[2], b[2])
+    assert one[4][0][2] > 0
