@@ -149,6 +149,11 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     Beside them: counter_frac / valu_issue_frac / salu_per_valu from the session's rocprofv3 passes."""
     launches = sum(s.trace_launches for s in stats)
     avg_launch_s = sum(s.ms_trace for s in stats) / max(1, launches) * 1e-3
+    # the launches' busy time (union of their intervals): two pixel lanes' trace launches overlap, so each
+    # launch's own duration includes the time it shares with the other lane's; the achieved rate divides
+    # the bytes by the busy time (one chain: busy = the sum of the durations, the same figure)
+    busy_s = sum(getattr(s, "ms_trace_busy", 0.0) for s in stats) * 1e-3
+    eff_launch_s = busy_s / max(1, launches) if busy_s > 0 else avg_launch_s
     tp = sum(s.traced_primary for s in stats)
     tb = sum(s.traced_bounce for s in stats)
     # visits and hit fractions per traversed ray, bounce 0 and later bounces (instrumented step)
@@ -173,17 +178,19 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     strag_bytes = node_b * sv[0] + 48.0 * sv[1] + 16.0 * sv[2] if residency == "hbm" else 0.0
     scene -= strag_bytes
     per_launch = (stream + scene) / max(1, launches)
-    achieved = per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    achieved = per_launch / eff_launch_s / 1e9 if eff_launch_s > 0 else 0.0
     s8d = ((STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (tp + tb) + 64.0 * (pp[0] * tp + pb[0] * tb)
            + 48.0 * (pp[1] * tp + pb[1] * tb) + 16.0 * (pp[2] * tp + pb[2] * tb)) / max(1, launches)
     out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    out.update(_counter_fracs(wl_name, "trace", avg_launch_s, stream_read / max(1, launches)))
+    out.update(_counter_fracs(wl_name, "trace", eff_launch_s, stream_read / max(1, launches)))
     if residency == "lds":
-        out["s8d_lds_frac"] = round(s8d / avg_launch_s / 1e9 / LDS_PEAK_GBS, 4) if avg_launch_s else None
+        out["s8d_lds_frac"] = round(s8d / eff_launch_s / 1e9 / LDS_PEAK_GBS, 4) if eff_launch_s else None
     else:
-        out["frac_s8d"] = round(s8d / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4) if avg_launch_s else None
+        out["frac_s8d"] = round(s8d / eff_launch_s / 1e9 / HBM_PEAK_GBS, 4) if eff_launch_s else None
     out.update({
+        "busy_ms_per_step": round(busy_s * 1e3 / max(1, steps), 4),
+        "busy_us_per_launch": round(eff_launch_s * 1e6, 2),
         "s8d_bytes_per_launch": round(s8d),
         "bytes_per_launch": round(per_launch), "stream_bytes_per_launch": round(stream / max(1, launches)),
         "scene_hbm_bytes_per_bounce_ray": round(scene_b) if residency == "hbm" else 0,
@@ -578,10 +585,11 @@ def main():
             ev[1].record()
         if distributed:
             gather_tiles(src, gathered, world, rank)
-        else:
+        elif shards > 1:  # --emulate-shards: shard 0's tiles in the gather buffer (the others stay 0)
             gathered[: src.numel()].copy_(src)
+        tiles_in = gathered if shards > 1 else src  # one GPU, whole frame: unpacked in place
         if rank == 0:
-            r.unpack_tiles(gathered.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
+            r.unpack_tiles(tiles_in.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
         if ev:
             ev[2].record()
 
@@ -778,8 +786,10 @@ def main():
                 "shadow": {k: ss[k] for k in ("achieved", "frac", "avg_launch_us", "launches_per_step", "bytes_per_launch")}
                 if ss else None}
         line["pixel_lanes"] = {"requested": lanes_info["requested"], "active": lanes_info["active"],
-                               "note": "two lanes: the shard's even and odd tiles as two concurrent launch chains "
-                                       "(each launch's duration includes the other chain's time)"
+                               "note": "two lanes: the shard's even and odd tiles as two concurrent launch chains; "
+                                       "each launch's duration (avg_launch_us) includes the other chain's time, so "
+                                       "roofline.achieved divides the trace bytes by the trace launches' busy time "
+                                       "(the union of their intervals over both lanes, busy_us_per_launch)"
                                if lanes_info["active"] else "one launch chain"}
         if stats_one:
             ro = roofline(cnt, stats_one, layout, wl.name, args.steps, env_bytes=env_bytes)

@@ -199,6 +199,9 @@ typedef struct sptr_stats {
                                          (sptr_set_stragglers) */
   uint64_t strag_visits[3];           /* ABI 6: node visits, triangle and sphere tests of the handed-off
                                          rays' walks made by the straggler kernel (every call) */
+  double ms_trace_busy;               /* ABI 8, SPTR_FRAME_TIMING / _TIMING_TRACE: the trace launches'
+                                         busy time, the union of their intervals (= ms_trace for one
+                                         launch chain; two pixel lanes' trace launches overlap) */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */

@@ -329,6 +329,42 @@ struct StageTimer {
   }
 };
 
+// Busy time of the trace stage over the pending calls of contexts cs[0..n): the union of the trace
+// launches' intervals (stages 1 and 5), each placed on one clock by its events' offsets from the first
+// trace mark's begin event (two pixel lanes' trace launches run on two streams and overlap).  0 when a
+// stream or an event fails (collect_pending reports that failure).
+double trace_busy_ms(Context* const* cs, int n) {
+  std::vector<std::pair<float, float>> iv;
+  hipEvent_t ref = nullptr;
+  for (int k = 0; k < n; ++k) {
+    Context& c = *cs[k];
+    if (c.pending == 0) continue;
+    if (hipStreamSynchronize(c.pending_stream) != hipSuccess) return 0.0;
+    for (const StageMark& m : c.marks) {
+      if ((m.stage != 1 && m.stage != 5) || m.b >= c.events.size() || m.e >= c.events.size()) continue;
+      if (!ref) ref = c.events[m.b];
+      float b = 0.0f, e = 0.0f;
+      if (hipEventElapsedTime(&b, ref, c.events[m.b]) != hipSuccess ||
+          hipEventElapsedTime(&e, ref, c.events[m.e]) != hipSuccess)
+        return 0.0;
+      iv.emplace_back(b, e);
+    }
+  }
+  std::sort(iv.begin(), iv.end());
+  double busy = 0.0;
+  float lo = 0.0f, hi = 0.0f;
+  for (size_t i = 0; i < iv.size(); ++i) {
+    if (i == 0 || iv[i].first > hi) {
+      busy += hi - lo;
+      lo = iv[i].first;
+      hi = iv[i].second;
+    } else {
+      hi = std::max(hi, iv[i].second);
+    }
+  }
+  return busy + (hi - lo);
+}
+
 // Wait for the pending render calls, fold their device counters and stage events into *stats
 // (may be null) and start a new collection window.
 int collect_pending(Context& c, sptr_stats* stats) {
@@ -336,6 +372,8 @@ int collect_pending(Context& c, sptr_stats* stats) {
   if (c.pending == 0) return SPTR_OK;
   // (the side streams' work is joined into pending_stream: complete once it is)
   const hipError_t se = hipStreamSynchronize(c.pending_stream);
+  Context* self = &c;
+  const double busy = se == hipSuccess && stats ? trace_busy_ms(&self, 1) : 0.0;
   double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t trace_launches = 0, shadow_launches = 0;
   for (const StageMark& m : c.marks) {
@@ -397,6 +435,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   stats->paths_handed_off = tot[kTotStrag];
   for (int i = 0; i < 3; ++i) stats->strag_visits[i] = tot[kTotStragNodes + i];
   stats->cull_launches = culls;
+  stats->ms_trace_busy = busy;
   return SPTR_OK;
 }
 
@@ -517,7 +556,7 @@ bool overlap_enabled(const Context& c) {
   }();
   if (!env) return false;
 #endif
-  return c.launch_mode != 2;
+  return c.launch_mode != 2 && c.side_stream && c.side2_stream;  // (a pixel lane has no side streams)
 }
 
 // Launch sequence of a wavefront call (batches of k samples, tail from bounce T) on stream s (the
@@ -908,6 +947,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     // would fold the next direct launches into a dead graph): end the capture on any that did not
     bool stuck = false;
     for (hipStream_t st : {c.cap_stream, c.cap_side, c.cap_side2}) {
+      if (!st) continue;
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
         stuck = true;
@@ -1045,13 +1085,14 @@ static void install_segv_trace() {
   });
 }
 
-static int create_one(int device, sptr_ctx** out);
+static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent);
 int sptr_create(int device, sptr_ctx** out) {
-  const int rc = create_one(device, out);
+  const int rc = create_one(device, out, nullptr);
   if (rc != SPTR_OK) return rc;
   sptr_ctx* x = *out;
-  // the pixel lane: a context of its own (created now, given a scene only when it is staged into LDS)
-  if (create_one(device, &x->lane) != SPTR_OK) x->lane = nullptr;
+  // the pixel lane: a context of its own (created now, given a scene and a stream only when the scene
+  // is staged into LDS)
+  if (create_one(device, &x->lane, x) != SPTR_OK) x->lane = nullptr;
   if (x->lane) {
     x->lane->is_lane = true;
     if (hipEventCreateWithFlags(&x->lane_fork, hipEventDisableTiming) != hipSuccess ||
@@ -1064,7 +1105,13 @@ int sptr_create(int device, sptr_ctx** out) {
   return SPTR_OK;
 }
 
-static int create_one(int device, sptr_ctx** out) {
+// parent: a pixel lane's context.  It creates no stream here: it borrows the parent's capture stream
+// (captures run one at a time on the calling thread), gets its render stream when it is given a scene
+// (sptr_upload_scene) and has no side streams (it renders only scenes staged into LDS, whose launches
+// run on one stream).  r05zw: every stream a context creates is one more for the runtime to place on
+// the process's hardware queues, and a lane created with a full set of six slowed the parent's
+// overlapped C5 / C3 calls from 7.23 / 3.33 to 8.48 / 3.67 ms with the lane never used.
+static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
   if (!out) return SPTR_ERR_INVALID;
   install_segv_trace();
   *out = nullptr;
@@ -1074,7 +1121,16 @@ static int create_one(int device, sptr_ctx** out) {
   sptr_ctx* x = new sptr_ctx();
   Context& c = x->c;
   c.device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
+  if (parent) {
+    c.cap_stream = parent->c.cap_stream;
+    c.prio_lo = parent->c.prio_lo;
+    c.prio_hi = parent->c.prio_hi;
+    if (hipSetDevice(device) != hipSuccess || !create_events(c)) {
+      c.cap_stream = nullptr;
+      delete x;
+      return SPTR_ERR_HIP;
+    }
+  } else if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess ||
       // the side streams at the lowest priority: a priority of its own puts a stream on a hardware
       // queue of its own, so that its launches can run beside the main sequence's.  (r05t: the main
@@ -1106,8 +1162,9 @@ int sptr_destroy(sptr_ctx* x) {
   free_buf(x->tiles_full);
   Context& c = x->c;
   (void)hipSetDevice(c.device);
+  if (x->is_lane) c.cap_stream = nullptr;  // (the parent's)
   if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
-  (void)hipStreamSynchronize(c.stream);
+  if (c.stream) (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
                     &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist};
@@ -1519,12 +1576,15 @@ int sptr_collect_stats(sptr_ctx* x, sptr_stats* stats) {
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
   if (!x->lane || x->lane->c.pending == 0) return collect_pending(c, stats);
+  Context* both[2] = {&c, &x->lane->c};
+  const double busy = stats ? trace_busy_ms(both, 2) : 0.0;
   sptr_stats a{}, b{};
   int rc = collect_pending(c, &a);
   if (rc != SPTR_OK) return rc;
   rc = collect_pending(x->lane->c, &b);
   if (rc != SPTR_OK) return fail(c, rc, std::string("pixel lane: ") + x->lane->c.err);
   add_stats(a, b);
+  a.ms_trace_busy = busy;
   if (stats) *stats = a;
   return SPTR_OK;
 }
@@ -1784,6 +1844,14 @@ int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
   // larger scene traversed from L2/HBM compete for the same memory latency (r05zs: C5 8.0 -> 7.6-7.7 ms,
   // but a second copy of a 10M-triangle scene), and C3's VALU-bound sky gains nothing (3.55-3.63 -> 3.65)
   if (x->lane && scene_view(x->c).lds_bytes != 0) {
+    Context& cy = x->lane->c;
+    // (a priority of its own puts the lane's stream on a hardware queue apart from the render stream's:
+    // created at the default priority it shared that queue and the two chains ran one after the other,
+    // r05zx, C2 3.24 ms; at the lowest priority, the side streams', 2.56-2.58; at the highest 2.67-2.69)
+    if (!cy.stream && hipStreamCreateWithPriority(&cy.stream, hipStreamNonBlocking, x->c.prio_lo) != hipSuccess) {
+      cy.stream = nullptr;
+      return fail(x->c, SPTR_ERR_HIP, "pixel lane: stream creation failed");
+    }
     const int r1 = upload_scene_one(x->lane, s);
     if (r1 != SPTR_OK) return lane_forward(x, r1);
     x->lane_scene = true;
@@ -1869,6 +1937,7 @@ static void add_stats(sptr_stats& a, const sptr_stats& b) {
   a.paths_handed_off += b.paths_handed_off;
   for (int i = 0; i < 3; ++i) a.strag_visits[i] += b.strag_visits[i];
   a.ms_total = total;
+  a.ms_trace_busy = std::max(a.ms_trace_busy, b.ms_trace_busy);  // (the callers set the union)
 }
 
 int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stats) {
@@ -1936,12 +2005,15 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     if (stats) std::memset(stats, 0, sizeof(*stats));
     return SPTR_OK;
   }
+  Context* both[2] = {&c, &cy};
+  const double busy = stats ? trace_busy_ms(both, 2) : 0.0;
   sptr_stats a{}, b{};
   rc = collect_pending(c, &a);
   if (rc != SPTR_OK) return rc;
   rc = collect_pending(cy, &b);
   if (rc != SPTR_OK) return fail(c, rc, std::string("pixel lane: ") + cy.err);
   add_stats(a, b);
+  a.ms_trace_busy = busy;
   if (stats) *stats = a;
   return SPTR_OK;
 }

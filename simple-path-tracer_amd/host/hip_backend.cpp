@@ -92,6 +92,14 @@ bool HipBackend::renderInternal(int w, int h, const Camera& camera) {
   const std::array<float, 9> cam = {p.x, p.y, p.z, f.x, f.y, f.z, u.x, u.y, u.z};
   bool changed = !has_last_camera_ || w != last_w_ || h != last_h_;
   for (int i = 0; i < 9 && !changed; ++i) changed = std::fabs(cam[size_t(i)] - last_cam_[size_t(i)]) > 1e-4f;
+  if (settings_.pixel_lanes != lanes_applied_) {
+    if (sptr_set_pixel_lanes(ctx_, settings_.pixel_lanes) != SPTR_OK) {
+      err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);
+      return false;
+    }
+    lanes_applied_ = settings_.pixel_lanes;
+    changed = true;  // a new accumulation in the new lane mode
+  }
   if (changed) frame_index_ = 0;
   has_last_camera_ = true;
   last_cam_ = cam;

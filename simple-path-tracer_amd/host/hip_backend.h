@@ -28,6 +28,9 @@ class HipBackend {
     // sptr_set_launch_mode: 0 = replay a captured graph for repeated call shapes (default), 1 = direct
     // launches, 2 = direct on one stream, 3 = a graph for every repeated shape
     uint32_t launch_mode = 0;
+    // sptr_set_pixel_lanes: 0 = two concurrent launch chains for calls of >= 2^24 samples on scenes
+    // staged in LDS (default), 1 = one chain, 2 = two chains; a change restarts the accumulation
+    uint32_t pixel_lanes = 0;
   };
 
   explicit HipBackend(int device = 0);
@@ -72,6 +75,7 @@ class HipBackend {
   std::vector<uint32_t> geom_material_;
   std::string err_;
   int debug_mode_ = 0;
+  uint32_t lanes_applied_ = 0;  // the pixel-lane setting the context holds
 };
 
 }  // namespace backends

@@ -16,6 +16,9 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def renderer():
+    # torch first, as in bench.py: the library then binds to the HIP runtime torch loaded, and the tests
+    # that hand its device buffers to torch (tiles_device) see one runtime whichever subset runs
+    import torch  # noqa: F401
     import sptr
 
     r = sptr.Renderer(0)

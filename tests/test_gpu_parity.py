@@ -859,3 +859,56 @@ def test_pixel_lanes_equal_one_chain(renderer, shard):
         assert a[4] == b[4]
         assert np.array_equal(a[2], b[2])
     assert one[4][0][2] > 0
+
+
+@pytest.mark.gpu
+def test_trace_busy_time(renderer):
+    """sptr_stats::ms_trace_busy, the union of the trace launches' intervals: equal to the summed launch
+    durations (ms_trace) for one launch chain, and between half of them and all of them for two pixel
+    lanes, whose trace launches overlap."""
+    W, H = 320, 200
+    sptr.setup_default(renderer, "default_emitter")
+    cam = sptr.camera_lookat(aspect=W / H)
+    try:
+        for lanes in (1, 2):
+            renderer.set_pixel_lanes(lanes)
+            st = renderer.render(cam, W, H, spp=8, flags=sptr.SPTR_FRAME_TIMING_TRACE)
+            assert renderer.pixel_lanes_info()["active"] == (lanes == 2)
+            assert st.ms_trace > 0 and st.ms_trace_busy > 0
+            assert st.ms_trace_busy <= st.ms_trace * 1.001 + 1e-3
+            if lanes == 1:
+                assert st.ms_trace_busy >= st.ms_trace * 0.999 - 1e-3
+            else:
+                assert st.ms_trace_busy >= st.ms_trace * 0.5 - 1e-3
+    finally:
+        renderer.set_pixel_lanes(0)
+
+
+@pytest.mark.gpu
+def test_pixel_lanes_graph_replay(renderer):
+    """Pixel lanes in launch mode 3: each lane context captures its repeated call shape into a graph of
+    its own (on its own capture stream) and replays it on its lane stream between the fork and the join;
+    the accumulation equals one chain's direct launches bit for bit."""
+    W, H = 320, 200
+    sptr.setup_default(renderer, "default_emitter")
+    cam = sptr.camera_lookat(aspect=W / H)
+
+    def run(lanes, mode):
+        renderer.set_launch_mode(mode)
+        renderer.set_pixel_lanes(lanes)
+        g0 = renderer.graph_info()
+        for fb in (1, 5, 9, 13):
+            renderer.render(cam, W, H, spp=4, frame_begin=fb)
+        g = renderer.graph_info()
+        return renderer.read_accum().copy(), renderer.read_rgb8().copy(), g["captures"] - g0["captures"], g["valid"]
+
+    try:
+        one = run(1, 1)
+        two = run(2, 3)
+    finally:
+        renderer.set_pixel_lanes(0)
+        renderer.set_launch_mode(0)
+    assert one[2] == 0
+    assert two[2] >= 1 and two[3] == 1, "the lane call shape was not captured"
+    assert np.array_equal(one[0].view(np.uint32), two[0].view(np.uint32))
+    assert np.array_equal(one[1], two[1])
