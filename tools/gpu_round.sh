@@ -25,8 +25,9 @@ fi
 # newest summary by its collection time); tools/save_profiles.sh copies them into the tracked tree.
 for wl in "$@"; do
   echo "[$(date +%T)] rocprof kernel trace + stats $wl"
+  # (no untimed one-stream / one-chain passes: the statistics pool only launches run as the timed steps run)
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_$wl" -o run -- \
-    python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive > "$out/stats_$wl.log" 2>&1
+    python3 bench.py --workload "$wl" --steps 3 --warmup 1 --no-cpu-baseline --no-interactive --no-serial-pass $benchflags > "$out/stats_$wl.log" 2>&1
   if [ "$wl" = c3 ] || [ "$wl" = c5 ]; then  # the launches alone: one stream, nothing overlapped (roofline_serial)
     echo "[$(date +%T)] rocprof kernel trace + stats $wl, launch mode 2"
     timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats_${wl}_serial" -o run -- \

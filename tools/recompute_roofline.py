@@ -7,8 +7,13 @@ With a third file (the kernel statistics of a one-stream run, launch mode 2) the
 fractions are recomputed the same way.  step_roofline: bytes_per_step = the sum of its per-kernel bytes,
 frac = bytes_per_step / ms_per_step / peak.
 
+With --trace <kernel trace csv> (the same run's rocprofv3 run_kernel_trace.csv) and a line whose roofline
+carries busy_us_per_launch (pixel lanes: two launch chains whose trace launches overlap), the trace
+launches' busy time — the union of their dispatch intervals — per launch is recomputed from the
+dispatch timestamps and priced the way the line prices it.
+
     usage: tools/recompute_roofline.py profiles/<tag>_bench_<wl>.json profiles/<tag>_kernel_stats_<wl>.csv
-                                       [profiles/<tag>_kernel_stats_<wl>_serial.csv]
+                                       [profiles/<tag>_kernel_stats_<wl>_serial.csv] [--trace <trace csv>]
 """
 import csv
 import json
@@ -35,6 +40,33 @@ def pooled(rows, family):
     return (total / calls * 1e-3, calls) if calls else (None, 0)
 
 
+def _timed(name, family):
+    """The timed-path (kCount = false) instantiation of a kernel of `family`, by its demangled name."""
+    m = re.search(r"sptr::(k_\w+)<([^>]*)>", name)
+    if not m or m.group(1) not in COUNT_ARG or not m.group(1).startswith(family):
+        return False
+    if family == "k_trace" and m.group(1).startswith("k_shadow"):
+        return False
+    args = [a.strip() for a in m.group(2).split(",")]
+    return args[COUNT_ARG[m.group(1)]] == "false"
+
+
+def busy_per_launch(trace_rows, family="k_trace"):
+    """(union of the timed-path dispatch intervals of `family` / their count in us, count)."""
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace_rows if _timed(r["Kernel_Name"], family))
+    if not iv:
+        return None, 0
+    busy, lo, hi = 0, iv[0][0], iv[0][1]
+    for b, e in iv[1:]:
+        if b > hi:
+            busy += hi - lo
+            lo, hi = b, e
+        else:
+            hi = max(hi, e)
+    busy += hi - lo
+    return busy / len(iv) * 1e-3, len(iv)
+
+
 def _one(r, rows, family, peak):
     avg_us, calls = pooled(rows, family)
     achieved = r["bytes_per_launch"] / (avg_us * 1e-6) / 1e9
@@ -43,7 +75,7 @@ def _one(r, rows, family, peak):
             "rel_diff": round(abs(achieved / peak - r["frac"]) / r["frac"], 4)}
 
 
-def recompute(bench_path, stats_path, serial_stats_path=None):
+def recompute(bench_path, stats_path, serial_stats_path=None, trace_path=None):
     line = json.loads(open(bench_path).read().splitlines()[-1])
     rows = list(csv.DictReader(open(stats_path)))
     out = {}
@@ -51,6 +83,13 @@ def recompute(bench_path, stats_path, serial_stats_path=None):
         r = line.get(key)
         if r:
             out[key] = _one(r, rows, family, r["peak"])
+    r = line.get("roofline")
+    if r and trace_path and r.get("busy_us_per_launch"):
+        busy_us, n = busy_per_launch(list(csv.DictReader(open(trace_path))))
+        frac = r["bytes_per_launch"] / (busy_us * 1e-6) / 1e9 / r["peak"]
+        out["roofline"].update({"line_busy_us_per_launch": r["busy_us_per_launch"], "trace_busy_us_per_launch": round(busy_us, 2),
+                                "trace_launches": n, "frac_busy": round(frac, 4),
+                                "rel_diff_busy": round(abs(frac - r["frac"]) / r["frac"], 4)})
     ser = line.get("roofline_serial")
     if ser and serial_stats_path:
         srows = list(csv.DictReader(open(serial_stats_path)))
@@ -67,4 +106,10 @@ def recompute(bench_path, stats_path, serial_stats_path=None):
 
 
 if __name__ == "__main__":
-    print(json.dumps(recompute(*sys.argv[1:4]), indent=1))
+    argv = sys.argv[1:]
+    trace = None
+    if "--trace" in argv:
+        i = argv.index("--trace")
+        trace = argv[i + 1]
+        del argv[i:i + 2]
+    print(json.dumps(recompute(*argv[:3], trace_path=trace) if len(argv) >= 2 else {}, indent=1))

@@ -10,6 +10,7 @@ for wl in "$@"; do
   [ -f $run/bench_${wl}_stages.json ] && tail -1 $run/bench_${wl}_stages.json > profiles/${tag}_bench_${wl}_stages.json
   cp $run/summary_$wl.txt profiles/${tag}_summary_$wl.txt
   cp $run/stats_$wl/run_kernel_stats.csv profiles/${tag}_kernel_stats_$wl.csv
+  cp $run/stats_$wl/run_kernel_trace.csv profiles/${tag}_kernel_trace_$wl.csv
   [ -f $run/stats_${wl}_serial/run_kernel_stats.csv ] && cp $run/stats_${wl}_serial/run_kernel_stats.csv profiles/${tag}_kernel_stats_${wl}_serial.csv
   for k in trace shadow; do
     [ -f $run/pmc_${wl}_$k.json ] && cp $run/pmc_${wl}_$k.json profiles/${tag}_pmc_${wl}_$k.json
