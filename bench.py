@@ -124,7 +124,10 @@ def env_hbm_bytes(lookups, env_bytes, launches):
 
 def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     """Roofline of the dominant kernel, k_trace (all its launches: bounce 0 and the wavefront bounces
-    before the path-per-thread tail; one template).
+    before the path-per-thread tail; one template), with the fused bounce launches
+    (k_bounce: the trace and the shading of a bounce in one launch, LDS scenes in batches of at most
+    2^26 paths — the pixel lanes' chains and the sharded frames) counted as trace launches: they are the
+    same traversal, and in those chains they hold most of the traversal time.
 
     cnt: the stats of one instrumented (SPTR_FRAME_COUNT_VISITS) step, used only for per-ray ratios (BVH
     visits, hit fraction); stats: the K timed steps (launch times, launch counts and the rays the trace
@@ -156,6 +159,7 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     eff_launch_s = busy_s / max(1, launches) if busy_s > 0 else avg_launch_s
     tp = sum(s.traced_primary for s in stats)
     tb = sum(s.traced_bounce for s in stats)
+    tf = sum(getattr(s, "traced_fused", 0) for s in stats)  # bounce rays of k_bounce
     # visits and hit fractions per traversed ray, bounce 0 and later bounces (instrumented step)
     vp = [cnt.node_visits_primary, cnt.tri_tests_primary, cnt.sphere_tests_primary]
     vb = [cnt.node_visits - vp[0], cnt.tri_tests - vp[1], cnt.sphere_tests - vp[2]]
@@ -168,10 +172,14 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     scene_b = node_b * pb[0] + 48.0 * pb[1] + 16.0 * pb[2]
     stream = (tp * (hp * HIT_RECORD_BYTES + (1.0 - hp) * RAD_BYTES)
               + tb * (RAY_READ_BYTES + hb * HIT_RECORD_BYTES + (1.0 - hb) * (THR_READ_BYTES + 2 * RAD_BYTES)))
-    stream += env_hbm_bytes(tp * (1.0 - hp) + tb * (1.0 - hb), env_bytes, launches)
-    stream_read = tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))  # coalesced reads
+    # fused bounce rays (k_bounce): the visit-count pass runs them as separate trace launches, so its
+    # bounce hit fraction and visits per ray apply to them
+    stream += tf * (hb * FUSED_HIT_BYTES + (1.0 - hb) * FUSED_MISS_BYTES)
+    stream += env_hbm_bytes(tp * (1.0 - hp) + (tb + tf) * (1.0 - hb), env_bytes, launches)
+    stream_read = (tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))
+                   + tf * (RAY_READ_BYTES + THR_READ_BYTES + RAD_BYTES))  # coalesced reads
     residency, footprint = _residency(layout)
-    scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * tb}[residency]
+    scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * (tb + tf)}[residency]
     # straggler hand-off (hbm scenes): the rest of a handed-off ray's walk runs in k_strag, not in the
     # trace launch; its visits (counted in every call) are not the trace launch's bytes
     sv = [sum(list(getattr(s, "strag_visits", (0, 0, 0)))[i] for s in stats) for i in range(3)]
@@ -179,9 +187,10 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     scene -= strag_bytes
     per_launch = (stream + scene) / max(1, launches)
     achieved = per_launch / eff_launch_s / 1e9 if eff_launch_s > 0 else 0.0
-    s8d = ((STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (tp + tb) + 64.0 * (pp[0] * tp + pb[0] * tb)
-           + 48.0 * (pp[1] * tp + pb[1] * tb) + 16.0 * (pp[2] * tp + pb[2] * tb)) / max(1, launches)
-    out = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    tbf = tb + tf
+    s8d = ((STREAM_READ_BYTES + STREAM_WRITE_BYTES) * (tp + tbf) + 64.0 * (pp[0] * tp + pb[0] * tbf)
+           + 48.0 * (pp[1] * tp + pb[1] * tbf) + 16.0 * (pp[2] * tp + pb[2] * tbf)) / max(1, launches)
+    out = {"bound": "hbm", "kernel": "k_trace + k_bounce" if tf else "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4)}
     out.update(_counter_fracs(wl_name, "trace", eff_launch_s, stream_read / max(1, launches)))
     if residency == "lds":
@@ -196,7 +205,8 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
         "scene_hbm_bytes_per_bounce_ray": round(scene_b) if residency == "hbm" else 0,
         "avg_launch_us": round(avg_launch_s * 1e6, 2),
         "launches_per_step": round(launches / max(1, steps), 3),
-        "traversed_rays_per_launch": round((tp + tb) / max(1, launches)),
+        "traversed_rays_per_launch": round((tp + tb + tf) / max(1, launches)),
+        "fused_bounce_rays_per_step": round(tf / max(1, steps)),
         "handed_off": {"paths_per_launch": round(sum(getattr(s, "paths_handed_off", 0) for s in stats) / max(1, launches)),
                        "resumed_walk_bytes_per_launch": round(strag_bytes / max(1, launches))},
         "hit_fraction": {"primary": round(hp, 4), "bounce": round(hb, 4)},
@@ -259,6 +269,11 @@ def shadow_roofline(cnt, stats, layout, wl_name, steps):
 # k_shade per shaded hit: hit record (12) + ray origin/direction (32) + throughput (16) read, continuation
 # ray (o, d, thr: 48) written, radiance read-modify-write (32)
 SHADE_BYTES_PER_HIT = 12.0 + 32.0 + 16.0 + 48.0 + 32.0
+# a bounce ray of the fused k_bounce (trace + shading in one launch, LDS scenes): its ray and throughput
+# read once (48 B); a hit writes the continuation ray (48 B) and read-modify-writes the radiance (32 B,
+# charged to every hit as for k_shade), a miss read-modify-writes the radiance (32 B); no hit record
+FUSED_HIT_BYTES = 32.0 + 16.0 + 48.0 + 32.0
+FUSED_MISS_BYTES = 32.0 + 16.0 + 32.0
 SHADOW_TASK_WRITE_BYTES = 32.0  # a shadow task written by k_shade where the shadow ray has a launch of its own
 ACCUM_BYTES_PER_PIXEL = 32.0 + 7.0  # accum read-modify-write; resolved RGBA8 tile + RGB8 image written
 

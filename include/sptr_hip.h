@@ -202,6 +202,11 @@ typedef struct sptr_stats {
   double ms_trace_busy;               /* ABI 8, SPTR_FRAME_TIMING / _TIMING_TRACE: the trace launches'
                                          busy time, the union of their intervals (= ms_trace for one
                                          launch chain; two pixel lanes' trace launches overlap) */
+  uint64_t traced_fused;              /* ABI 8: queued rays of bounces >= 1 traced by the fused bounce
+                                         kernel (k_bounce: trace and shading of a bounce in one launch,
+                                         LDS-staged scenes; every call).  Its launches count as trace
+                                         launches (ms_trace, trace_launches, ms_trace_busy), and its rays
+                                         are in traced_by_depth, not in traced_bounce */
 } sptr_stats;
 
 /* ---- context ---------------------------------------------------------------------------------- */

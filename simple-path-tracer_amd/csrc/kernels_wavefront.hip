@@ -17,6 +17,7 @@
 // for line (see sptr_math.h); the file is compiled with -ffp-contract=off.  Box tests are the one
 // place that uses fma: they only prune traversal and are padded to stay conservative.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -60,11 +61,24 @@
 #endif
 #define SPTR_STR2(x) #x
 #define SPTR_STR(x) SPTR_STR2(x)  // a register name for an occupancy cap's clobber list
+// A launch timed by the stage timer (g_launch_timing set: the dispatch records its start and end into
+// the two events), else a plain launch.
+#define SPTR_TIMED_LAUNCH(kern, grid, block, lds, stream, ...)                                              \
+  do {                                                                                                   \
+    if (g_launch_timing.start) {                                                                         \
+      const LaunchTiming lt_ = g_launch_timing;                                                          \
+      g_launch_timing = LaunchTiming{};                                                                  \
+      hipExtLaunchKernelGGL(kern, grid, block, lds, stream, lt_.start, lt_.stop, 0u, __VA_ARGS__);         \
+    } else {                                                                                             \
+      hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);                                   \
+    }                                                                                                    \
+  } while (0)
 #ifndef SPTR_SHADOW4_WAVES
 #define SPTR_SHADOW4_WAVES 7  // BVH4 from L2/HBM with 64-B nodes: C5 shadow 7.85 -> 7.44 ms/step (r02 ab2;
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
 
 namespace sptr {
+thread_local LaunchTiming g_launch_timing;  // (sptr_internal.h)
 // Any-hit wide walks visit the farthest hit child first: a ray leaving a surface has no occluder among
 // the boxes around its origin, so the near-first order explores them before the far occluder (r03b A/B:
 // C5 shadow 4.42 -> 3.88 ms/step, C3 0.81 -> 0.80).  The any-hit BVH2 walk of LDS scenes stays
@@ -2296,7 +2310,11 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
   const Staged sc = stage_scene<true>(sv, lds);
   uint32_t per_in = 0u;
   const uint32_t n = seg_scan(w.segN, nseg_in, s_off, per_in);
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&w.tot[kTotClosest], (unsigned long long)(n));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)(n));
+    atomicAdd(&w.tot[kTotTracedF], (unsigned long long)(n));
+    atomicAdd(&w.tot[kTotTracedD + stat_depth(depth)], (unsigned long long)(n));
+  }
   const RayStream rin = w.rs[depth & 1], rout = w.rs[(depth + 1) & 1];
   const bool last = (uint32_t)(depth + 1) >= f.max_depth;
   Visits vc;
@@ -3678,7 +3696,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
               return 0u;  // not instantiated: the high-occupancy form is for LDS-staged BVH2 scenes
             } else {
               const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube, Hi>, lb);
-              hipLaunchKernelGGL((k_trace_wp<Lc, C, Wc, Cube, Hi>), dim3(g), b, lb, s, sv, ev, f, w);
+              SPTR_TIMED_LAUNCH((k_trace_wp<Lc, C, Wc, Cube, Hi>), dim3(g), b, lb, s, sv, ev, f, w);
               return g;
             }
           }(fl);
@@ -3690,7 +3708,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         [&](auto fl) -> unsigned {
           return [&]<bool C, bool Wc, bool Cube>(Flags<C, Wc, Cube>) {
             const unsigned g = resident_grid((const void*)&k_trace_pm<C, Wc, Cube>, lb);
-            hipLaunchKernelGGL((k_trace_pm<C, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w);
+            SPTR_TIMED_LAUNCH((k_trace_pm<C, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w);
             return g;
           }(fl);
         },
@@ -3704,7 +3722,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
         [&](auto fl) -> unsigned {
           return [&]<bool C, bool Pc, bool Cube, bool Q>(Flags<C, Pc, Cube, Q>) {
             const unsigned g = resident_grid((const void*)&k_trace_dyn<false, C, Pc, true, Cube, Q>, lbd);
-            hipLaunchKernelGGL((k_trace_dyn<false, C, Pc, true, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
+            SPTR_TIMED_LAUNCH((k_trace_dyn<false, C, Pc, true, Cube, Q>), dim3(g), b, lbd, s, sv, ev, f, w, depth, nseg);
             return g;
           }(fl);
         },
@@ -3714,7 +3732,7 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
       [&](auto fl) -> unsigned {
         return [&]<bool Lc, bool C, bool Pc, bool Wc, bool Cube>(Flags<Lc, C, Pc, Wc, Cube>) {
           const unsigned g = resident_grid((const void*)&k_trace<Lc, C, Pc, Wc, Cube>, lb);
-          hipLaunchKernelGGL((k_trace<Lc, C, Pc, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
+          SPTR_TIMED_LAUNCH((k_trace<Lc, C, Pc, Wc, Cube>), dim3(g), b, lb, s, sv, ev, f, w, depth, nseg);
           return g;
         }(fl);
       },
@@ -3763,10 +3781,10 @@ unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView
   unsigned g;
   if (sh.env.env != nullptr) {
     g = resident_grid((const void*)&k_bounce<true>, lb);
-    hipLaunchKernelGGL(k_bounce<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+    SPTR_TIMED_LAUNCH(k_bounce<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
   } else {
     g = resident_grid((const void*)&k_bounce<false>, lb);
-    hipLaunchKernelGGL(k_bounce<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+    SPTR_TIMED_LAUNCH(k_bounce<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
   }
   return g;
 }
@@ -3786,7 +3804,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
         [&](auto fl) -> unsigned {
           return [&]<bool C, bool Q>(Flags<C, Q>) {
             const unsigned gq = resident_grid((const void*)&k_shadow_dyn<C, Q>, lbd);
-            hipLaunchKernelGGL((k_shadow_dyn<C, Q>), dim3(gq), b, lbd, s, sv, sh, w, depth, nseg);
+            SPTR_TIMED_LAUNCH((k_shadow_dyn<C, Q>), dim3(gq), b, lbd, s, sv, sh, w, depth, nseg);
             return gq;
           }(fl);
         },
@@ -3795,7 +3813,7 @@ unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView&
 #define SPTR_SHADOW(Lc, C, Wc)                                                                      \
   do {                                                                                              \
     g = resident_grid((const void*)&k_shadow<Lc, C, Wc>, lb);                                       \
-    hipLaunchKernelGGL((k_shadow<Lc, C, Wc>), dim3(g), b, lb, s, sv, sh, w, depth, nseg);           \
+    SPTR_TIMED_LAUNCH((k_shadow<Lc, C, Wc>), dim3(g), b, lb, s, sv, sh, w, depth, nseg);           \
   } while (0)
 #define SPTR_SHADOW_W(Lc, C) \
   do {                       \

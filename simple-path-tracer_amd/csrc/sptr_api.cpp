@@ -270,10 +270,11 @@ ShadeView shade_view(const Context& c) {
 }
 
 // Stage events on the render stream, kept in the context's pool until collected.  Stages: 0 whole
-// render call (always recorded), 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum +
-// resolve, 5 trace bounce 0 (raygen fused), 6 shade bounce 0, 7 tail, 8 pixel cull; 1-8 only with
-// SPTR_FRAME_TIMING (1, 3, 5 and 8 also with SPTR_FRAME_TIMING_TRACE).
-constexpr int kStages = 9;
+// render call, 1 trace (bounce >= 1), 2 shade (>= 1), 3 shadow, 4 accum + resolve, 5 trace bounce 0
+// (raygen fused), 6 shade bounce 0, 7 tail, 8 pixel cull, 9 fused bounce (k_bounce: the trace and the
+// shading of a bounce in one launch, counted with the trace launches); 0-9 with SPTR_FRAME_TIMING,
+// 1, 3, 5 and 9 with SPTR_FRAME_TIMING_TRACE.
+constexpr int kStages = 10;
 struct StageTimer {
   Context& c;
   bool on;                  // SPTR_FRAME_TIMING or SPTR_FRAME_TIMING_TRACE
@@ -307,15 +308,36 @@ struct StageTimer {
     }
     return i;
   }
+  // the stages that are exactly one launch: timed by the launch itself (g_launch_timing), the others
+  // by events recorded on s around them (an event record between two launches idles the GPU for
+  // ~5-10 us: r05 8-way C2 shard, 6 records per step -> 2 without the cull and call spans)
+  static bool one_launch(int stage) { return stage == 1 || stage == 5 || stage == 9 || stage == 3; }
+  bool launch_timed = false;
   void begin(int stage) {
-    // (an event record between two launches idles the GPU for ~5-10 us: r05 8-way C2 shard, 6 records per
-    // step -> 2 without the cull and call spans)
-    if (!on || capturing || (trace_only && stage != 1 && stage != 5 && stage != 3)) return;
+    if (!on || capturing || (trace_only && !one_launch(stage))) return;
+    if (one_launch(stage)) {
+      const size_t b = alloc(), e = alloc();
+      if (b == SIZE_MAX || e == SIZE_MAX) return;
+      open = c.marks.size();
+      c.marks.push_back(StageMark{stage, b, e});
+      g_launch_timing = LaunchTiming{c.events[b], c.events[e]};
+      launch_timed = true;
+      return;
+    }
     open = c.marks.size();
     c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
   void end() {
     if (open == SIZE_MAX) return;
+    if (launch_timed) {
+      launch_timed = false;
+      if (g_launch_timing.start) {  // nothing was launched: no events recorded, no mark
+        g_launch_timing = LaunchTiming{};
+        c.marks.erase(c.marks.begin() + (std::ptrdiff_t)open);
+      }
+      open = SIZE_MAX;
+      return;
+    }
     c.marks[open].e = next();
     open = SIZE_MAX;
   }
@@ -341,7 +363,7 @@ double trace_busy_ms(Context* const* cs, int n) {
     if (c.pending == 0) continue;
     if (hipStreamSynchronize(c.pending_stream) != hipSuccess) return 0.0;
     for (const StageMark& m : c.marks) {
-      if ((m.stage != 1 && m.stage != 5) || m.b >= c.events.size() || m.e >= c.events.size()) continue;
+      if ((m.stage != 1 && m.stage != 5 && m.stage != 9) || m.b >= c.events.size() || m.e >= c.events.size()) continue;
       if (!ref) ref = c.events[m.b];
       float b = 0.0f, e = 0.0f;
       if (hipEventElapsedTime(&b, ref, c.events[m.b]) != hipSuccess ||
@@ -374,14 +396,14 @@ int collect_pending(Context& c, sptr_stats* stats) {
   const hipError_t se = hipStreamSynchronize(c.pending_stream);
   Context* self = &c;
   const double busy = se == hipSuccess && stats ? trace_busy_ms(&self, 1) : 0.0;
-  double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t trace_launches = 0, shadow_launches = 0;
   for (const StageMark& m : c.marks) {
     float t = 0.0f;
     if (se == hipSuccess && m.b < c.events.size() && m.e < c.events.size())
       (void)hipEventElapsedTime(&t, c.events[m.b], c.events[m.e]);
     ms[m.stage] += t;
-    if (m.stage == 1 || m.stage == 5) ++trace_launches;
+    if (m.stage == 1 || m.stage == 5 || m.stage == 9) ++trace_launches;
     if (m.stage == 3) ++shadow_launches;
   }
   c.marks.clear();
@@ -397,7 +419,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   if (!stats) return SPTR_OK;
   stats->ms_total = ms[0];
   stats->ms_raygen = 0.0;  // raygen is fused into the bounce-0 trace (ms_trace0)
-  stats->ms_trace = ms[1] + ms[5];
+  stats->ms_trace = ms[1] + ms[5] + ms[9];
   stats->ms_shade = ms[2] + ms[6];
   stats->ms_trace0 = ms[5];
   stats->ms_shade0 = ms[6];
@@ -436,6 +458,7 @@ int collect_pending(Context& c, sptr_stats* stats) {
   for (int i = 0; i < 3; ++i) stats->strag_visits[i] = tot[kTotStragNodes + i];
   stats->cull_launches = culls;
   stats->ms_trace_busy = busy;
+  stats->traced_fused = tot[kTotTracedF];
   return SPTR_OK;
 }
 
@@ -692,7 +715,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
         WaveView wf = w;
         wf.segN = rays_tab;
         wf.segH = spare_tab;
-        tm.begin(2);
+        tm.begin(9);  // (a trace launch that also shades: ms_trace, trace_launches)
         g_shade = launch_bounce(sv, sh, fv, wf, d, g_shade, s);
         tm.end();
         std::swap(rays_tab, spare_tab);
@@ -1936,6 +1959,7 @@ static void add_stats(sptr_stats& a, const sptr_stats& b) {
   a.hits_bounce += b.hits_bounce;
   a.paths_handed_off += b.paths_handed_off;
   for (int i = 0; i < 3; ++i) a.strag_visits[i] += b.strag_visits[i];
+  a.traced_fused += b.traced_fused;
   a.ms_total = total;
   a.ms_trace_busy = std::max(a.ms_trace_busy, b.ms_trace_busy);  // (the callers set the union)
 }

@@ -217,12 +217,13 @@ enum : int {
   kTotHitB,                          // closest hits found by the later trace kernels (COUNT_VISITS)
   kTotStrag,                         // paths k_trace_dyn handed off to k_strag
   kTotStragNodes, kTotStragTris, kTotStragSph,  // the handed-off walks' visits made by k_strag (every call)
+  kTotTracedF,                       // queued rays of bounces >= 1 traced by the fused k_bounce (every call)
   kTotWords
 };
 
 constexpr int kStatDepths = 8;  // per-bounce statistics: bounces 0..6, and 7 = every later one
 constexpr int kHistBins = 16;   // per-ray visit histograms: bin b holds 2^(b-1) <= visits < 2^b (bin 0: none)
-static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 6, "totals layout");
+static_assert(kTotWords == kTotTracedD + 8 + 8 + 16 + 16 + 7, "totals layout");
 
 // Segment table of one block-segmented queue: producer block b wrote cnt[b] records at slots
 // [b*per*mult, ...) where per (written by producer block 0) is the producer's input slice size.
@@ -305,6 +306,15 @@ struct StageMark {
   int stage;
   size_t b, e;  // begin / end event indices in Context::events
 };
+
+// Events the next trace, fused-bounce or shadow launch of this thread records its own start and end
+// into (hipExtLaunchKernelGGL: the timestamps of the dispatch itself, so no marker packet sits between
+// two launches — a hipEventRecord there idled the GPU for 5-10 us).  Set by the stage timer right
+// before the launch, taken (and cleared) by SPTR_TIMED_LAUNCH.
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchTiming g_launch_timing;
 
 // Launch-graph cache of one render-call shape (sptr_api.cpp run_graph).  The key is every input of
 // the call's launch sequence except the per-call device words (FrameView::dyn): the state epoch (bumped

@@ -89,7 +89,7 @@ class Stats(C.Structure):
                 ("traced_by_depth", C.c_uint64 * 8), ("nodes_by_depth", C.c_uint64 * 8),
                 ("trace_visit_hist", C.c_uint64 * 16), ("shadow_visit_hist", C.c_uint64 * 16),
                 ("hits_primary", C.c_uint64), ("hits_bounce", C.c_uint64), ("paths_handed_off", C.c_uint64), ("strag_visits", C.c_uint64 * 3),
-                ("ms_trace_busy", C.c_double)]
+                ("ms_trace_busy", C.c_double), ("traced_fused", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: (list(v) if isinstance(v, C.Array) else v) for k, v in ((k, getattr(self, k)) for k, _ in self._fields_)}

@@ -912,3 +912,18 @@ def test_pixel_lanes_graph_replay(renderer):
     assert two[2] >= 1 and two[3] == 1, "the lane call shape was not captured"
     assert np.array_equal(one[0].view(np.uint32), two[0].view(np.uint32))
     assert np.array_equal(one[1], two[1])
+
+
+@pytest.mark.gpu
+def test_ray_accounting_fused_bounces(renderer):
+    """Every closest-hit query is a camera ray (one per sample, culled or not), a bounce ray of a trace
+    launch (traced_bounce), of a fused bounce launch (traced_fused: k_bounce) or of the path-per-thread
+    tail (rays_tail); the per-bounce counts cover the traversed ones."""
+    W, H = 320, 200
+    sptr.setup_default(renderer, "default_emitter")
+    cam = sptr.camera_lookat(aspect=W / H)
+    st = renderer.render(cam, W, H, spp=8, flags=sptr.SPTR_FRAME_TIMING_TRACE)
+    assert st.traced_fused > 0, "the small LDS-scene call is expected to fuse its bounces"
+    assert st.rays_closest == st.samples + st.traced_bounce + st.traced_fused + st.rays_tail
+    assert sum(st.traced_by_depth) == st.traced_primary + st.traced_bounce + st.traced_fused
+    assert st.trace_launches > 1 and st.ms_trace > 0

@@ -40,8 +40,9 @@ for wl in "$@"; do
   done
   python3 tools/prof_summary.py "$out/stats_$wl" "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" > "$out/summary_$wl.txt"
   for k in trace shadow; do
+    kn=k_$k; [ $k = trace ] && kn=k_trace,k_bounce  # (the fused bounce launches count as trace launches)
     python3 tools/prof_summary.py "$out/pmc_FETCH_SIZE_$wl" "$out/pmc_WRITE_SIZE_$wl" --emit "$out/pmc_${wl}_$k.json" \
-      --kernel k_$k --workload "$wl" > /dev/null
+      --kernel $kn --workload "$wl" > /dev/null
     cp "$out/pmc_${wl}_$k.json" "profiles/${tag}_pmc_${wl}_$k.json"
   done
   if [ $sq = 1 ]; then
@@ -51,7 +52,8 @@ for wl in "$@"; do
       python3 bench.py --workload "$wl" --steps 1 --warmup 0 --no-cpu-baseline --no-interactive > "$out/pmc_SQ_$wl.log" 2>&1
     python3 tools/prof_summary.py "$out/pmc_SQ_$wl" > "$out/sq_$wl.txt"
     for k in trace shadow; do
-      python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_$k.json" --kernel k_$k --workload "$wl" > /dev/null
+      kn=k_$k; [ $k = trace ] && kn=k_trace,k_bounce
+      python3 tools/prof_summary.py "$out/pmc_SQ_$wl" --emit "$out/sq_${wl}_$k.json" --kernel $kn --workload "$wl" > /dev/null
       cp "$out/sq_${wl}_$k.json" "profiles/${tag}_sq_${wl}_$k.json"
     done
   fi

@@ -2,7 +2,8 @@
 """Summarise rocprofv3 CSV output: per-kernel launch stats and PMC counters (per dispatch mean).
 
 usage: prof_summary.py <rocprof output dir> [...] [--emit OUT.json --kernel k_trace --workload c2]
---emit writes the per-launch HBM bytes of every dispatch whose name contains --kernel (all template
+--emit writes the per-launch HBM bytes of every dispatch whose name contains --kernel (a comma list:
+any of them; all template
 instantiations pooled), combining FETCH_SIZE and WRITE_SIZE from separate --pmc passes, for bench.py's
 roofline.traffic.
 FETCH_SIZE is reported doubled (gfx950 counts 128-B requests as 64 B for wide streams:
@@ -49,7 +50,7 @@ def emit(dirs, kernel, out_path, workload):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             vals = collections.defaultdict(float)
             for r in csv.DictReader(open(f)):
-                if kernel in r["Kernel_Name"] and not _is_count_variant(r["Kernel_Name"]):
+                if any(k in r["Kernel_Name"] for k in kernel.split(",")) and not _is_count_variant(r["Kernel_Name"]):
                     vals[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
                     if r["Counter_Name"] == "SQ_INSTS_VALU":
                         dur.append((r["Dispatch_Id"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))

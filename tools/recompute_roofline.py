@@ -21,34 +21,30 @@ import re
 import sys
 
 # position of the kCount template argument per kernel
-COUNT_ARG = {"k_trace_pm": 0, "k_trace": 1, "k_trace_wp": 1, "k_trace_dyn": 1, "k_shadow": 1, "k_shadow_dyn": 0}
-
-
-def pooled(rows, family):
-    calls, total = 0, 0.0
-    for r in rows:
-        m = re.search(r"sptr::(k_\w+)<([^>]*)>", r["Name"])
-        if not m or m.group(1) not in COUNT_ARG or not m.group(1).startswith(family):
-            continue
-        if family == "k_trace" and m.group(1).startswith("k_shadow"):
-            continue
-        args = [a.strip() for a in m.group(2).split(",")]
-        if args[COUNT_ARG[m.group(1)]] != "false":  # the instrumented (visit-count) pass
-            continue
-        calls += int(r["Calls"])
-        total += float(r["TotalDurationNs"])
-    return (total / calls * 1e-3, calls) if calls else (None, 0)
+COUNT_ARG = {"k_trace_pm": 0, "k_trace": 1, "k_trace_wp": 1, "k_trace_dyn": 1, "k_shadow": 1, "k_shadow_dyn": 0,
+             "k_bounce": None}  # (k_bounce: no count instantiation; the visit-count pass runs no fused bounce)
+FAMILY = {"k_trace": ("k_trace", "k_bounce"), "k_shadow": ("k_shadow",)}
 
 
 def _timed(name, family):
     """The timed-path (kCount = false) instantiation of a kernel of `family`, by its demangled name."""
     m = re.search(r"sptr::(k_\w+)<([^>]*)>", name)
-    if not m or m.group(1) not in COUNT_ARG or not m.group(1).startswith(family):
+    if not m or m.group(1) not in COUNT_ARG or not m.group(1).startswith(FAMILY[family]):
         return False
-    if family == "k_trace" and m.group(1).startswith("k_shadow"):
-        return False
+    pos = COUNT_ARG[m.group(1)]
+    if pos is None:
+        return True
     args = [a.strip() for a in m.group(2).split(",")]
-    return args[COUNT_ARG[m.group(1)]] == "false"
+    return args[pos] == "false"  # (true: the instrumented visit-count pass)
+
+
+def pooled(rows, family):
+    calls, total = 0, 0.0
+    for r in rows:
+        if _timed(r["Name"], family):
+            calls += int(r["Calls"])
+            total += float(r["TotalDurationNs"])
+    return (total / calls * 1e-3, calls) if calls else (None, 0)
 
 
 def busy_per_launch(trace_rows, family="k_trace"):
