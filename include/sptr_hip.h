@@ -258,8 +258,10 @@ int sptr_set_launch_mode(sptr_ctx* ctx, uint32_t mode);
 /* Pixel lanes (ABI 8): 2 = a wavefront call renders the even and the odd half of its shard's tiles as
  * two launch chains on two streams of the same GPU, each with its own buffers (the context holds a
  * second, internal context with a copy of the scene), so that each chain's launch tails run beside the
- * other's work; 1 = one chain; 0 (default) = two lanes for calls of >= 2^24 samples on scenes staged into
- * LDS, one chain otherwise.  An accumulation keeps the lane mode of its first call (frame_begin 1).
+ * other's work; 1 = one chain; 0 (default) = two lanes for calls of >= 2^24 samples, one chain otherwise.
+ * Only scenes staged into LDS (sptr_scene_layout_info: lds_bytes > 0) and the wavefront integrator run
+ * in two lanes; other calls run as one chain whatever the setting.  An accumulation keeps the lane mode
+ * of its first call (frame_begin 1); a change of setting or scene starts a new one.
  * Results are identical either way (each pixel's samples are the same operations in the same order);
  * sptr_tiles_device, sptr_read_rgb8 and sptr_read_accum return the shard as one chain would. */
 int sptr_set_pixel_lanes(sptr_ctx* ctx, uint32_t lanes);

@@ -1861,6 +1861,7 @@ static int lane_forward(sptr_ctx* x, int rc_lane) {
 int sptr_upload_scene(sptr_ctx* x, const sptr_scene* s) {
   const int rc = upload_scene_one(x, s);
   if (rc != SPTR_OK) return rc;
+  if (x->split) x->c.W = 0;  // the pixel buffers describe the even lane: re-laid out for the next call
   x->split = false;
   x->lane_scene = false;
   // the lane gets a copy only of scenes staged into LDS (small by construction): the two chains of a
@@ -1890,6 +1891,7 @@ int sptr_set_pixel_lanes(sptr_ctx* x, uint32_t lanes) {
   if (sync_pending(x->c) != SPTR_OK) return SPTR_ERR_HIP;
   if (x->lane && sync_pending(x->lane->c) != SPTR_OK) return SPTR_ERR_HIP;
   x->lanes_req = lanes;
+  if (x->split) x->c.W = 0;  // (as in sptr_upload_scene)
   x->split = false;  // the next call starts an accumulation of its own (frame_begin 1)
   x->c.last_samples = 0;
   return SPTR_OK;

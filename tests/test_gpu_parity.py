@@ -927,3 +927,28 @@ def test_ray_accounting_fused_bounces(renderer):
     assert st.rays_closest == st.samples + st.traced_bounce + st.traced_fused + st.rays_tail
     assert sum(st.traced_by_depth) == st.traced_primary + st.traced_bounce + st.traced_fused
     assert st.trace_launches > 1 and st.ms_trace > 0
+
+
+@pytest.mark.gpu
+def test_pixel_lanes_scene_changes(renderer):
+    """Two lanes apply to scenes staged into LDS only (a 40 000-triangle mesh renders as one chain even
+    when two lanes are asked for), and a scene upload in the middle of a two-lane accumulation starts
+    the next one afresh: the default scene rendered again after the mesh equals its first render."""
+    W, H = 320, 200
+    cam = sptr.camera_lookat(aspect=W / H)
+    try:
+        renderer.set_pixel_lanes(2)
+        sptr.setup_default(renderer, "default_emitter")
+        renderer.render(cam, W, H, spp=4)
+        assert renderer.pixel_lanes_info()["active"]
+        first = renderer.read_accum().copy()
+        sptr.setup_default(renderer, "sphere_mesh", 100, 200)
+        assert renderer.scene_layout()["lds_bytes"] == 0
+        renderer.render(cam, W, H, spp=4)
+        assert not renderer.pixel_lanes_info()["active"]
+        sptr.setup_default(renderer, "default_emitter")
+        renderer.render(cam, W, H, spp=4)
+        assert renderer.pixel_lanes_info()["active"]
+        assert np.array_equal(first.view(np.uint32), renderer.read_accum().view(np.uint32))
+    finally:
+        renderer.set_pixel_lanes(0)
