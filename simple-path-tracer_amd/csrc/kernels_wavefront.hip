@@ -78,7 +78,15 @@
 #endif                        // 5 -> 6 waves was 8.34 -> 7.19 with 128-B nodes)
 
 namespace sptr {
-thread_local LaunchTiming g_launch_timing;  // (sptr_internal.h)
+thread_local LaunchTiming g_launch_timing;
+thread_local unsigned long long* g_tslot = nullptr;
+// w with the timing slot the stage timer set for this launch (taken: the next launch is untimed)
+WaveView with_tslot(const WaveView& w) {
+  WaveView t = w;
+  t.tslot = g_tslot;
+  g_tslot = nullptr;
+  return t;
+}  // (sptr_internal.h)
 // Any-hit wide walks visit the farthest hit child first: a ray leaving a surface has no occluder among
 // the boxes around its origin, so the near-first order explores them before the far occluder (r03b A/B:
 // C5 shadow 4.42 -> 3.88 ms/step, C3 0.81 -> 0.80).  The any-hit BVH2 walk of LDS scenes stays
@@ -1388,6 +1396,29 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
   return (kD * diffuse + spec) * NdotL;
 }
 
+// --------------------------------------------------------------------------------- launch timing
+// A slot-timed launch (WaveView::tslot set by the stage timer: one launch chain) leaves the device's
+// constant-rate wall clock (wall_clock64, 100 MHz) in its slot: block 0, the first dispatched, stores
+// its start in word 0, and every block's thread 0, once the block is done, takes the maximum of its end
+// into one of kTimeEndLines words on lines of their own (atomicMax on a zeroed slot).  No packet sits
+// between the launch and its neighbours: the 8-way C2 shard 0.541-0.544 ms with dispatch events,
+// 0.525-0.532 with slots (r05zzj).  One shared end word made it 0.71 ms (thousands of atomics on one
+// address); every wave's end on 64 words 0.541-0.543.  The kernels have no early return: every thread
+// reaches ktime_end's barrier.  The two kernels of the pixel lanes' chains (k_trace_wp, k_bounce) carry
+// it only in their kTimed instantiation: the slot pointer held across them cost spills, and the
+// end-of-block barrier keeps a block's wave slots until its last wave is done, which the other lane
+// would fill (two-lane C2 2.61-2.66 ms with it compiled in, 2.55-2.61 without; the lanes' launches are
+// timed by dispatch events, Context::time_by_events).
+__device__ __forceinline__ void ktime_begin(const WaveView& w) {
+  if (w.tslot && blockIdx.x == 0 && threadIdx.x == 0) w.tslot[0] = (unsigned long long)wall_clock64();
+}
+__device__ __forceinline__ void ktime_end(const WaveView& w) {
+  if (!w.tslot) return;  // (uniform: a kernel argument)
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(w.tslot + kTimeLineWords * (1u + (blockIdx.x & (kTimeEndLines - 1u))), (unsigned long long)wall_clock64());
+}
+
 // --------------------------------------------------------------------------------- k_trace
 // Bounce 0, pixel-major (f.pixel_major == kFoldThread: LDS-staged scenes, where every primary ray
 // costs about the same, in batches with >= kPixelMajorItems pixels per resident thread): thread <-
@@ -1404,6 +1435,7 @@ __device__ __forceinline__ vec3 eval_brdf(const DevMaterial& m, vec3 N, vec3 V, 
 template <bool kCount, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_PM_WAVES)
     k_trace_pm(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
+  ktime_begin(w);
   const FrameView f = frame_dyn(fin);
   __shared__ LdsStack s_stack;
   extern __shared__ float4 lds[];
@@ -1481,6 +1513,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
     flush_depth_nodes(vc, w.tot, 0);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
+  ktime_end(w);
 }
 
 // Bounce 0, lane groups per pixel (f.pixel_major == kFoldWave: LDS-staged scenes in batches of >=
@@ -1496,9 +1529,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
 // kHiOcc: 8 waves/SIMD for shards whose pixels fill the resident waves only a few times (r04u: the
 // 8-way C2 shard 0.554 -> 0.541 ms, while 2- and 4-way shards lose ~1.5 % at 8 waves)
-template <bool kLds, bool kCount, bool kW4, bool kCube, bool kHiOcc = false>
+template <bool kLds, bool kCount, bool kW4, bool kCube, bool kHiOcc = false, bool kTimed = false>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 : SPTR_TRACE_WP_WAVES))
     k_trace_wp(SceneView sv, EnvView sh, FrameView fin, WaveView w) {
+  if constexpr (kTimed) ktime_begin(w);
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -1585,6 +1619,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
     flush_depth_nodes(vc, w.tot, 0);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
+  if constexpr (kTimed) ktime_end(w);
 }
 // Closest hit for every ray of this bounce.  A miss ends the path here: the environment term
 // (wf_pt_cpu.cpp:98-103) is added to rad[p] in place, so only hits go on to k_shade, as dense hit
@@ -1594,6 +1629,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
 template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  ktime_begin(w);
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -1686,6 +1722,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_depth_nodes(vc, w.tot, depth);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
+  ktime_end(w);
 }
 
 // BVH2 (LDS-staged) or wide walk over the staged / global scene pointers
@@ -1799,6 +1836,7 @@ __device__ __forceinline__ uint32_t xcd_take(XcdQueue& q, bool need, uint32_t* s
 template <bool kLds, bool kCount, bool kPrimary, bool kW4, bool kCube, bool kQueue>
 __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES : SPTR_TRACE_WAVES)
     k_trace_dyn(SceneView sv, EnvView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  ktime_begin(w);
   const FrameView f = frame_dyn(fin);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
@@ -1963,6 +2001,7 @@ __global__ void __launch_bounds__(kBlock, (kW4 && !kPrimary) ? SPTR_TRACE4_WAVES
     flush_depth_nodes(vc, w.tot, depth);
     hist_flush(s_hist, w.tot, kTotHistT);
   }
+  ktime_end(w);
 }
 
 // --------------------------------------------------------------------------------- shading steps
@@ -2296,9 +2335,10 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADE_WAVES)
 // order of the radiance updates of the two kernels — so no hit-record stream and one launch less
 // per bounce.  Input: the rays of w.segN / rs[d & 1]; output: the continuation rays in this
 // block's segment of w.segH / rs[(d + 1) & 1] (the host alternates the two tables between bounces).
-template <bool kCube>
+template <bool kCube, bool kTimed = false>
 __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
     k_bounce(SceneView sv, ShadeView sh, FrameView fin, WaveView w, int depth, uint32_t nseg_in) {
+  if constexpr (kTimed) ktime_begin(w);
   const FrameView f = frame_dyn(fin);
   extern __shared__ float4 lds[];
   uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + sv.lds_bytes / 16u);
@@ -2386,6 +2426,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
     w.bstat[blockIdx.x] += s_rays;
     if (blockIdx.x == 0) *w.segH.per = sd.per;
   }
+  if constexpr (kTimed) ktime_end(w);
 }
 
 // --------------------------------------------------------------------------------- k_shadow
@@ -2394,6 +2435,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
 // queries issued are tallied per block (bstat) and reduced by k_accum: no global atomics.
 template <bool kLds, bool kCount, bool kW4>
 __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW_WAVES) k_shadow(SceneView sv, ShadeView sh, WaveView w, int depth, uint32_t nseg_in) {
+  ktime_begin(w);
   __shared__ KernelStack<kLds> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays;
@@ -2446,6 +2488,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
     flush_visits(vc, w.tot, kTotShNodes);
     hist_flush(s_hist, w.tot, kTotHistS);
   }
+  ktime_end(w);
 }
 
 // k_shadow for wide BVHs traversed from L2/HBM with one light (C3, C5): the any-hit queries of the
@@ -2458,6 +2501,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_SHADOW4_WAVES : SPTR_SHADOW
 template <bool kCount, bool kQueue>
 __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(SceneView sv, ShadeView sh, WaveView w, int depth,
                                                                            uint32_t nseg_in) {
+  ktime_begin(w);
   __shared__ KernelStack<false> s_stack;
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_rays, s_next;
@@ -2542,6 +2586,7 @@ __global__ void __launch_bounds__(kBlock, SPTR_SHADOW4_WAVES) k_shadow_dyn(Scene
     flush_visits(vc, w.tot, kTotShNodes);
     hist_flush(s_hist, w.tot, kTotHistS);
   }
+  ktime_end(w);
 }
 
 // --------------------------------------------------------------------------------- k_tail
@@ -3676,8 +3721,9 @@ static unsigned dispatch(Fn&& fn, Flags<B...>, bool first, Rest... rest) {
 }
 
 
-unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w_in, int depth,
                       bool count, uint32_t nseg, hipStream_t s) {
+  const WaveView w = with_tslot(w_in);
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
   const bool P = depth == 0;
@@ -3695,6 +3741,11 @@ unsigned launch_trace(const SceneView& sv, const ShadeView& sh, const FrameView&
             if constexpr (Hi && (Wc || !Lc)) {
               return 0u;  // not instantiated: the high-occupancy form is for LDS-staged BVH2 scenes
             } else {
+              if (w.tslot) {
+                const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube, Hi, true>, lb);
+                SPTR_TIMED_LAUNCH((k_trace_wp<Lc, C, Wc, Cube, Hi, true>), dim3(g), b, lb, s, sv, ev, f, w);
+                return g;
+              }
               const unsigned g = resident_grid((const void*)&k_trace_wp<Lc, C, Wc, Cube, Hi>, lb);
               SPTR_TIMED_LAUNCH((k_trace_wp<Lc, C, Wc, Cube, Hi>), dim3(g), b, lb, s, sv, ev, f, w);
               return g;
@@ -3775,22 +3826,24 @@ void launch_cull(const SceneView& sv, const FrameView& f, uint32_t* mask, uint32
   hipLaunchKernelGGL(k_cull, dim3(f.P / kTilePixels), dim3(kBlock), 0, s, sv, f, mask, plist);
 }
 
-unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
+unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w_in, int depth,
                        uint32_t nseg, hipStream_t s) {
+  const WaveView w = with_tslot(w_in);
   const unsigned lb = sv.lds_bytes + (4u * (nseg + 1u) + 15u) / 16u * 16u;
-  unsigned g;
-  if (sh.env.env != nullptr) {
-    g = resident_grid((const void*)&k_bounce<true>, lb);
-    SPTR_TIMED_LAUNCH(k_bounce<true>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
-  } else {
-    g = resident_grid((const void*)&k_bounce<false>, lb);
-    SPTR_TIMED_LAUNCH(k_bounce<false>, dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
-  }
-  return g;
+  return dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Cube, bool T>(Flags<Cube, T>) {
+          const unsigned g = resident_grid((const void*)&k_bounce<Cube, T>, lb);
+          SPTR_TIMED_LAUNCH((k_bounce<Cube, T>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, sh.env.env != nullptr, w.tslot != nullptr);
 }
 
-unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w, int depth, bool count,
+unsigned launch_shadow(const SceneView& sv, const ShadeView& sh, const WaveView& w_in, int depth, bool count,
                        uint32_t nseg, hipStream_t s) {
+  const WaveView w = with_tslot(w_in);
   const dim3 b(kBlock);
   const bool L = sv.lds_bytes != 0;
   const bool W = sv.width == (uint32_t)kWide;

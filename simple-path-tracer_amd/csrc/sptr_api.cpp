@@ -315,12 +315,20 @@ struct StageTimer {
   bool launch_timed = false;
   void begin(int stage) {
     if (!on || capturing || (trace_only && !one_launch(stage))) return;
-    if (one_launch(stage)) {
+    if (one_launch(stage) && c.time_by_events) {  // timed by the dispatch's events (g_launch_timing)
       const size_t b = alloc(), e = alloc();
       if (b == SIZE_MAX || e == SIZE_MAX) return;
       open = c.marks.size();
       c.marks.push_back(StageMark{stage, b, e});
       g_launch_timing = LaunchTiming{c.events[b], c.events[e]};
+      launch_timed = true;
+      return;
+    }
+    if (one_launch(stage)) {  // timed by the kernel itself (g_tslot -> WaveView::tslot)
+      if (!c.tslots.p || c.tslots_used >= kTimeSlots) return;
+      open = c.marks.size();
+      c.marks.push_back(StageMark{stage, SIZE_MAX, SIZE_MAX, c.tslots_used});
+      g_tslot = static_cast<unsigned long long*>(c.tslots.p) + (size_t)kTimeSlotWords * c.tslots_used++;
       launch_timed = true;
       return;
     }
@@ -331,7 +339,9 @@ struct StageTimer {
     if (open == SIZE_MAX) return;
     if (launch_timed) {
       launch_timed = false;
-      if (g_launch_timing.start) {  // nothing was launched: no events recorded, no mark
+      if (g_tslot || g_launch_timing.start) {  // nothing was launched: nothing recorded, no mark
+        if (g_tslot) --c.tslots_used;
+        g_tslot = nullptr;
         g_launch_timing = LaunchTiming{};
         c.marks.erase(c.marks.begin() + (std::ptrdiff_t)open);
       }
@@ -351,40 +361,73 @@ struct StageTimer {
   }
 };
 
-// Busy time of the trace stage over the pending calls of contexts cs[0..n): the union of the trace
-// launches' intervals (stages 1 and 5), each placed on one clock by its events' offsets from the first
-// trace mark's begin event (two pixel lanes' trace launches run on two streams and overlap).  0 when a
-// stream or an event fails (collect_pending reports that failure).
-double trace_busy_ms(Context* const* cs, int n) {
-  std::vector<std::pair<float, float>> iv;
-  hipEvent_t ref = nullptr;
-  for (int k = 0; k < n; ++k) {
-    Context& c = *cs[k];
-    if (c.pending == 0) continue;
-    if (hipStreamSynchronize(c.pending_stream) != hipSuccess) return 0.0;
-    for (const StageMark& m : c.marks) {
-      if ((m.stage != 1 && m.stage != 5 && m.stage != 9) || m.b >= c.events.size() || m.e >= c.events.size()) continue;
-      if (!ref) ref = c.events[m.b];
-      float b = 0.0f, e = 0.0f;
-      if (hipEventElapsedTime(&b, ref, c.events[m.b]) != hipSuccess ||
-          hipEventElapsedTime(&e, ref, c.events[m.e]) != hipSuccess)
-        return 0.0;
-      iv.emplace_back(b, e);
-    }
+// The launch intervals [start, end] (device wall-clock ticks) of the context's slot-timed launches in
+// this collection window, by slot; {0, 0} for a slot whose launch left no time.
+std::vector<std::pair<uint64_t, uint64_t>> read_slots(Context& c) {
+  std::vector<std::pair<uint64_t, uint64_t>> iv(c.tslots_used, {0, 0});
+  if (c.tslots_used == 0) return iv;
+  std::vector<unsigned long long> w((size_t)kTimeSlotWords * c.tslots_used);
+  if (hipMemcpy(w.data(), c.tslots.p, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return iv;
+  for (uint32_t i = 0; i < c.tslots_used; ++i) {
+    const unsigned long long* sl = w.data() + (size_t)kTimeSlotWords * i;
+    uint64_t t1 = 0;
+    for (uint32_t j = 1; j <= kTimeEndLines; ++j) t1 = std::max<uint64_t>(t1, sl[kTimeLineWords * j]);
+    const uint64_t t0 = sl[0];
+    if (t0 != 0 && t1 >= t0) iv[i] = {t0, t1};
   }
+  return iv;
+}
+
+// Length of the union of intervals.
+template <typename T>
+double union_length(std::vector<std::pair<T, T>>& iv) {
+  if (iv.empty()) return 0.0;
   std::sort(iv.begin(), iv.end());
   double busy = 0.0;
-  float lo = 0.0f, hi = 0.0f;
-  for (size_t i = 0; i < iv.size(); ++i) {
-    if (i == 0 || iv[i].first > hi) {
-      busy += hi - lo;
+  T lo = iv[0].first, hi = iv[0].second;
+  for (size_t i = 1; i < iv.size(); ++i) {
+    if (iv[i].first > hi) {
+      busy += (double)(hi - lo);
       lo = iv[i].first;
       hi = iv[i].second;
     } else {
       hi = std::max(hi, iv[i].second);
     }
   }
-  return busy + (hi - lo);
+  return busy + (double)(hi - lo);
+}
+
+// Busy time of the trace stage over the pending calls of contexts cs[0..n): the union of the trace
+// launches' intervals (stages 1, 5 and 9).  Slot-timed launches are placed on the device's wall clock,
+// event-timed ones (the pixel lanes' calls) by their events' offsets from the first such event; both
+// clocks are shared by every stream and both lanes, whose trace launches overlap.  (A window holding
+// calls of both kinds adds the two unions: such calls run one after the other on the render stream.)
+// 0 when a stream fails (collect_pending reports that failure).
+double trace_busy_ms(Context* const* cs, int n) {
+  std::vector<std::pair<uint64_t, uint64_t>> iv;
+  std::vector<std::pair<float, float>> ev;
+  double khz = 0.0;
+  hipEvent_t ref = nullptr;
+  for (int k = 0; k < n; ++k) {
+    Context& c = *cs[k];
+    if (c.pending == 0) continue;
+    if (hipStreamSynchronize(c.pending_stream) != hipSuccess) return 0.0;
+    const auto sl = read_slots(c);
+    khz = c.wall_khz;
+    for (const StageMark& m : c.marks) {
+      if (m.stage != 1 && m.stage != 5 && m.stage != 9) continue;
+      if (m.slot != UINT32_MAX) {
+        if (m.slot < sl.size() && sl[m.slot].second) iv.push_back(sl[m.slot]);
+      } else if (m.b < c.events.size() && m.e < c.events.size()) {
+        if (!ref) ref = c.events[m.b];
+        float b = 0.0f, e = 0.0f;
+        if (hipEventElapsedTime(&b, ref, c.events[m.b]) == hipSuccess &&
+            hipEventElapsedTime(&e, ref, c.events[m.e]) == hipSuccess)
+          ev.emplace_back(b, e);
+      }
+    }
+  }
+  return (khz > 0.0 ? union_length(iv) / khz : 0.0) + union_length(ev);
 }
 
 // Wait for the pending render calls, fold their device counters and stage events into *stats
@@ -398,16 +441,24 @@ int collect_pending(Context& c, sptr_stats* stats) {
   const double busy = se == hipSuccess && stats ? trace_busy_ms(&self, 1) : 0.0;
   double ms[kStages] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t trace_launches = 0, shadow_launches = 0;
+  const auto slots = se == hipSuccess ? read_slots(c) : std::vector<std::pair<uint64_t, uint64_t>>();
   for (const StageMark& m : c.marks) {
     float t = 0.0f;
-    if (se == hipSuccess && m.b < c.events.size() && m.e < c.events.size())
+    if (m.slot != UINT32_MAX) {  // timed by the launch itself
+      if (m.slot < slots.size()) t = (float)((double)(slots[m.slot].second - slots[m.slot].first) / c.wall_khz);
+    } else if (se == hipSuccess && m.b < c.events.size() && m.e < c.events.size()) {
       (void)hipEventElapsedTime(&t, c.events[m.b], c.events[m.e]);
+    }
     ms[m.stage] += t;
     if (m.stage == 1 || m.stage == 5 || m.stage == 9) ++trace_launches;
     if (m.stage == 3) ++shadow_launches;
   }
   c.marks.clear();
   c.events_used = 0;
+  if (c.tslots_used) {  // the slots this window used, zeroed for the next one (the streams are idle)
+    if (se == hipSuccess) (void)hipMemset(c.tslots.p, 0, (size_t)c.tslots_used * kTimeSlotWords * 8);
+    c.tslots_used = 0;
+  }
   const uint64_t samples = c.pending_samples, waves = c.pending_waves, culls = c.pending_culls;
   c.pending = 0;
   c.pending_samples = c.pending_waves = c.pending_culls = 0;
@@ -1167,11 +1218,16 @@ static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
     delete x;
     return SPTR_ERR_HIP;
   }
+  int khz = 0;
   if (ensure_buf(c.wb.seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
-      ensure_buf(c.dyn, kDynBytes) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess) {
+      ensure_buf(c.dyn, kDynBytes) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess ||
+      ensure_buf(c.tslots, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
+      hipMemset(c.tslots.p, 0, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
     delete x;
     return SPTR_ERR_OOM;
   }
+  c.wall_khz = khz;
   *out = x;
   return SPTR_OK;
 }
@@ -1190,7 +1246,7 @@ int sptr_destroy(sptr_ctx* x) {
   if (c.stream) (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
                     &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
-                    &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist};
+                    &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist, &c.tslots};
   for (DevBuf* b : bufs) free_buf(*b);
   for (DevBuf* b : {&c.wb.hrec, &c.wb.rad, &c.wb.stask, &c.wb.seg, &c.wb.strag}) free_buf(*b);
   for (auto& r : c.wb.rs)
@@ -1976,6 +2032,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
       x->split = false;
       c.W = 0;  // the pixel buffers describe the even lane: re-laid out for the whole shard
     }
+    c.time_by_events = false;
     return render_one(x, f, stream, stats);
   }
   // two lanes: this context renders shard (R, 2G) — the even half of shard (R, G)'s tiles — and the
@@ -2006,6 +2063,7 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
     API_HIP(hipMemsetAsync(x->tiles_full.p, 0, (size_t)x->full_tiles * kTilePixels * 4, s));
   }
   x->split = true;
+  c.time_by_events = cy.time_by_events = true;  // (LaunchTiming, sptr_internal.h)
   // this context's pixel buffers first (the image both lanes resolve into is cleared on s before the fork)
   bool resized = false;
   int rc = ensure_pixels(c, f->width, f->height, 2 * G, R, s, resized);

@@ -288,6 +288,8 @@ struct WaveView {
   // traces that shadow ray before the path's next bounce, so shadow(carry_depth) no longer has to end
   // before the tail starts.  kNoHit: no carry.
   uint32_t carry_depth;
+  // launch timing (ktime_begin / ktime_end): this launch's slot of Context::tslots, or null (untimed)
+  unsigned long long* tslot = nullptr;
 };
 
 struct DevBuf {
@@ -304,8 +306,12 @@ struct WaveBufs {
 
 struct StageMark {
   int stage;
-  size_t b, e;  // begin / end event indices in Context::events
+  size_t b, e;                 // begin / end event indices in Context::events (stages timed by events)
+  uint32_t slot = UINT32_MAX;  // the launch's Context::tslots slot (one-chain launches timed by the kernel)
 };
+constexpr uint32_t kTimeSlots = 4096;  // slot-timed launches per collection window (the rest run untimed)
+// a slot: the start word, then kTimeEndLines end words, each on a 64-B line of its own (ktime_end)
+constexpr uint32_t kTimeLineWords = 8, kTimeEndLines = 16, kTimeSlotWords = kTimeLineWords * (1 + kTimeEndLines);
 
 // Events the next trace, fused-bounce or shadow launch of this thread records its own start and end
 // into (hipExtLaunchKernelGGL: the timestamps of the dispatch itself, so no marker packet sits between
@@ -315,6 +321,12 @@ struct LaunchTiming {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local LaunchTiming g_launch_timing;
+// Or the timing slot (Context::tslots) of the next such launch: set by the stage timer, taken by the
+// launcher (with_tslot) and filled by the kernel itself (ktime_begin / ktime_end: the device's wall
+// clock, and not even a dispatch event).  One launch chain is timed this way; the pixel lanes' calls by
+// dispatch events (Context::time_by_events), see kernels_wavefront.hip "launch timing".
+extern thread_local unsigned long long* g_tslot;
+WaveView with_tslot(const WaveView& w);
 
 // Launch-graph cache of one render-call shape (sptr_api.cpp run_graph).  The key is every input of
 // the call's launch sequence except the per-call device words (FrameView::dyn): the state epoch (bumped
@@ -362,6 +374,10 @@ struct Context {
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
+  DevBuf tslots;                     // [kTimeSlots][kTimeSlotWords] launch timing slots, zeroed
+  uint32_t tslots_used = 0;          // slots handed out in this collection window
+  double wall_khz = 0.0;             // the device wall clock's rate (wall_clock64 ticks per ms)
+  bool time_by_events = false;       // one-launch stages timed by dispatch events, not slots (pixel lanes)
   GraphCache graph;
   int32_t capture_status = 0;        // hipError_t of the last capture that fell back to direct launches (0: none)
   std::string capture_error;         // ... and the call that returned it
