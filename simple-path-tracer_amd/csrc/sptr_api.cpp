@@ -315,7 +315,11 @@ struct StageTimer {
   bool launch_timed = false;
   void begin(int stage) {
     if (!on || capturing || (trace_only && !one_launch(stage))) return;
-    if (one_launch(stage) && c.time_by_events) {  // timed by the dispatch's events (g_launch_timing)
+    // timed by the dispatch's events (g_launch_timing): the pixel lanes' launches, and the shadow launches,
+    // which run on a side stream beside the bounce traces and may wait there after their dispatch for
+    // the CUs: a slot's start (block 0 running) leaves that wait out, a dispatch event and rocprofv3's
+    // kernel trace count it (C5 r05i: shadow frac 0.48 from slots vs 0.29 from the kernel trace)
+    if (one_launch(stage) && (c.time_by_events || stage == 3)) {
       const size_t b = alloc(), e = alloc();
       if (b == SIZE_MAX || e == SIZE_MAX) return;
       open = c.marks.size();

@@ -58,10 +58,10 @@ for wl in "$@"; do
     done
   fi
   echo "[$(date +%T)] bench $wl"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
+  timeout -k 10 420 python3 bench.py --workload "$wl" $benchflags > "$out/bench_$wl.json" 2> "$out/bench_$wl.err"
   tail -1 "$out/bench_$wl.json"
   echo "[$(date +%T)] bench $wl --stage-timing"
-  timeout -k 10 420 python3 bench.py --workload "$wl" --steps 5 --warmup 1 --stage-timing --no-cpu-baseline --no-interactive \
+  timeout -k 10 420 python3 bench.py --workload "$wl" --stage-timing --no-cpu-baseline --no-interactive \
     > "$out/bench_${wl}_stages.json" 2> "$out/bench_${wl}_stages.err"
 done
 echo "[$(date +%T)] done"
