@@ -103,12 +103,16 @@ typedef struct sptr_camera {
 } sptr_camera;
 
 enum sptr_frame_flags {
-  SPTR_FRAME_TIMING = 1u,     /* record per-stage HIP events (adds sync at the end of the call) */
+  SPTR_FRAME_TIMING = 1u,     /* per-stage times (adds sync at the end of the call).  The trace, fused-bounce
+                                 and shadow launches time themselves (one launch chain's trace launches on
+                                 the device wall clock, up to 4096 per collection window — later ones in
+                                 the window go untimed; the shadow launches and the pixel lanes' launches
+                                 by their dispatch events); the other stages by HIP events around them */
   SPTR_FRAME_NO_RESOLVE = 2u, /* skip the tonemap/resolve pass */
   SPTR_FRAME_COUNT_VISITS = 4u, /* one instrumented trace pass: count BVH node / primitive fetches */
   SPTR_FRAME_ASYNC = 8u, /* enqueue only: return without waiting; stats are left zero and the call's
                             counters and stage times accumulate until sptr_collect_stats */
-  SPTR_FRAME_TIMING_TRACE = 16u, /* HIP events around the trace and shadow launches only (ms_trace,
+  SPTR_FRAME_TIMING_TRACE = 16u, /* the trace and shadow launches' times only (ms_trace,
                                    ms_trace0, trace_launches, ms_shadow, shadow_launches): the other
                                    stages run back to back, and ms_total / ms_cull stay 0 */
   SPTR_FRAME_NO_CULL = 32u, /* diagnostic: bounce 0 traverses every camera ray, without the pixel-frustum
