@@ -607,21 +607,24 @@ def main():
             r.unpack_tiles(tiles_in.data_ptr(), shards, tiles_per_rank, W, H, image.data_ptr(), stream=stream)
         if ev:
             ev[2].record()
+        return src
 
+    # The timed steps are the calls a default caller makes: no stage-timing flag, so the library launches
+    # them as it launches any render (launch mode 0: a captured graph where one replays faster, DESIGN.md
+    # §6).  Every timed step recomputes the bounce-0 cull mask (SPTR_FRAME_RECULL): it is a per-camera
+    # structure, and a renderer whose camera moves pays it every frame, so it is inside the timed step.
+    # (--stage-timing: events around every stage inside the timed steps, a timing study, not a headline.)
+    timed = sptr.SPTR_FRAME_RECULL | (sptr.SPTR_FRAME_TIMING if args.stage_timing else 0)
     for _ in range(args.warmup):
-        step()
+        step(timed)
     r.collect_stats()
     # untimed instrumented pass: BVH node / primitive fetch counts for the algorithmic-bytes model
     step(sptr.SPTR_FRAME_COUNT_VISITS)
     cnt = r.collect_stats()
-    # the timed call shape (its event flag differs from the warmup's) seen twice before timing.  Its
-    # stage events (the trace launches' durations for the roofline) make every timed call a direct
-    # launch sequence; graph_replay below times the same steps replayed from a launch graph.
-    # Every timed step recomputes the bounce-0 cull mask (SPTR_FRAME_RECULL): it is a per-camera
-    # structure, and a renderer whose camera moves pays it every frame, so it is inside the timed step.
-    timing = (sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE) | sptr.SPTR_FRAME_RECULL
+    # the timed call shape seen twice right before timing (a graph, where mode 0 captures one, is captured
+    # on the second call)
     for _ in range(2):
-        step(timing)
+        step(timed)
     r.collect_stats()
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
@@ -630,14 +633,50 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(timing, evs[i])
+        last_tiles = step(timed, evs[i])
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stats = [r.collect_stats()]  # the K timed steps' counters and stage events, summed
+    stats = [r.collect_stats()]  # the K timed steps' counters, summed
     render_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     gather_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+
+    # The last timed step's output against an untimed render of the same frame (default flags, the
+    # library's own stream, synchronous: the call shape tests/test_gpu_golden.py checks against the oracle):
+    # this rank's resolved tiles, and on one GPU the unpacked RGB8 image, byte for byte.
+    tiles_timed = last_tiles.clone()
+    image_timed = image.clone() if rank == 0 else None
+    torch.cuda.synchronize()
+    r.render(cam, W, H, spp=frames, max_depth=wl.max_depth, shard_rank=shard, shard_count=shards,
+             integrator=integ, samples_per_frame=4)
+    ref_ptr, ref_bytes = r.tiles_device()
+    ref_tiles = torch.as_tensor(_DevArray(ref_ptr, ref_bytes), device=dev)
+    n_cmp = min(ref_tiles.numel(), tiles_timed.numel())
+    tile_words_differing = int((ref_tiles[:n_cmp] != tiles_timed[:n_cmp]).sum().item()) + \
+        abs(ref_tiles.numel() - tiles_timed.numel())
+    image_bytes_differing = None
+    if rank == 0 and shards == 1:
+        ref_rgb = torch.from_numpy(r.read_rgb8().reshape(-1)).to(dev)
+        image_bytes_differing = int((ref_rgb != image_timed).sum().item())
+    output_check = {"reference": "untimed render of the same frame, default flags, synchronous",
+                    "identical": tile_words_differing == 0 and not image_bytes_differing,
+                    "tile_words_differing": tile_words_differing, "image_bytes_differing": image_bytes_differing}
+
+    # Launch durations for the roofline: an untimed pass of the same K steps in which the trace, fused-bounce
+    # and shadow launches time themselves (SPTR_FRAME_TIMING_TRACE; such calls always run as direct launches).
+    # Counts (rays, visits) are the same as the timed steps'; the durations are these launches' own.
+    timing = (sptr.SPTR_FRAME_TIMING if args.stage_timing else sptr.SPTR_FRAME_TIMING_TRACE) | sptr.SPTR_FRAME_RECULL
+    for _ in range(2):
+        step(timing)
+    r.collect_stats()
+    torch.cuda.synchronize()
+    tr0 = time.perf_counter()
+    for i in range(args.steps):
+        step(timing)
+    torch.cuda.synchronize()
+    rf_elapsed = time.perf_counter() - tr0
+    stats_rf = [r.collect_stats()]
 
     # one untimed step with events around every stage (the timed steps record them around the trace and
     # shadow launches only: each record between two launches idles the GPU for several microseconds)
@@ -727,7 +766,7 @@ def main():
         assert int(tsum[2]) == want, (int(tsum[2]), want)
 
     if rank == 0:
-        stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats) / args.steps, 3)
+        stage_ms = {k: round(sum(getattr(s, "ms_" + k) for s in stats_rf) / args.steps, 3)
                     for k in (("trace0", "trace", "shade0", "shade", "shadow", "tail", "accum", "cull")
                               if args.stage_timing else ("trace0", "trace", "shadow"))}
         knobs = {k: os.environ[k] for k in KNOB_VARS if os.environ.get(k)}
@@ -760,10 +799,14 @@ def main():
             "world_size": world,
             "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
-            "roofline": roofline(cnt, stats, layout, wl.name, args.steps, env_bytes=env_bytes),
-            "shadow_roofline": shadow_roofline(cnt, stats, layout, wl.name, args.steps),
+            "roofline": roofline(cnt, stats_rf, layout, wl.name, args.steps, env_bytes=env_bytes),
+            "shadow_roofline": shadow_roofline(cnt, stats_rf, layout, wl.name, args.steps),
+            # the launch durations above come from this untimed pass of the same steps
+            "roofline_pass": {"flags": "SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_RECULL (direct launches)",
+                              "ms_per_step": round(rf_elapsed / args.steps * 1e3, 3)},
+            "output_check": output_check,
             "overlap_probe": probe,
-            "stage_ms_per_step": stage_ms,
+            "stage_ms_per_step": stage_ms,  # (the roofline pass's)
             # all stages of one untimed step, events around each (stage spans overlap on L2/HBM scenes)
             "stage_ms_untimed_step": stage_full,
             "cull_ms": stage_full["cull"],

@@ -620,7 +620,7 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
   }
   return false;
 }
-// The same traversal with one fetch per lane per step (SPTR_WALK_UNIFIED): a step visits one item,
+// The same traversal with one fetch per lane per step (the unified walk): a step visits one item,
 // an internal node or a leaf.  A node's hit children — leaves included — are ordered like internal
 // children (the nearest is visited next, the others pushed), so a leaf's primitive is tested on a
 // step of its own.  Every lane issues its step's loads from one selected address (the node's 56 B,
@@ -634,16 +634,12 @@ __device__ __forceinline__ bool wide_walk_inl(WideWalk& wk, TravStack<N>& stack,
 // branchy step (walk_fetch + walk_apply) or as the branch-free step (walk_step_bf, r05).  The two
 // unified forms visit the same items in the same order (k_strag resumes either's state).
 enum : int { kWalkInline = 0, kWalkUnified = 1, kWalkBranchFree = 2 };
-#ifndef SPTR_WALK_BF
-#define SPTR_WALK_BF 1  // the unified walk's form: 1 branch-free, 0 r04's step (A/B builds)
-#endif
-#ifndef SPTR_BF_PRIMARY
-#define SPTR_BF_PRIMARY 0  // 1: camera rays (k_trace_dyn<primary>) take the branch-free form too (r05d A/B: C5
-                           // bounce-0 trace 1.57-1.59 vs 1.46 ms with the r04 step: coherent waves rarely split,
-                           // and the branch-free step runs both the node and the triangle test)
-#endif
-constexpr int kWalkU = SPTR_WALK_BF ? kWalkBranchFree : kWalkUnified;
-constexpr int kWalkPrimary = SPTR_BF_PRIMARY ? kWalkU : kWalkUnified;
+// The unified walk of every query except camera rays takes the branch-free step (r05: C5 SALU/VALU of the
+// shadow launches 0.65 -> 0.30).  Camera rays (k_trace_dyn<primary>) keep r04's step (r05d
+// A/B: C5 bounce-0 trace 1.57-1.59 ms with the branch-free step vs 1.46: coherent waves rarely split, and
+// the branch-free step runs both the node and the triangle test).
+constexpr int kWalkU = kWalkBranchFree;
+constexpr int kWalkPrimary = kWalkUnified;
 // the branch-free step reads every node from L2/HBM, so kernels stage the LDS top levels only for the others
 __host__ __device__ constexpr bool walk_reads_top(int kind) { return kind != kWalkBranchFree; }
 // One step of the unified walk: its fetch (the 56 B of the item wk.cur names: a wide node from the

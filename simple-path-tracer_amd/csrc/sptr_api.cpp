@@ -16,8 +16,10 @@
 
 #include "sptr_internal.h"
 
+#include <dlfcn.h>
 #include <execinfo.h>
 #include <csignal>
+#include <ucontext.h>
 #include <unistd.h>
 
 struct sptr_ctx {
@@ -66,6 +68,11 @@ void free_buf(DevBuf& b) {
   b.p = nullptr;
   b.bytes = 0;
 }
+
+// The context whose shading state (materials and their device table, the geomID -> material table,
+// lights, environment, debug mode) a render of c uses: a pixel lane reads its parent's (ADVICE r05:
+// a copy per lane put the HDR cubemap into HBM twice, also for scenes the lane never renders).
+inline const Context& shading(const Context& c) { return c.parent ? *c.parent : c; }
 
 // One wavefront batch holds up to 2^29 paths (160 B of path state each with one light: 86 GB, under
 // a third of the 288 GB of HBM).  Every batch pays the secondary bounces' latency floor once: their
@@ -165,7 +172,7 @@ int ensure_wave(Context& c, uint64_t cap, uint32_t L, uint32_t ts, uint32_t k_sl
 }
 
 uint32_t task_stride(const Context& c) {
-  for (const DevLight& l : c.lights_host)
+  for (const DevLight& l : shading(c).lights_host)
     if (l.type != 0) return 3u;
   return 2u;
 }
@@ -191,7 +198,7 @@ WaveView wave_view(Context& c) {
   w.bstat_closest = w.bstat + kMaxSegs;
   w.work = reinterpret_cast<uint32_t*>(w.bstat_closest + kMaxSegs);
   w.tot = static_cast<unsigned long long*>(c.w_tot.p);
-  w.L = (uint32_t)c.lights_host.size();
+  w.L = (uint32_t)shading(c).lights_host.size();
   w.tstride = task_stride(c);
   w.defer_miss = 0u;
   w.seg_cap = (uint32_t)(wb.cap + (uint64_t)kMaxSegs * kBlock);
@@ -253,7 +260,8 @@ FrameView frame_view(const Context& c, const sptr_frame& f) {
   return v;
 }
 
-ShadeView shade_view(const Context& c) {
+ShadeView shade_view(const Context& cc) {
+  const Context& c = shading(cc);
   ShadeView s{};
   s.mats = static_cast<const DevMaterial*>(c.mats.p);
   s.num_mats = (uint32_t)c.mats_host.size();
@@ -313,7 +321,13 @@ struct StageTimer {
   // ~5-10 us: r05 8-way C2 shard, 6 records per step -> 2 without the cull and call spans)
   static bool one_launch(int stage) { return stage == 1 || stage == 5 || stage == 9 || stage == 3; }
   bool launch_timed = false;
+  bool quiet = false, quiet_open = false;  // untimed launch with dispatch events (run_call)
   void begin(int stage) {
+    if (quiet && !on && !capturing && one_launch(stage)) {
+      g_launch_timing = LaunchTiming{c.quiet_ev[0], c.quiet_ev[1]};
+      quiet_open = true;
+      return;
+    }
     if (!on || capturing || (trace_only && !one_launch(stage))) return;
     // timed by the dispatch's events (g_launch_timing): the pixel lanes' launches, and the shadow launches,
     // which run on a side stream beside the bounce traces and may wait there after their dispatch for
@@ -340,6 +354,11 @@ struct StageTimer {
     c.marks.push_back(StageMark{stage, next(), SIZE_MAX});
   }
   void end() {
+    if (quiet_open) {
+      quiet_open = false;
+      g_launch_timing = LaunchTiming{};  // (taken by the launch; cleared if there was none)
+      return;
+    }
     if (open == SIZE_MAX) return;
     if (launch_timed) {
       launch_timed = false;
@@ -575,7 +594,7 @@ void optix_frame_params(const Context& c, const sptr_frame& f, FrameView& v) {
   v.ox_has_light = 0u;
   v.ox_light_dir = v3(0.0f, -1.0f, 0.0f);
   v.ox_light_rad = v3(0.0f, 0.0f, 0.0f);
-  for (const DevLight& l : c.lights_host)
+  for (const DevLight& l : shading(c).lights_host)
     if (l.type == 0) {  // DevLight keeps the direction TO the light
       v.ox_light_dir = -v3(l.v[0], l.v[1], l.v[2]);
       v.ox_light_rad = v3(l.radiance[0], l.radiance[1], l.radiance[2]);
@@ -987,11 +1006,18 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   // and 0.30/0.20; 800x600 0.33/0.21 vs 0.31/0.22; 1280x720 0.37-0.38/0.22 vs 0.35/0.24; 1920x1080 (whose
   // pixel-major bounce 0 forks nothing) 0.46/0.25 vs 0.41-0.42/0.23 — the replays' device time is at best
   // 10 us shorter and their wall time has spikes.  Calls from kGraphMinSamples on (C2: 2.98 vs 3.02 ms).
-  const bool graphable = c.launch_mode == 3 || (c.launch_mode == 0 && !c.last_forked && samples >= kGraphMinSamples);
+  // Nor the halves of a two-lane call (time_by_events marks them): the two lanes' graphs replayed beside
+  // each other measured slower than their direct launches (r05i, C2: 2.865 vs 2.528 ms per call).
+  const bool graphable = c.launch_mode == 3 ||
+                         (c.launch_mode == 0 && !c.last_forked && !c.time_by_events && samples >= kGraphMinSamples);
   const bool bad = c.have_bad_key && same_key(key, c.bad_key);  // this shape failed to capture before
   auto direct = [&]() -> int {
     c.last_forked = false;  // (set by the launch sequence if it forks)
     StageTimer tm{c, timing, trace_only, s};
+    // untimed two-lane calls launch their trace and fused-bounce kernels with dispatch events all the same
+    // (two events reused by every such launch, never read): r06l, C2 2.512-2.531 vs 2.548-2.565 ms per step
+    // with plain launches, on one box
+    tm.quiet = !timing && c.time_by_events && c.quiet_ev[1] != nullptr;
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
@@ -1001,6 +1027,16 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   if (!graphable || timing || bad || !(repeat || (c.graph.valid && same_key(key, c.graph.key)))) return direct();
   if (!(c.graph.valid && same_key(key, c.graph.key))) {  // capture this shape
     drop_graph(c);
+    // a pixel lane's capture stream is its own, created on its first capture (only launch mode 3 captures
+    // a lane's calls).  r06: with one capture stream shared by the two contexts, a parent's capture after
+    // the lane's (a mode-3 two-lane shape, then direct two-lane calls, then a one-chain shape captured in
+    // mode 0) was instantiated, and its first hipGraphLaunch faulted inside torch's HIP runtime (a null
+    // member read at libamdhip64+0xaee41, gpurun_out/r06e); with a stream per context it does not.
+    if (!c.cap_stream && hipStreamCreateWithFlags(&c.cap_stream, hipStreamNonBlocking) != hipSuccess) {
+      c.cap_stream = nullptr;
+      (void)hipGetLastError();
+      return direct();
+    }
     GraphShape gshape;
     // A shape that cannot be captured (the capture fails, leaves a forked stream capturing, or yields
     // a graph check_graph rejects or the runtime cannot instantiate) is remembered and launched
@@ -1119,6 +1155,8 @@ std::vector<hipEvent_t*> dep_events(Context& c) {
 bool create_events(Context& c) {
   for (hipEvent_t* e : dep_events(c))
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
+  for (hipEvent_t& e : c.quiet_ev)
+    if (hipEventCreate(&e) != hipSuccess) return false;
   return true;
 }
 }  // namespace
@@ -1133,11 +1171,52 @@ static void add_stats(sptr_stats& a, const sptr_stats& b);  // (pixel lanes, bel
 int sptr_abi_version(void) { return SPTR_ABI_VERSION; }
 
 
-// SPTR_SEGV_TRACE=1 (diagnostics only): a host SIGSEGV prints the native backtrace before the default
-// action.  Installed once per process, on the first sptr_create, for the thread that creates the
-// context (its alternate signal stack); the backtrace machinery is primed at install time, so the
-// handler's backtrace() call does not load anything.
-static void segv_trace(int sig) {
+// SPTR_SEGV_TRACE=1 (diagnostics only): a host SIGSEGV prints, before the default action, the fault
+// address, the faulting instruction and stack pointer, each code address among the 512 words above the
+// stack pointer as library + offset (a scan that needs no unwinder, so it works on an overflowed stack),
+// and then the unwinder's backtrace.  Installed once per process, on the first sptr_create, for the
+// thread that creates the context (its alternate signal stack).
+static void segv_put(const char* s) { (void)!write(2, s, strlen(s)); }
+static void segv_hex(uint64_t v) {
+  char b[19] = "0x";
+  for (int i = 0; i < 16; ++i) b[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15u];
+  b[18] = 0;
+  segv_put(b);
+}
+static void segv_where(uint64_t pc) {
+  Dl_info di{};
+  segv_hex(pc);
+  if (dladdr(reinterpret_cast<void*>(pc), &di) && di.dli_fname) {
+    segv_put(" ");
+    segv_put(di.dli_fname);
+    segv_put("+");
+    segv_hex(pc - reinterpret_cast<uint64_t>(di.dli_fbase));
+    if (di.dli_sname) {
+      segv_put(" ");
+      segv_put(di.dli_sname);
+    }
+  }
+  segv_put("\n");
+}
+static void segv_trace(int sig, siginfo_t* si, void* uc_v) {
+  const ucontext_t* uc = static_cast<const ucontext_t*>(uc_v);
+  const uint64_t pc = (uint64_t)uc->uc_mcontext.gregs[REG_RIP], sp = (uint64_t)uc->uc_mcontext.gregs[REG_RSP];
+  segv_put("sptr SIGSEGV: addr ");
+  segv_hex(reinterpret_cast<uint64_t>(si->si_addr));
+  segv_put(" sp ");
+  segv_hex(sp);
+  segv_put("\n  pc ");
+  segv_where(pc);
+  const uint64_t* st = reinterpret_cast<const uint64_t*>(sp);
+  for (int i = 0, shown = 0; i < 512 && shown < 96; ++i) {
+    Dl_info di{};
+    const uint64_t v = st[i];
+    if (v > 4096 && dladdr(reinterpret_cast<void*>(v), &di) && di.dli_fname) {
+      ++shown;
+      segv_put("  ret? ");
+      segv_where(v);
+    }
+  }
   void* fr[64];
   const int n = backtrace(fr, 64);
   backtrace_symbols_fd(fr, n, 2);
@@ -1151,14 +1230,14 @@ static void install_segv_trace() {
     if (getenv("SPTR_SEGV_TRACE") == nullptr) return;
     void* prime[2];
     (void)backtrace(prime, 2);
-    static char alt[1 << 16];
+    static char alt[1 << 20];
     stack_t ss{};
     ss.ss_sp = alt;
     ss.ss_size = sizeof(alt);
     sigaltstack(&ss, nullptr);
     struct sigaction sa{};
-    sa.sa_handler = segv_trace;
-    sa.sa_flags = SA_ONSTACK;
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_ONSTACK | SA_SIGINFO;
     sigaction(SIGSEGV, &sa, nullptr);
   });
 }
@@ -1200,11 +1279,10 @@ static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
   Context& c = x->c;
   c.device = device;
   if (parent) {
-    c.cap_stream = parent->c.cap_stream;
+    c.parent = &parent->c;
     c.prio_lo = parent->c.prio_lo;
     c.prio_hi = parent->c.prio_hi;
     if (hipSetDevice(device) != hipSuccess || !create_events(c)) {
-      c.cap_stream = nullptr;
       delete x;
       return SPTR_ERR_HIP;
     }
@@ -1238,6 +1316,11 @@ static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
 
 int sptr_destroy(sptr_ctx* x) {
   if (!x) return SPTR_ERR_INVALID;
+  // this context's stream first: after an asynchronous two-lane call it may still run
+  // k_interleave_tiles, which reads the lane's tiles
+  (void)hipSetDevice(x->c.device);
+  if (x->c.pending) (void)hipStreamSynchronize(x->c.pending_stream);
+  if (x->c.stream) (void)hipStreamSynchronize(x->c.stream);
   if (x->lane) (void)sptr_destroy(x->lane);
   x->lane = nullptr;
   for (hipEvent_t e : {x->lane_fork, x->lane_join})
@@ -1245,7 +1328,6 @@ int sptr_destroy(sptr_ctx* x) {
   free_buf(x->tiles_full);
   Context& c = x->c;
   (void)hipSetDevice(c.device);
-  if (x->is_lane) c.cap_stream = nullptr;  // (the parent's)
   if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
   if (c.stream) (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
@@ -1266,6 +1348,8 @@ int sptr_destroy(sptr_ctx* x) {
   if (c.cap_side) (void)hipStreamDestroy(c.cap_side);
   for (hipEvent_t* e : dep_events(c))
     if (*e) (void)hipEventDestroy(*e);
+  for (hipEvent_t e : c.quiet_ev)
+    if (e) (void)hipEventDestroy(e);
   delete x;
   return SPTR_OK;
 }
@@ -1468,7 +1552,7 @@ static int render_one(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats
   Context& c = x->c;
   API_HIP(hipSetDevice(c.device));
   if (!c.have_scene) return fail(c, SPTR_ERR_NO_SCENE, "render: no scene uploaded");
-  if (c.mats_host.empty()) return fail(c, SPTR_ERR_NO_SCENE, "render: no materials set");
+  if (shading(c).mats_host.empty()) return fail(c, SPTR_ERR_NO_SCENE, "render: no materials set");
   if (f->width <= 0 || f->height <= 0 || f->spp == 0 || f->max_depth == 0 || f->max_depth > (uint32_t)kMaxDepth ||
       f->frame_begin == 0)
     return fail(c, SPTR_ERR_INVALID, "render: bad frame parameters");
@@ -1517,7 +1601,7 @@ static int render_one(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) {
           const uint32_t hm = hrec_mult(scene_view(c));
           const uint64_t held = c.wb.cap ? c.wb.cap * wave_path_bytes(c.wb.L, c.wb.ts, hm) : 0ull;
-          const uint32_t L = std::max<uint32_t>(1u, (uint32_t)c.lights_host.size());
+          const uint32_t L = std::max<uint32_t>(1u, (uint32_t)shading(c).lights_host.size());
           // budget net of the streams' segment slack (worst case: pixel-major hit records, k <= spp)
           const double budget = ((double)free_b + (double)held) * kWaveMemFraction -
                                 (double)wave_slack_bytes(L, task_stride(c), std::min<uint32_t>(f->spp, 1024u), hm);
@@ -1538,7 +1622,7 @@ static int render_one(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats
         pm = pm || bounce0_pixel_major(scene_view(c), probe) != 0u;
       }
       // hit-record segments hold twice the static shares when k_trace_dyn takes its rays from the per-XCD queues
-      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)c.lights_host.size(), task_stride(c), pm ? k : 1u,
+      rc = ensure_wave(c, (uint64_t)k * c.P, (uint32_t)shading(c).lights_host.size(), task_stride(c), pm ? k : 1u,
                        hrec_mult(scene_view(c)));
       if (rc != SPTR_OK) return rc;
     }
@@ -2055,7 +2139,9 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c.stream;
   const bool serial = c.launch_mode == 2u;  // one stream: the lanes one after the other
   hipStream_t sy = serial ? s : cy.stream;
-  if (c.pending && s != c.pending_stream)
+  // both halves checked before either is enqueued (a change into or out of launch mode 2 between two
+  // asynchronous calls moves the lane's half between its own stream and s: ADVICE r05)
+  if ((c.pending && s != c.pending_stream) || (cy.pending && sy != cy.pending_stream))
     return fail(c, SPTR_ERR_INVALID, "render: asynchronous renders must stay on one stream until sptr_collect_stats");
   if (!x->split || c.W != f->width || c.H != f->height || x->full_G != G || x->full_R != R) {
     if (f->frame_begin != 1) return fail(c, SPTR_ERR_INVALID, "render: frame_begin must continue the accumulation (last + 1) or be 1");
@@ -2106,10 +2192,20 @@ int sptr_render(sptr_ctx* x, const sptr_frame* f, void* stream, sptr_stats* stat
   return SPTR_OK;
 }
 
-int sptr_set_debug_mode(sptr_ctx* x, int mode) {
-  const int rc = set_debug_mode_one(x, mode);
-  return rc == SPTR_OK ? lane_forward(x, set_debug_mode_one(x ? x->lane : nullptr, mode)) : rc;
+// The shading setters change only this context: a pixel lane reads its parent's shading state
+// (shading()).  A lane render still pending reads the parent's device buffers, so the setters that
+// replace them wait for it first; every shading change drops the lane's captured graph (epoch).
+static int lane_shading_sync(sptr_ctx* x) {
+  if (!x || !x->lane || x->lane->c.pending == 0) return SPTR_OK;
+  if (sync_pending(x->lane->c) != SPTR_OK) return fail(x->c, SPTR_ERR_HIP, std::string("pixel lane: ") + x->lane->c.err);
+  return SPTR_OK;
 }
+static int lane_shading_changed(sptr_ctx* x, int rc) {
+  if (x && x->lane) ++x->lane->c.epoch;
+  return rc;
+}
+
+int sptr_set_debug_mode(sptr_ctx* x, int mode) { return lane_shading_changed(x, set_debug_mode_one(x, mode)); }
 
 int sptr_set_leaf_size(sptr_ctx* x, uint32_t n) {
   const int rc = set_leaf_size_one(x, n);
@@ -2142,23 +2238,24 @@ int sptr_set_wave_paths(sptr_ctx* x, uint64_t max_paths) {
 }
 
 int sptr_set_materials(sptr_ctx* x, const sptr_material* m, uint32_t n) {
-  const int rc = set_materials_one(x, m, n);
-  return rc == SPTR_OK ? lane_forward(x, set_materials_one(x ? x->lane : nullptr, m, n)) : rc;
+  const int rs = lane_shading_sync(x);
+  if (rs != SPTR_OK) return rs;
+  return lane_shading_changed(x, set_materials_one(x, m, n));
 }
 
 int sptr_set_lights(sptr_ctx* x, const sptr_light* l, uint32_t n) {
-  const int rc = set_lights_one(x, l, n);
-  return rc == SPTR_OK ? lane_forward(x, set_lights_one(x ? x->lane : nullptr, l, n)) : rc;
+  return lane_shading_changed(x, set_lights_one(x, l, n));  // (by value in every launch's arguments)
 }
 
 int sptr_set_environment(sptr_ctx* x, const sptr_environment* e) {
-  const int rc = set_environment_one(x, e);
-  return rc == SPTR_OK ? lane_forward(x, set_environment_one(x ? x->lane : nullptr, e)) : rc;
+  const int rs = lane_shading_sync(x);
+  if (rs != SPTR_OK) return rs;
+  return lane_shading_changed(x, set_environment_one(x, e));
 }
 
 int sptr_set_launch_mode(sptr_ctx* x, uint32_t mode) {
   const int rc = set_launch_mode_one(x, mode);
-  return rc == SPTR_OK ? lane_forward(x, set_launch_mode_one(x ? x->lane : nullptr, mode)) : rc;
+  return rc == SPTR_OK ? lane_forward(x, set_launch_mode_one(x->lane, mode)) : rc;
 }
 
 }  // extern "C"

@@ -352,7 +352,7 @@ struct GraphCache {
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t cap_stream = nullptr;  // launch-graph capture
+  hipStream_t cap_stream = nullptr;  // launch-graph capture (a pixel lane's: created on its first capture)
   // side streams for launches that overlap the main sequence: the shadow launches (side) and k_sky /
   // k_strag (side2; k_sky beside the tail of scenes beyond an XCD's L2 runs on side after the last
   // shadow join), for direct launches and inside a capture (cap_*).  Star-shaped fork/join only: a side
@@ -366,10 +366,14 @@ struct Context {
     hipEvent_t fork = nullptr, join = nullptr, sky = nullptr;
   } dev[2];
   int prio_lo = 0, prio_hi = 0;  // stream priority range (hipDeviceGetStreamPriorityRange)
+  hipEvent_t quiet_ev[2] = {nullptr, nullptr};  // dispatch events of untimed two-lane launches (StageTimer::quiet)
   // 0: replay a captured graph for repeated call shapes that fork no side-stream launch (run_call);
   // 1: direct launches; 2: direct, one stream; 3: graph for every repeated shape
   uint32_t launch_mode = 0;
   uint8_t* image_out = nullptr;  // a pixel lane's resolve target: its parent context's image (sptr_render)
+  // a pixel lane's parent: the lane reads the parent's shading state (materials, geomID -> material
+  // table, lights, environment, debug mode) instead of holding copies (shading(), sptr_api.cpp)
+  const Context* parent = nullptr;
   bool last_forked = false;          // the last direct launch sequence forked launches to a side stream
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on

@@ -18,6 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPTR_LIB") or os.path.join(HERE, "libsptr_hip.so")  # SPTR_LIB: A/B builds
 
+SPTR_ABI_VERSION = 8  # include/sptr_hip.h
 SPTR_FRAME_TIMING = 1
 SPTR_FRAME_NO_RESOLVE = 2
 SPTR_FRAME_COUNT_VISITS = 4
@@ -184,6 +185,8 @@ def lib() -> C.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if L.sptr_abi_version() != SPTR_ABI_VERSION:  # a stale build would misread the structs below
+        raise SptrError(f"{LIB_PATH}: ABI {L.sptr_abi_version()}, this binding expects {SPTR_ABI_VERSION} (rebuild)")
     _lib = L
     return L
 

@@ -99,9 +99,8 @@ def test_c3_chair_hdr_vs_oracle(renderer):
 
 
 def test_c3_batches_bit_exact(renderer):
-    """C3's L2-resident BVH4 + cubemap in one 32-sample batch: bit-identical to 8-sample batches
-    (and, with the experiment knob SPTR_FOLD=2, the non-LDS lane-group kernel k_trace_wp), and close
-    to the oracle."""
+    """C3's L2-resident BVH4 + cubemap in one 32-sample batch: bit-identical to 8-sample batches, and
+    close to the oracle."""
     wl = workloads.WORKLOADS["c3"]
     faces = workloads.hdr_env_faces()
     flat = sptr.setup_default(renderer, wl.scene, wl.p0, wl.p1, env_faces=faces)

@@ -120,6 +120,42 @@ def test_c2_full_size_deterministic_and_shardable(renderer, c2_full):
     assert rays == st0.rays_closest + st0.rays_shadow
 
 
+@pytest.mark.parametrize("lanes", [0, 1])
+@pytest.mark.parametrize("timing", [False, True])
+def test_c2_bench_step_shape_equals_validated_image(renderer, c2_full, lanes, timing):
+    """bench.py's step() at full C2 size, call for call: SPTR_FRAME_RECULL | SPTR_FRAME_ASYNC on a torch
+    stream (the timed steps; with SPTR_FRAME_TIMING_TRACE, the roofline pass, whose pixel-lane launches
+    run the kTimed kernel instantiations), three calls so that a shape launch mode 0 captures is also
+    replayed, then sptr_tiles_device -> sptr_unpack_tiles on that stream.  The unpacked image must equal
+    the oracle-checked c2_full RGB8 image byte for byte, with pixel lanes automatic (two lanes at this
+    size) and as one chain."""
+    import torch
+
+    cam, st0, rgb0, _ = c2_full
+    W, H, S = 1920, 1080, 64
+    sptr.setup_default(renderer, "default_emitter")
+    renderer.set_pixel_lanes(lanes)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    image = torch.zeros(W * H * 3, dtype=torch.uint8, device=dev)
+    flags = sptr.SPTR_FRAME_RECULL | sptr.SPTR_FRAME_ASYNC | (sptr.SPTR_FRAME_TIMING_TRACE if timing else 0)
+    try:
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                renderer.render(cam, W, H, spp=S, flags=flags, stream=stream.cuda_stream)
+                ptr, nbytes = renderer.tiles_device()
+                renderer.unpack_tiles(ptr, 1, nbytes // 4096, W, H, image.data_ptr(), stream=stream.cuda_stream)
+        st = renderer.collect_stats()
+        stream.synchronize()
+        assert renderer.pixel_lanes_info()["active"] == (lanes == 0)
+        assert np.array_equal(image.cpu().numpy().reshape(H, W, 3), rgb0)
+        assert (st.rays_closest, st.rays_shadow) == (3 * st0.rays_closest, 3 * st0.rays_shadow)
+        if timing:
+            assert st.trace_launches > 0 and st.ms_trace > 0.0
+    finally:
+        renderer.set_pixel_lanes(0)
+
+
 def _read_ppm(path):
     with open(path, "rb") as f:
         data = f.read()
