@@ -389,7 +389,9 @@ def interactive(steps):
     every frame, as GLRenderer::renderLoop drives a backend (src/GLRenderer.cpp:161-176).  Runs the C++
     harness (backends::HipBackend through the C ABI) as a child process: the default scene at 800x600
     and 1080p, and the L2/HBM scenes C3 (chair + HDR environment) and C5 (10M triangles) at 1080p; the
-    1080p legs in launch mode 0 (graph replay where it pays, the default) and 1 (direct launches)."""
+    1080p legs in launch mode 0 (graph replay where it pays, the default) and 1 (direct launches), and
+    with HipBackend::Settings::lagged_readback (each render() returns the previous frame's image, read
+    back beside the next frame's kernels: sptr_read_rgb8_lagged)."""
     import tempfile
 
     cli = os.path.join(ROOT, "simple-path-tracer_amd", "sptr_cli")
@@ -404,6 +406,9 @@ def interactive(steps):
         for mode in (0, 1):
             legs.append((["--scene", c3.scene, "--env", sky], 1920, 1080, mode))
             legs.append((["--scene", f"sphere_mesh:{c5.p0}:{c5.p1}"], 1920, 1080, mode))
+        legs += [(["--scene", "default", "--lagged"], 800, 600, 0), (["--scene", "default", "--lagged"], 1920, 1080, 0),
+                 (["--scene", c3.scene, "--env", sky, "--lagged"], 1920, 1080, 0),
+                 (["--scene", f"sphere_mesh:{c5.p0}:{c5.p1}", "--lagged"], 1920, 1080, 0)]
         for extra, w, h, mode in legs:
             r = subprocess.run([cli, *extra, "--w", str(w), "--h", str(h), "--spp", str(steps), "--warmup", "10",
                                 "--launch-mode", str(mode), "--json", "--out", "/dev/null"], capture_output=True,
@@ -707,6 +712,9 @@ def main():
     # trace and shadow launches' own durations, with nothing beside them (roofline_serial)
     stats_serial = None
     residency = _residency(layout)[0]
+    # the committed counter summaries (profiles/r*_pmc_<wl>_*.json) describe the workload's default line; an
+    # emulated shard or a one-chain pass runs other launches, so they take no counter fractions
+    prof = wl.name if not args.emulate_shards else f"{wl.name}_shard{args.emulate_shards}"
     if world == 1 and residency != "lds" and not args.no_serial_pass and args.launch_mode == 0 and \
             args.integrator == "wavefront":
         r.set_launch_mode(2)
@@ -799,8 +807,8 @@ def main():
             "world_size": world,
             "collective": ("RCCL gather of the RGBA8 tiles to rank 0 (point-to-point over xGMI), once per step" if distributed
                            else "none (1 rank)"),
-            "roofline": roofline(cnt, stats_rf, layout, wl.name, args.steps, env_bytes=env_bytes),
-            "shadow_roofline": shadow_roofline(cnt, stats_rf, layout, wl.name, args.steps),
+            "roofline": roofline(cnt, stats_rf, layout, prof, args.steps, env_bytes=env_bytes),
+            "shadow_roofline": shadow_roofline(cnt, stats_rf, layout, prof, args.steps),
             # the launch durations above come from this untimed pass of the same steps
             "roofline_pass": {"flags": "SPTR_FRAME_TIMING_TRACE | SPTR_FRAME_RECULL (direct launches)",
                               "ms_per_step": round(rf_elapsed / args.steps * 1e3, 3)},
@@ -850,7 +858,7 @@ def main():
                                        "(the union of their intervals over both lanes, busy_us_per_launch)"
                                if lanes_info["active"] else "one launch chain"}
         if stats_one:
-            ro = roofline(cnt, stats_one, layout, wl.name, args.steps, env_bytes=env_bytes)
+            ro = roofline(cnt, stats_one, layout, wl.name + "_one_chain", args.steps, env_bytes=env_bytes)
             line["roofline_one_chain"] = {
                 "note": "untimed pass of the same steps as one launch chain (sptr_set_pixel_lanes 1): the trace "
                         "launches' own durations; the headline value is the two-lane run's",

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SPTR_ABI_VERSION 8
+#define SPTR_ABI_VERSION 9
 
 enum sptr_status {
   SPTR_OK = 0,
@@ -321,6 +321,16 @@ int sptr_collect_stats(sptr_ctx* ctx, sptr_stats* stats);
  * (width*height*3 floats; divide by the frame count for the mean): linear radiance in wavefront
  * mode, tonemapped per-frame colours in PathTracer mode (what GLRenderer accumulates). */
 int sptr_read_rgb8(sptr_ctx* ctx, uint8_t* rgb);
+/* ABI 9, the interactive loop's readback with one frame of latency (GLRenderer::renderLoop calls render()
+ * once per frame, src/GLRenderer.cpp:161-176): call it after an asynchronous render (SPTR_FRAME_ASYNC).  The
+ * image of that call is snapshotted on the device (a device-to-device copy ordered after it); the snapshot
+ * taken by the previous sptr_read_rgb8_lagged call, if it is of the same size, is copied into rgb on a
+ * copy stream of its own — beside the render just enqueued — and waited for: *got = 1.  Otherwise rgb is
+ * left alone and *got = 0 (the first frame, or a resize: read that frame with sptr_read_rgb8).  rgb is
+ * page-locked (hipHostRegister) while the context uses it as a destination, so the copy is a DMA that
+ * overlaps the next frame's kernels; it is unregistered when another buffer takes its place and by
+ * sptr_destroy.  The render stream is not waited for: sptr_collect_stats collects the calls' counters. */
+int sptr_read_rgb8_lagged(sptr_ctx* ctx, uint8_t* rgb, uint32_t* got);
 int sptr_read_accum(sptr_ctx* ctx, float* accum);
 /* Device view of this shard's resolved tiles: RGBA8, [local tile][32][32] uint32, for the
  * multi-GPU gather.  *bytes = local_tiles * 4096. */

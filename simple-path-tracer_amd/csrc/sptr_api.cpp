@@ -36,6 +36,19 @@ struct sptr_ctx {
   sptr::DevBuf tiles_full;  // with split: this context's tiles, interleaved from the two lanes'
   uint32_t full_tiles = 0;
   int full_G = 1, full_R = 0;
+  // sptr_read_rgb8_lagged: two device snapshots of the RGB8 image, alternately written; a copy stream and
+  // the registered host destination (created / registered on first use)
+  struct Snap {
+    sptr::DevBuf buf;
+    hipEvent_t ready = nullptr;
+    int W = 0, H = 0;
+    bool valid = false;
+  } snap[2];
+  uint32_t snap_cur = 0;
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t copy_done = nullptr;
+  void* reg_ptr = nullptr;
+  size_t reg_bytes = 0;
 };
 
 namespace sptr {
@@ -324,7 +337,8 @@ struct StageTimer {
   bool quiet = false, quiet_open = false;  // untimed launch with dispatch events (run_call)
   void begin(int stage) {
     if (quiet && !on && !capturing && one_launch(stage)) {
-      g_launch_timing = LaunchTiming{c.quiet_ev[0], c.quiet_ev[1]};
+      if (c.time_by_events) g_launch_timing = LaunchTiming{c.quiet_ev[0], c.quiet_ev[1]};
+      else g_tslot = static_cast<unsigned long long*>(c.tslots.p) + (size_t)kTimeSlotWords * kTimeSlots;  // (never read)
       quiet_open = true;
       return;
     }
@@ -357,6 +371,7 @@ struct StageTimer {
     if (quiet_open) {
       quiet_open = false;
       g_launch_timing = LaunchTiming{};  // (taken by the launch; cleared if there was none)
+      g_tslot = nullptr;
       return;
     }
     if (open == SIZE_MAX) return;
@@ -1017,7 +1032,10 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     // untimed two-lane calls launch their trace and fused-bounce kernels with dispatch events all the same
     // (two events reused by every such launch, never read): r06l, C2 2.512-2.531 vs 2.548-2.565 ms per step
     // with plain launches, on one box
-    tm.quiet = !timing && c.time_by_events && c.quiet_ev[1] != nullptr;
+#ifndef SPTR_QUIET_SLOTS
+#define SPTR_QUIET_SLOTS 0
+#endif
+    tm.quiet = !timing && (c.time_by_events ? c.quiet_ev[1] != nullptr : (SPTR_QUIET_SLOTS && c.tslots.p != nullptr));
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
@@ -1303,8 +1321,8 @@ static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
   int khz = 0;
   if (ensure_buf(c.wb.seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
       ensure_buf(c.dyn, kDynBytes) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess ||
-      ensure_buf(c.tslots, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
-      hipMemset(c.tslots.p, 0, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
+      ensure_buf(c.tslots, (size_t)(kTimeSlots + 1) * kTimeSlotWords * 8) != hipSuccess ||
+      hipMemset(c.tslots.p, 0, (size_t)(kTimeSlots + 1) * kTimeSlotWords * 8) != hipSuccess ||
       hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
     delete x;
     return SPTR_ERR_OOM;
@@ -1321,6 +1339,16 @@ int sptr_destroy(sptr_ctx* x) {
   (void)hipSetDevice(x->c.device);
   if (x->c.pending) (void)hipStreamSynchronize(x->c.pending_stream);
   if (x->c.stream) (void)hipStreamSynchronize(x->c.stream);
+  if (x->copy_stream) {  // the lagged readback's copy stream, snapshots and registered destination
+    (void)hipStreamSynchronize(x->copy_stream);
+    (void)hipStreamDestroy(x->copy_stream);
+  }
+  if (x->copy_done) (void)hipEventDestroy(x->copy_done);
+  for (auto& sn : x->snap) {
+    free_buf(sn.buf);
+    if (sn.ready) (void)hipEventDestroy(sn.ready);
+  }
+  if (x->reg_ptr) (void)hipHostUnregister(x->reg_ptr);
   if (x->lane) (void)sptr_destroy(x->lane);
   x->lane = nullptr;
   for (hipEvent_t e : {x->lane_fork, x->lane_join})
@@ -1764,6 +1792,53 @@ int sptr_read_rgb8(sptr_ctx* x, uint8_t* rgb) {
   if (!c.image.p) return fail(c, SPTR_ERR_NO_SCENE, "read_rgb8: nothing rendered");
   API_HIP(hipSetDevice(c.device));
   API_HIP(hipMemcpy(rgb, c.image.p, (size_t)c.W * c.H * 3, hipMemcpyDeviceToHost));
+  return SPTR_OK;
+}
+
+int sptr_read_rgb8_lagged(sptr_ctx* x, uint8_t* rgb, uint32_t* got) {
+  if (!x || !rgb || !got) return SPTR_ERR_INVALID;
+  Context& c = x->c;
+  *got = 0;
+  if (!c.image.p || c.pending == 0)
+    return fail(c, SPTR_ERR_INVALID, "read_rgb8_lagged: call after an asynchronous render (SPTR_FRAME_ASYNC)");
+  API_HIP(hipSetDevice(c.device));
+  if (!x->copy_stream) {
+    // a priority of its own (the lowest): its own hardware queue, apart from the render stream's
+    API_HIP(hipStreamCreateWithPriority(&x->copy_stream, hipStreamNonBlocking, c.prio_lo));
+    API_HIP(hipEventCreateWithFlags(&x->copy_done, hipEventDisableTiming));
+    for (auto& sn : x->snap) API_HIP(hipEventCreateWithFlags(&sn.ready, hipEventDisableTiming));
+  }
+  const size_t bytes = (size_t)c.W * c.H * 3;
+  auto& cur = x->snap[x->snap_cur];
+  auto& prev = x->snap[x->snap_cur ^ 1u];
+  // this call's image, snapshotted on its stream after it (with two lanes, the lane's resolve into this
+  // image is joined into that stream before the call's last launch).  The slot's last reader was the copy
+  // two calls back, which that call waited for.
+  API_HIP(ensure_buf(cur.buf, bytes));
+  API_HIP(hipMemcpyAsync(cur.buf.p, c.image.p, bytes, hipMemcpyDeviceToDevice, c.pending_stream));
+  API_HIP(hipEventRecord(cur.ready, c.pending_stream));
+  if (prev.valid && prev.W == c.W && prev.H == c.H) {
+    if (x->reg_ptr != rgb || x->reg_bytes != bytes) {  // page-lock the destination: the copy becomes a DMA
+      if (x->reg_ptr) (void)hipHostUnregister(x->reg_ptr);
+      x->reg_ptr = nullptr;
+      x->reg_bytes = 0;
+      if (hipHostRegister(rgb, bytes, hipHostRegisterDefault) == hipSuccess) {
+        x->reg_ptr = rgb;
+        x->reg_bytes = bytes;
+      } else {
+        (void)hipGetLastError();  // (a pageable destination works too, through staging)
+      }
+    }
+    API_HIP(hipStreamWaitEvent(x->copy_stream, prev.ready, 0));
+    API_HIP(hipMemcpyAsync(rgb, prev.buf.p, bytes, hipMemcpyDeviceToHost, x->copy_stream));
+    API_HIP(hipEventRecord(x->copy_done, x->copy_stream));
+    API_HIP(hipEventSynchronize(x->copy_done));
+    *got = 1;
+  }
+  cur.valid = true;
+  cur.W = c.W;
+  cur.H = c.H;
+  x->snap_cur ^= 1u;
   return SPTR_OK;
 }
 

@@ -378,7 +378,8 @@ struct Context {
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
-  DevBuf tslots;                     // [kTimeSlots][kTimeSlotWords] launch timing slots, zeroed
+  DevBuf tslots;                     // [kTimeSlots + 1][kTimeSlotWords] launch timing slots, zeroed (the last
+                                     // one is written by untimed launches and never read: StageTimer::quiet)
   uint32_t tslots_used = 0;          // slots handed out in this collection window
   double wall_khz = 0.0;             // the device wall clock's rate (wall_clock64 ticks per ms)
   bool time_by_events = false;       // one-launch stages timed by dispatch events, not slots (pixel lanes)

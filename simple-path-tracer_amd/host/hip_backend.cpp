@@ -22,6 +22,7 @@ bool HipBackend::ensureContext() {
 }
 
 void HipBackend::destroy() {
+  if (ctx_) (void)flushStats();
   if (ctx_) sptr_destroy(ctx_);
   ctx_ = nullptr;
   built_ = false;
@@ -78,7 +79,31 @@ bool HipBackend::syncState() {
   return true;
 }
 
-bool HipBackend::renderInternal(int w, int h, const Camera& camera) {
+void HipBackend::addStats(const sptr_stats& s) {
+  flushed_.rays_closest += s.rays_closest;
+  flushed_.rays_shadow += s.rays_shadow;
+  flushed_.samples += s.samples;
+  flushed_.waves += s.waves;
+  flushed_.ms_total += s.ms_total;
+  flushed_.ms_trace += s.ms_trace;
+  flushed_.trace_launches += s.trace_launches;
+}
+
+sptr_stats HipBackend::flushStats() {
+  if (ctx_ && async_calls_) {
+    sptr_stats s{};
+    if (sptr_collect_stats(ctx_, &s) == SPTR_OK) {
+      stats_ = s;
+      addStats(s);
+    }
+    async_calls_ = 0;
+  }
+  const sptr_stats out = flushed_;
+  flushed_ = sptr_stats{};
+  return out;
+}
+
+bool HipBackend::renderInternal(int w, int h, const Camera& camera, bool async) {
   if (!built_ || !ctx_) {
     err_ = "HipBackend::render: build() has not succeeded";
     return false;
@@ -117,22 +142,51 @@ bool HipBackend::renderInternal(int w, int h, const Camera& camera) {
   fr.shard_count = 1;
   fr.integrator = settings_.integrator;
   fr.samples_per_frame = settings_.samples_per_frame;
+  if (async) fr.flags |= SPTR_FRAME_ASYNC;
   if (sptr_set_launch_mode(ctx_, settings_.launch_mode) != SPTR_OK) {
     err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);
     return false;
   }
-  const int rc = sptr_render(ctx_, &fr, nullptr, &stats_);
+  sptr_stats st{};
+  const int rc = sptr_render(ctx_, &fr, nullptr, &st);
   if (rc != SPTR_OK) {
     err_ = std::string("HipBackend::render: ") + sptr_last_error(ctx_);
     return false;
+  }
+  if (async) {
+    ++async_calls_;
+  } else {
+    stats_ = st;  // (a synchronous call also collects any pending asynchronous ones)
+    addStats(st);
+    async_calls_ = 0;
   }
   frame_index_ += fr.spp;
   return true;
 }
 
 void HipBackend::render(unsigned char* pixels, int width, int height, const Camera& camera) {
-  if (!renderInternal(width, height, camera)) {
+  const bool lagged = settings_.lagged_readback;
+  if (!renderInternal(width, height, camera, lagged)) {
     std::fprintf(stderr, "%s\n", err_.c_str());
+    return;
+  }
+  if (lagged) {
+    // the previous frame's image, copied while this frame's kernels run; none yet (the first frame or a
+    // resize): this frame's, synchronously
+    uint32_t got = 0;
+    if (sptr_read_rgb8_lagged(ctx_, pixels, &got) != SPTR_OK) {
+      std::fprintf(stderr, "HipBackend: %s\n", sptr_last_error(ctx_));
+      return;
+    }
+    if (!got && sptr_read_rgb8(ctx_, pixels) != SPTR_OK) std::fprintf(stderr, "HipBackend: %s\n", sptr_last_error(ctx_));
+    if (async_calls_ >= kLaggedCollect) {  // bounded: each pending call holds its call-span events
+      sptr_stats s{};
+      if (sptr_collect_stats(ctx_, &s) == SPTR_OK) {
+        stats_ = s;
+        addStats(s);
+      }
+      async_calls_ = 0;
+    }
     return;
   }
   if (sptr_read_rgb8(ctx_, pixels) != SPTR_OK) std::fprintf(stderr, "HipBackend: %s\n", sptr_last_error(ctx_));

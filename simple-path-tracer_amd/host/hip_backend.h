@@ -31,7 +31,13 @@ class HipBackend {
     // sptr_set_pixel_lanes: 0 = two concurrent launch chains for calls of >= 2^24 samples on scenes
     // staged in LDS (default), 1 = one chain, 2 = two chains; a change restarts the accumulation
     uint32_t pixel_lanes = 0;
+    // render() returns the previous call's image (one frame of latency) so that the read back of one frame
+    // runs beside the next frame's kernels (sptr_read_rgb8_lagged); the first frame after a reset or a
+    // resize is read synchronously.  The pixel buffer stays page-locked while render() writes into it.
+    // Counters (stats()) are collected every kLaggedCollect calls and by flushStats().
+    bool lagged_readback = false;
   };
+  static constexpr uint32_t kLaggedCollect = 32;
 
   explicit HipBackend(int device = 0);
   ~HipBackend();
@@ -51,6 +57,8 @@ class HipBackend {
   // linear accumulated radiance mean (width*height*3) of the current accumulation
   bool renderLinear(float* rgb32, int width, int height, const Camera& camera);
   const sptr_stats& stats() const { return stats_; }
+  // the counters of every render() since the last flush, summed (waits for the pending frames)
+  sptr_stats flushStats();
   uint32_t frameIndex() const { return frame_index_; }
   const std::string& lastError() const { return err_; }
   const std::vector<uint32_t>& getGeomMaterialMapping() const { return geom_material_; }
@@ -58,7 +66,8 @@ class HipBackend {
  private:
   bool ensureContext();
   bool syncState();
-  bool renderInternal(int width, int height, const Camera& camera);
+  bool renderInternal(int width, int height, const Camera& camera, bool async = false);
+  void addStats(const sptr_stats& s);
 
   int device_;
   sptr_ctx* ctx_ = nullptr;
@@ -76,6 +85,8 @@ class HipBackend {
   std::string err_;
   int debug_mode_ = 0;
   uint32_t lanes_applied_ = 0;  // the pixel-lane setting the context holds
+  sptr_stats flushed_{};        // counters since the last flushStats()
+  uint32_t async_calls_ = 0;    // lagged mode: render calls not yet collected
 };
 
 }  // namespace backends

@@ -18,7 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPTR_LIB") or os.path.join(HERE, "libsptr_hip.so")  # SPTR_LIB: A/B builds
 
-SPTR_ABI_VERSION = 8  # include/sptr_hip.h
+SPTR_ABI_VERSION = 9  # include/sptr_hip.h
 SPTR_FRAME_TIMING = 1
 SPTR_FRAME_NO_RESOLVE = 2
 SPTR_FRAME_COUNT_VISITS = 4
@@ -113,7 +113,7 @@ EXPORTS = [
     "sptr_abi_version", "sptr_create", "sptr_destroy", "sptr_last_error", "sptr_set_debug_mode",
     "sptr_set_wave_paths", "sptr_set_launch_mode", "sptr_set_pixel_lanes", "sptr_pixel_lanes_info", "sptr_graph_info", "sptr_capture_error", "sptr_overlap_probe", "sptr_set_tail_depth", "sptr_set_leaf_size", "sptr_set_split_refs", "sptr_set_stragglers", "sptr_set_bvh_width", "sptr_upload_scene", "sptr_set_materials", "sptr_set_lights",
     "sptr_set_environment", "sptr_scene_info", "sptr_scene_layout_info", "sptr_render", "sptr_collect_stats",
-    "sptr_read_rgb8",
+    "sptr_read_rgb8", "sptr_read_rgb8_lagged",
     "sptr_read_accum",
     "sptr_tiles_device", "sptr_unpack_tiles", "sptr_intersect", "sptr_occluded", "sptr_primary_rays",
     "sptr_sort_pairs_u64", "sptr_scan_u32", "sptr_eval_math",
@@ -160,6 +160,7 @@ def lib() -> C.CDLL:
         "sptr_render": (C.c_int, [vp, C.POINTER(Frame), vp, C.POINTER(Stats)]),
         "sptr_collect_stats": (C.c_int, [vp, C.POINTER(Stats)]),
         "sptr_read_rgb8": (C.c_int, [vp, bp]),
+        "sptr_read_rgb8_lagged": (C.c_int, [vp, bp, C.POINTER(u32)]),
         "sptr_read_accum": (C.c_int, [vp, fp]),
         "sptr_tiles_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_size_t)]),
         "sptr_unpack_tiles": (C.c_int, [vp, vp, i32, u32, i32, i32, vp, vp]),
@@ -489,6 +490,14 @@ class Renderer:
         out = np.zeros((self.height, self.width, 3), np.uint8)
         self._check(self._L.sptr_read_rgb8(self._h, _b(out)), "read_rgb8")
         return out
+
+    def read_rgb8_lagged(self, out: np.ndarray) -> bool:
+        """After an asynchronous render: out <- the image of the previous such call (True), or False
+        (out untouched) when there is none of this size yet.  out stays page-locked while in use."""
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size == self.width * self.height * 3
+        got = C.c_uint32()
+        self._check(self._L.sptr_read_rgb8_lagged(self._h, _b(out), C.byref(got)), "read_rgb8_lagged")
+        return bool(got.value)
 
     def read_accum(self) -> np.ndarray:
         out = np.zeros((self.height, self.width, 3), np.float32)

@@ -5,10 +5,12 @@
 //   sptr_cli [--scene default|default_emitter|test_triangle|sphere_mesh:STACKS:SLICES|gltf:PATH]
 //            [--w 800] [--h 600] [--spp 4] [--depth 6] [--env sky|FILE.hdr] [--out image.ppm]
 //            [--warmup N] [--json] [--integrator wavefront|pathtracer|optix] [--spf 4] [--launch-mode 0-3]
+//            [--lagged]
 // --spp N renders N progressive frames of 1 spp each (GLRenderer's m_accumulated_samples loop);
 // --warmup N renders N untimed frames first (then restarts the accumulation by a camera change);
 // --json prints one line with per-frame wall-clock statistics (render + RGB8 read back, as the
-// window loop pays them) for bench.py's interactive leg.
+// window loop pays them) for bench.py's interactive leg.  --lagged: HipBackend::Settings::lagged_readback
+// (each render() returns the previous frame's image, read back beside the next frame's kernels).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -41,7 +43,7 @@ static bool build_scene(const std::string& s, scene::SceneDesc& sd, MaterialMana
 int main(int argc, char** argv) {
   std::string scene_name = "default", env = "sky", out = "image.ppm";
   int w = 800, h = 600, spp = 4, depth = 6, warmup = 0;
-  bool json = false;
+  bool json = false, lagged = false;
   std::string integrator = "wavefront";
   int spf = 4, launch_mode = 0;
   for (int i = 1; i < argc; ++i) {
@@ -59,6 +61,7 @@ int main(int argc, char** argv) {
     else if (a == "--integrator") integrator = next();
     else if (a == "--spf") spf = std::atoi(next());
     else if (a == "--launch-mode") launch_mode = std::atoi(next());
+    else if (a == "--lagged") lagged = true;
     else {
       std::fprintf(stderr, "usage: %s [--scene S] [--w W] [--h H] [--spp N] [--depth D] [--env sky|F.hdr] [--out F] [--warmup N] [--json]\n",
                    argv[0]);
@@ -93,6 +96,7 @@ int main(int argc, char** argv) {
   }
   st.samples_per_frame = uint32_t(spf);
   st.launch_mode = uint32_t(launch_mode);
+  st.lagged_readback = lagged;
   be.setSettings(st);
   if (!be.build(sd)) {
     std::fprintf(stderr, "%s\n", be.lastError().c_str());
@@ -103,19 +107,19 @@ int main(int argc, char** argv) {
     Camera wcam(vec3{0.0f, 3.0f, 8.5f}, vec3{0.0f, 1.0f, 0.0f}, vec3{0.0f, 1.0f, 0.0f}, 60.0f, float(w) / float(h));
     for (int f = 0; f < warmup; ++f) be.render(img.data(), w, h, wcam);  // the camera change below resets
   }
-  uint64_t rays = 0;
-  double ms = 0.0;
   std::vector<double> frame_ms;
   frame_ms.reserve(size_t(spp));
+  (void)be.flushStats();  // (the warmup's counters)
   const auto t0 = std::chrono::steady_clock::now();
   for (int f = 0; f < spp; ++f) {
     const auto f0 = std::chrono::steady_clock::now();
     be.render(img.data(), w, h, cam);
     frame_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count());
-    rays += be.stats().rays_closest + be.stats().rays_shadow;
-    ms += be.stats().ms_total;
   }
+  const sptr_stats tot = be.flushStats();  // (lagged: waits for the last frames, inside the clock)
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const uint64_t rays = tot.rays_closest + tot.rays_shadow;
+  const double ms = tot.ms_total;
   if (json) {
     std::vector<double> s = frame_ms;
     std::sort(s.begin(), s.end());
@@ -123,9 +127,10 @@ int main(int argc, char** argv) {
     std::printf("{\"scene\": \"%s\", \"launch_mode\": %d, \"width\": %d, \"height\": %d, \"frames\": %d, \"spp_per_frame\": 1, "
                 "\"depth\": %d, \"ms_per_frame_wall\": %.4f, \"ms_per_frame_p50\": %.4f, \"ms_per_frame_p99\": %.4f, "
                 "\"ms_per_frame_device\": %.4f, \"fps\": %.1f, \"mrays_per_s_wall\": %.1f, "
-                "\"path\": \"backends::HipBackend::render (sptr_render + sptr_read_rgb8 per frame)\"}\n",
+                "\"lagged_readback\": %s, \"path\": \"backends::HipBackend::render (sptr_render + %s per frame)\"}\n",
                 scene_name.c_str(), launch_mode, w, h, spp, depth, wall / spp, pct(0.5), pct(0.99), ms / spp,
-                wall > 0 ? 1e3 * spp / wall : 0.0, wall > 0 ? rays / (wall * 1e3) : 0.0);
+                wall > 0 ? 1e3 * spp / wall : 0.0, wall > 0 ? rays / (wall * 1e3) : 0.0, lagged ? "true" : "false",
+                lagged ? "sptr_read_rgb8_lagged" : "sptr_read_rgb8");
   } else {
     std::printf("scene=%s %dx%d spp=%d depth=%d: %.2f ms device, %.2f ms wall, %.1f Mrays/s (device)\n",
                 scene_name.c_str(), w, h, spp, depth, ms, wall, ms > 0 ? rays / (ms * 1e3) : 0.0);

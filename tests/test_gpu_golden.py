@@ -14,6 +14,7 @@ import sptr
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
+_PAGE_LOCKED = []  # host buffers handed to sptr_read_rgb8_lagged: alive until the session's renderer is closed
 
 
 def _load(name):
@@ -164,17 +165,46 @@ def _read_ppm(path):
     return np.frombuffer(parts[3], np.uint8).reshape(h, w, 3)
 
 
-def test_hip_backend_cpp_harness(tmp_path):
+@pytest.mark.parametrize("lagged", [False, True])
+def test_hip_backend_cpp_harness(tmp_path, lagged):
     """backends::HipBackend (the C++ OptixBackend-surface class) driven frame by frame as
-    GLRenderer::renderLoop drives a backend: 3 progressive render() calls == oracle 3 spp."""
+    GLRenderer::renderLoop drives a backend: 3 progressive render() calls == oracle 3 spp.  With
+    lagged_readback (--lagged) each render() returns the previous frame's image: after 3 calls, 2 spp."""
     exe = os.path.join(ROOT, "simple-path-tracer_amd", "sptr_cli")
     assert os.path.exists(exe), "sptr_cli not built (make -C simple-path-tracer_amd)"
     out = tmp_path / "img.ppm"
-    res = subprocess.run([exe, "--scene", "default", "--w", "96", "--h", "64", "--spp", "3", "--out", str(out)],
-                         capture_output=True, text=True, timeout=120)
+    res = subprocess.run([exe, "--scene", "default", "--w", "96", "--h", "64", "--spp", "3", "--out", str(out)]
+                         + (["--lagged"] if lagged else []), capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stderr
     rgb = _read_ppm(out)
     P = oracle.Prepared(oracle.builtin_scene("default"), bvh=True)
     _, orgb, _ = P.render(oracle.camera(aspect=96 / 64), 96, 64, oracle.preset_materials(False),
-                          oracle.default_lights(), frames=3)
+                          oracle.default_lights(), frames=2 if lagged else 3)
     assert float((rgb == orgb).all(axis=2).mean()) >= 0.999
+
+
+@pytest.mark.parametrize("size", [(96, 64, 1), (1920, 1080, 64)])
+def test_read_rgb8_lagged(renderer, size):
+    """sptr_read_rgb8_lagged after asynchronous progressive calls returns, byte for byte, the image the
+    previous call left (read synchronously then), for a one-chain call and a two-lane (C2-size) call;
+    nothing for the first call and after a resize."""
+    W, H, S = size
+    sptr.setup_default(renderer, "default_emitter")
+    cam = sptr.camera_lookat(aspect=W / H)
+    buf = np.zeros(W * H * 3, np.uint8)
+    _PAGE_LOCKED.append(buf)  # (the library keeps a destination page-locked until another takes its place)
+    prev = None
+    for i in range(4):
+        renderer.render(cam, W, H, spp=S, frame_begin=1 + i * S, flags=sptr.SPTR_FRAME_ASYNC)
+        got = renderer.read_rgb8_lagged(buf)
+        assert got == (prev is not None)
+        if got:
+            assert np.array_equal(buf.reshape(H, W, 3), prev)
+        prev = renderer.read_rgb8().copy()
+    renderer.collect_stats()
+    # a resize: no snapshot of this size yet
+    renderer.render(cam, W // 2, H // 2, spp=1, flags=sptr.SPTR_FRAME_ASYNC)
+    small = np.zeros((W // 2) * (H // 2) * 3, np.uint8)
+    _PAGE_LOCKED.append(small)
+    assert not renderer.read_rgb8_lagged(small)
+    renderer.collect_stats()

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(sptr.EXPORTS)
-    assert L.sptr_abi_version() == 8
+    assert L.sptr_abi_version() == 9
 
 
 def test_no_device_means_loud_failure():
