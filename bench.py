@@ -664,6 +664,10 @@ def main():
     if rank == 0 and shards == 1:
         ref_rgb = torch.from_numpy(r.read_rgb8().reshape(-1)).to(dev)
         image_bytes_differing = int((ref_rgb != image_timed).sum().item())
+    if distributed:  # every rank's differing tile words
+        diff = torch.tensor([tile_words_differing], dtype=torch.int64, device=dev)
+        dist.all_reduce(diff)
+        tile_words_differing = int(diff.item())
     output_check = {"reference": "untimed render of the same frame, default flags, synchronous",
                     "identical": tile_words_differing == 0 and not image_bytes_differing,
                     "tile_words_differing": tile_words_differing, "image_bytes_differing": image_bytes_differing}
@@ -695,7 +699,12 @@ def main():
     # launches' own durations (roofline_one_chain)
     lanes_info = r.pixel_lanes_info()
     stats_one = None
-    if lanes_info["active"] and not args.no_serial_pass and args.integrator == "wavefront":
+    one_chain_pass = lanes_info["active"] and not args.no_serial_pass and args.integrator == "wavefront"
+    if distributed:  # (its steps gather: every rank runs it or none)
+        flag = torch.tensor([1 if one_chain_pass else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        one_chain_pass = bool(flag.item())
+    if one_chain_pass:
         r.set_pixel_lanes(1)
         step(timing)
         r.collect_stats()

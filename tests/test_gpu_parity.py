@@ -914,6 +914,52 @@ def test_pixel_lanes_graph_replay(renderer):
     assert np.array_equal(one[1], two[1])
 
 
+def test_pixel_lanes_follow_shading_changes(renderer):
+    """The lane context reads its parent's shading state (materials, lights, environment, debug mode)
+    instead of holding copies: after each change — with the lane's launch graph captured before it
+    (launch mode 3) — the two-lane image must equal the one-chain image, and must have changed."""
+    W, H = 160, 96
+    cam = sptr.camera_lookat(aspect=W / H)
+    faces = np.random.default_rng(5).random((6, 16, 16, 3), dtype=np.float32) * 2.0
+
+    def run(lanes):
+        out = []
+        sptr.setup_default(renderer, "default_emitter")
+        renderer.set_launch_mode(3)
+        renderer.set_pixel_lanes(lanes)
+        for step in range(5):
+            if step == 1:
+                lights = sptr.default_lights()
+                lights[0].intensity = 0.5
+                renderer.set_lights(lights)
+            elif step == 2:
+                mats = sptr.preset_materials(True)
+                mats[0].albedo[0], mats[0].albedo[1], mats[0].albedo[2] = 0.9, 0.1, 0.1
+                renderer.set_materials(mats)
+            elif step == 3:
+                renderer.set_environment(faces)
+            elif step == 4:
+                renderer.set_debug_mode(1)
+            for _ in range(3):  # (the shape is captured on its second call and replayed on its third)
+                renderer.render(cam, W, H, spp=4)
+            out.append(renderer.read_rgb8().copy())
+        renderer.set_debug_mode(0)
+        renderer.set_environment(None)
+        return out
+
+    try:
+        one = run(1)
+        two = run(2)
+    finally:
+        renderer.set_pixel_lanes(0)
+        renderer.set_launch_mode(0)
+        renderer.set_debug_mode(0)
+    for i, (a, b) in enumerate(zip(one, two)):
+        assert np.array_equal(a, b), f"step {i}: two lanes differ from one chain"
+        if i:
+            assert not np.array_equal(two[i], two[i - 1]), f"step {i}: the change had no effect"
+
+
 @pytest.mark.gpu
 def test_ray_accounting_fused_bounces(renderer):
     """Every closest-hit query is a camera ray (one per sample, culled or not), a bounce ray of a trace
