@@ -2425,6 +2425,125 @@ __global__ void __launch_bounds__(kBlock, SPTR_BOUNCE_WAVES)
   if constexpr (kTimed) ktime_end(w);
 }
 
+// --------------------------------------------------------------------------------- k_bounce01
+// The shading of bounce 0's hits and the whole of bounce 1 in one launch (LDS-staged one-light scenes whose
+// bounces fuse, after a lane-group or pixel-major bounce 0): per hit record of bounce 0, k_shade<primary,
+// fuse>'s steps (the path's camera ray recomputed from its id, emission, the light's contribution if its
+// in-place shadow ray is unoccluded, the continuation), then k_bounce's steps on that continuation, with the
+// path's radiance held in a register in between — the same float operations in the same order as the two
+// launches, which wrote it to rad[p] and read it back.  Every hit of bounce 0 continues (Russian roulette
+// starts after bounce 2), so the lanes stay as full as k_shade's.  Input: the hit records of w.segH (the
+// bounce-0 trace's); output: the rays of bounce 2 in w.segN / rs[0].  No continuation ray of bounce 1 is
+// written or read back, and the k_shade launch and its tail are gone.  
+#ifndef SPTR_BOUNCE01_WAVES
+#define SPTR_BOUNCE01_WAVES 5
+#endif
+template <bool kCube, bool kTimed = false>
+__global__ void __launch_bounds__(kBlock, SPTR_BOUNCE01_WAVES)
+    k_bounce01(SceneView sv, ShadeView sh, FrameView fin, WaveView w, uint32_t nseg_in) {
+  if constexpr (kTimed) ktime_begin(w);
+  const FrameView f = frame_dyn(fin);
+  extern __shared__ float4 lds[];
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds + sv.lds_bytes / 16u);
+  __shared__ DevMaterial smat[32];
+  __shared__ uint32_t s_cnt_n, s_rays, s_traced;
+  __shared__ LdsStack s_stack;
+  const uint32_t nm = stage_materials(sh, smat);
+  if (threadIdx.x == 0) s_cnt_n = s_rays = s_traced = 0u;
+  const Staged sc = stage_scene<true>(sv, lds);
+  uint32_t per_in = 0u;
+  const uint32_t n = seg_scan(w.segH, nseg_in, s_off, per_in);
+  const RayStream rout = w.rs[0];
+  const bool last1 = 1u >= f.max_depth, last2 = 2u >= f.max_depth;
+  const ImageDiv idiv = image_div(f);
+  Visits vc;
+  uint32_t rays = 0u, traced = 0u;
+  const Sched sd = block_sched(n);
+  for (uint32_t base = sd.first; base < sd.end; base += sd.step) {
+    const uint32_t i = base + threadIdx.x;
+    bool cont = false, active = i < n;
+    uint32_t p = 0u, rng = 0u;
+    vec3 thr = v3(1.0f, 1.0f, 1.0f), radv = v3(0.0f, 0.0f, 0.0f), ro, rd;
+    if (active) {  // bounce 0's shading (k_shade<true, true>)
+      uint3 h;
+      w.hrec.get(seg_slot(s_off, nseg_in, per_in, i), h.x, h.y, h.z);
+      p = h.x;
+      Primary pr;
+      primary_path(f, idiv, p, pr);
+      rng = pr.rng;
+      if (sh.debug_mode == 1) {
+        radv = v3(1.0f, 1.0f, 1.0f);
+        active = false;
+      } else {
+        const Surface sf = surface_at(sv, sh, smat, nm, f.cam_pos, pr.d, __uint_as_float(h.y), h.z);
+        const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
+        if (dot(emission, emission) > 0.0f) radv = radv + thr * emission;
+        vec3 so, ldir, contrib;
+        float stfar = 0.0f;
+        const bool lit = light_faces(sh.lights[0], sf) && light_term(sh.lights[0], sf, -pr.d, thr, so, ldir, stfar, contrib);
+        active = continue_path(sf, pr.d, 0u, thr, rng, ro, rd) && !last1;
+        if (lit) {
+          uint32_t sref = kNoHit;
+          ++rays;
+          if (!traverse_w<false, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, stfar, sref, vc, s_stack)) radv = radv + contrib;
+        }
+      }
+    }
+    bool lit = false;
+    vec3 no, nd, so, ldir, contrib;
+    float stfar = 0.0f;
+    if (active) {  // bounce 1 (k_bounce, depth 1): radv holds what rad[p] would
+      ++traced;
+      float tfar = __builtin_huge_valf();
+      uint32_t ref = kNoHit;
+      if (!traverse_w<false, false, false>(sc, sv, make_ray(ro, rd), 0.0f, tfar, ref, vc, s_stack)) {
+        radv = radv + thr * env_color<kCube>(sh.env, renormalized_again(rd));
+      } else {
+        const Surface sf = surface_at(sv, sh, smat, nm, ro, rd, tfar, ref);
+        const vec3 emission = v3(sf.m.emission[0], sf.m.emission[1], sf.m.emission[2]);
+        if (dot(emission, emission) > 0.0f) radv = radv + thr * emission;
+        if (light_faces(sh.lights[0], sf)) lit = light_term(sh.lights[0], sf, -rd, thr, so, ldir, stfar, contrib);
+        cont = continue_path(sf, rd, 1u, thr, rng, no, nd) && !last2;
+      }
+    }
+    const uint32_t jn = block_append(&s_cnt_n, cont);
+    if (cont && sd.seg0 + jn >= w.seg_cap) {
+      cont = false;
+      w.tot[kTotOverflow] = 1ull;  // cannot happen (ensure_wave slack); reported, never written
+    }
+    if (cont) {
+      rout.o[sd.seg0 + jn] = f4(no, __uint_as_float(rng));
+      rout.d[sd.seg0 + jn] = f4(nd, __uint_as_float(p));
+      rout.thr[sd.seg0 + jn] = f4(thr, 0.0f);
+    }
+    if (lit) {
+      uint32_t sref = kNoHit;
+      ++rays;
+      if (!traverse_w<false, true, false>(sc, sv, make_ray(so, ldir), 1e-4f, stfar, sref, vc, s_stack)) radv = radv + contrib;
+    }
+    if (i < n) w.rad[p] = f4(radv, 0.0f);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    rays += __shfl_xor(rays, off);
+    traced += __shfl_xor(traced, off);
+  }
+  if (lane_id() == 0u) {
+    atomicAdd(&s_rays, rays);
+    atomicAdd(&s_traced, traced);
+  }
+  report_stack(vc, w.tot);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    w.segN.cnt[logical_block()] = s_cnt_n;
+    w.bstat[blockIdx.x] += s_rays;
+    if (blockIdx.x == 0) *w.segN.per = sd.per;
+    atomicAdd(&w.tot[kTotClosest], (unsigned long long)s_traced);
+    atomicAdd(&w.tot[kTotTracedF], (unsigned long long)s_traced);
+    atomicAdd(&w.tot[kTotTracedD + 1], (unsigned long long)s_traced);
+  }
+  if constexpr (kTimed) ktime_end(w);
+}
+
 // --------------------------------------------------------------------------------- k_shadow
 // One thread per shadow record: any-hit test of each of its light tasks in light order; the
 // unoccluded contributions are added to rad[p] (Light::isOccluded, Light.cpp:21-40).  Any-hit
@@ -3831,6 +3950,21 @@ unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView
         return [&]<bool Cube, bool T>(Flags<Cube, T>) {
           const unsigned g = resident_grid((const void*)&k_bounce<Cube, T>, lb);
           SPTR_TIMED_LAUNCH((k_bounce<Cube, T>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, depth, nseg);
+          return g;
+        }(fl);
+      },
+      Flags<>{}, sh.env.env != nullptr, w.tslot != nullptr);
+}
+
+unsigned launch_bounce01(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w_in, uint32_t nseg,
+                         hipStream_t s) {
+  const WaveView w = with_tslot(w_in);
+  const unsigned lb = sv.lds_bytes + (4u * (nseg + 1u) + 15u) / 16u * 16u;
+  return dispatch(
+      [&](auto fl) -> unsigned {
+        return [&]<bool Cube, bool T>(Flags<Cube, T>) {
+          const unsigned g = resident_grid((const void*)&k_bounce01<Cube, T>, lb);
+          SPTR_TIMED_LAUNCH((k_bounce01<Cube, T>), dim3(g), dim3(kBlock), lb, s, sv, sh, f, w, nseg);
           return g;
         }(fl);
       },

@@ -337,8 +337,7 @@ struct StageTimer {
   bool quiet = false, quiet_open = false;  // untimed launch with dispatch events (run_call)
   void begin(int stage) {
     if (quiet && !on && !capturing && one_launch(stage)) {
-      if (c.time_by_events) g_launch_timing = LaunchTiming{c.quiet_ev[0], c.quiet_ev[1]};
-      else g_tslot = static_cast<unsigned long long*>(c.tslots.p) + (size_t)kTimeSlotWords * kTimeSlots;  // (never read)
+      g_launch_timing = LaunchTiming{c.quiet_ev[0], c.quiet_ev[1]};
       quiet_open = true;
       return;
     }
@@ -371,7 +370,6 @@ struct StageTimer {
     if (quiet_open) {
       quiet_open = false;
       g_launch_timing = LaunchTiming{};  // (taken by the launch; cleared if there was none)
-      g_tslot = nullptr;
       return;
     }
     if (open == SIZE_MAX) return;
@@ -850,6 +848,20 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
           launch_strag(sv, sh, fv, w, d, s);
         }
       }
+#ifndef SPTR_BOUNCE01
+#define SPTR_BOUNCE01 1
+#endif
+      if (SPTR_BOUNCE01 && d == 0 && fuse_from == 1 && T >= 2 && D >= 2) {
+        // bounce 0's shading and bounce 1 in one launch (k_bounce01): its rays of bounce 2 go to w.segN,
+        // so the fused bounces from 2 on start from that table
+        tm.begin(9);
+        g_shade = launch_bounce01(sv, sh, fv, w, g_trace, s);
+        tm.end();
+        rays_tab = w.segN;
+        spare_tab = w.segH;
+        d = 1;
+        continue;
+      }
       tm.begin(d == 0 ? 6 : 2);
       g_shade = launch_shade(sv, sh, fv, w, d, g_trace, fuse, s);
       tm.end();
@@ -1032,10 +1044,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     // untimed two-lane calls launch their trace and fused-bounce kernels with dispatch events all the same
     // (two events reused by every such launch, never read): r06l, C2 2.512-2.531 vs 2.548-2.565 ms per step
     // with plain launches, on one box
-#ifndef SPTR_QUIET_SLOTS
-#define SPTR_QUIET_SLOTS 0
-#endif
-    tm.quiet = !timing && (c.time_by_events ? c.quiet_ev[1] != nullptr : (SPTR_QUIET_SLOTS && c.tslots.p != nullptr));
+    tm.quiet = !timing && c.time_by_events && c.quiet_ev[1] != nullptr;
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
@@ -1321,8 +1330,8 @@ static int create_one(int device, sptr_ctx** out, const sptr_ctx* parent) {
   int khz = 0;
   if (ensure_buf(c.wb.seg, seg_table_bytes()) != hipSuccess || ensure_buf(c.w_tot, kTotWords * 8) != hipSuccess ||
       ensure_buf(c.dyn, kDynBytes) != hipSuccess || hipMemset(c.wb.seg.p, 0, seg_table_bytes()) != hipSuccess ||
-      ensure_buf(c.tslots, (size_t)(kTimeSlots + 1) * kTimeSlotWords * 8) != hipSuccess ||
-      hipMemset(c.tslots.p, 0, (size_t)(kTimeSlots + 1) * kTimeSlotWords * 8) != hipSuccess ||
+      ensure_buf(c.tslots, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
+      hipMemset(c.tslots.p, 0, (size_t)kTimeSlots * kTimeSlotWords * 8) != hipSuccess ||
       hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) {
     delete x;
     return SPTR_ERR_OOM;

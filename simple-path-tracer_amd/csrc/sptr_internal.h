@@ -378,8 +378,7 @@ struct Context {
   uint32_t strag_lanes = kStragLanesDefault;  // sptr_set_stragglers (0: no hand-off)
   uint64_t epoch = 1;                // bumped by every state change a captured graph depends on
   DevBuf dyn;                        // per-call {frame_begin, reset, total} (k_frame_dyn)
-  DevBuf tslots;                     // [kTimeSlots + 1][kTimeSlotWords] launch timing slots, zeroed (the last
-                                     // one is written by untimed launches and never read: StageTimer::quiet)
+  DevBuf tslots;                     // [kTimeSlots][kTimeSlotWords] launch timing slots, zeroed
   uint32_t tslots_used = 0;          // slots handed out in this collection window
   double wall_khz = 0.0;             // the device wall clock's rate (wall_clock64 ticks per ms)
   bool time_by_events = false;       // one-launch stages timed by dispatch events, not slots (pixel lanes)
@@ -465,6 +464,10 @@ bool shade_fuses_shadows(const SceneView& sv, const ShadeView& sh, bool count);
 bool shadow_overlaps(const SceneView& sv, const WaveView& w);
 unsigned launch_shade(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                       uint32_t nseg, bool fuse, hipStream_t s);
+// bounce 0's shading and bounce 1 in one launch (k_bounce01): bounce 0's hit records of w.segH in, the rays
+// of bounce 2 out in w.segN / rs[0]
+unsigned launch_bounce01(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, uint32_t nseg,
+                         hipStream_t s);
 // one fused bounce (k_bounce): rays of w.segN in, continuation rays of w.segH out
 unsigned launch_bounce(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, int depth,
                        uint32_t nseg, hipStream_t s);
