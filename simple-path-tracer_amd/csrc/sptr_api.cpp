@@ -848,12 +848,12 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
           launch_strag(sv, sh, fv, w, d, s);
         }
       }
-#ifndef SPTR_BOUNCE01
-#define SPTR_BOUNCE01 1
-#endif
-      if (SPTR_BOUNCE01 && d == 0 && fuse_from == 1 && T >= 2 && D >= 2) {
-        // bounce 0's shading and bounce 1 in one launch (k_bounce01): its rays of bounce 2 go to w.segN,
-        // so the fused bounces from 2 on start from that table
+      if (d == 0 && fuse && !no_bounce && T >= 2 && D >= 2) {
+        // bounce 0's shading and bounce 1 in one launch (k_bounce01), in batches of every size: its rays of
+        // bounce 2 go to w.segN, where the fused bounces from 2 on (or k_trace(2)) take them.  r06 A/B on one
+        // box: C2 (two lanes, fused bounces) 2.58-2.60 -> 2.36 ms/step, 8-way shard 0.52 -> 0.49; C4 (batches
+        // of 535 M paths, separate stages from bounce 2) 136.6 -> 122.4 ms, C2 as one chain 3.01 -> 2.76
+        // (gpurun_out/r06p, r06q)
         tm.begin(9);
         g_shade = launch_bounce01(sv, sh, fv, w, g_trace, s);
         tm.end();
