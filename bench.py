@@ -175,10 +175,15 @@ def roofline(cnt, stats, layout, wl_name, steps, env_bytes=0):
     # fused bounce rays (k_bounce): the visit-count pass runs them as separate trace launches, so its
     # bounce hit fraction and visits per ray apply to them
     stream += tf * (hb * FUSED_HIT_BYTES + (1.0 - hb) * FUSED_MISS_BYTES)
+    # the fused bounce-1 rays of k_bounce01 (LDS scenes: every fused chain starts with it) read a 12-B
+    # bounce-0 hit record instead of a 48-B ray + throughput
+    residency, footprint = _residency(layout)
+    t01 = sum(list(getattr(s, "traced_by_depth", [0, 0]))[1] for s in stats) if residency == "lds" and tf else 0
+    stream -= t01 * (RAY_READ_BYTES + THR_READ_BYTES - HIT_RECORD_BYTES)
     stream += env_hbm_bytes(tp * (1.0 - hp) + (tb + tf) * (1.0 - hb), env_bytes, launches)
     stream_read = (tb * (RAY_READ_BYTES + (1.0 - hb) * (THR_READ_BYTES + RAD_BYTES))
-                   + tf * (RAY_READ_BYTES + THR_READ_BYTES + RAD_BYTES))  # coalesced reads
-    residency, footprint = _residency(layout)
+                   + tf * (RAY_READ_BYTES + THR_READ_BYTES + RAD_BYTES)
+                   - t01 * (RAY_READ_BYTES + THR_READ_BYTES - HIT_RECORD_BYTES))  # coalesced reads
     scene = {"lds": 0.0, "l2": XCDS * footprint * launches, "hbm": scene_p * tp + scene_b * (tb + tf)}[residency]
     # straggler hand-off (hbm scenes): the rest of a handed-off ray's walk runs in k_strag, not in the
     # trace launch; its visits (counted in every call) are not the trace launch's bytes

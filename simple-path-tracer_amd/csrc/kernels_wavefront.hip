@@ -1523,6 +1523,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // global queue in k_cull's order measured slower, r04f).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
 // 289 us, 8 lanes 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
+#ifndef SPTR_WP_LDS_FOLD
+#define SPTR_WP_LDS_FOLD 0
+#endif
 // kHiOcc: 8 waves/SIMD for shards whose pixels fill the resident waves only a few times (r04u: the
 // 8-way C2 shard 0.554 -> 0.541 ms, while 2- and 4-way shards lose ~1.5 % at 8 waves)
 template <bool kLds, bool kCount, bool kW4, bool kCube, bool kHiOcc = false, bool kTimed = false>
@@ -1534,6 +1537,9 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
+#if SPTR_WP_LDS_FOLD
+  __shared__ float4 s_fold[kBlock];
+#endif
   if (threadIdx.x == 0) s_cnt = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
@@ -1588,11 +1594,28 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
       const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
       const uint32_t nact = f.k - r * kFoldLanes < kFoldLanes ? f.k - r * kFoldLanes : kFoldLanes;
       const uint32_t nfold = fold ? (hm ? (uint32_t)__builtin_ctz(hm) : nact) : 0u;
+#if SPTR_WP_LDS_FOLD
+      // the group's values through LDS: one write per lane, and the group's first lane (the one that
+      // stores the sum) reads and adds them in sample order; the wave's own LDS accesses are in order
+      s_fold[threadIdx.x] = make_float4(rv.x, rv.y, rv.z, 0.0f);
+      __builtin_amdgcn_wave_barrier();
+      if (q == 0u) {
+#pragma unroll
+        for (uint32_t j = 0; j < kFoldLanes; ++j) {
+          if (j < nfold) {
+            const float4 v = s_fold[threadIdx.x + j];
+            a = v3(a.x + v.x, a.y + v.y, a.z + v.z);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#else
 #pragma unroll
       for (uint32_t j = 0; j < kFoldLanes; ++j) {
         const float vx = __shfl(rv.x, (int)(g0 + j)), vy = __shfl(rv.y, (int)(g0 + j)), vz = __shfl(rv.z, (int)(g0 + j));
         if (j < nfold) a = v3(a.x + vx, a.y + vy, a.z + vz);
       }
+#endif
       if (fold && hm) {
         fold = false;
         resume = r * kFoldLanes + nfold;
