@@ -1523,9 +1523,6 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : SPTR_TRACE_P
 // global queue in k_cull's order measured slower, r04f).  (Measured on the 8-way C2 shard: 4 lanes per pixel with DPP quad broadcasts
 // 289 us, 8 lanes 234 us, 64 lanes 449 us; path-major 196 us + 54 us more in k_accum.)
 constexpr uint32_t kFoldLanes = 8;  // samples per pixel per round = lanes per pixel group
-#ifndef SPTR_WP_LDS_FOLD
-#define SPTR_WP_LDS_FOLD 0
-#endif
 // kHiOcc: 8 waves/SIMD for shards whose pixels fill the resident waves only a few times (r04u: the
 // 8-way C2 shard 0.554 -> 0.541 ms, while 2- and 4-way shards lose ~1.5 % at 8 waves)
 template <bool kLds, bool kCount, bool kW4, bool kCube, bool kHiOcc = false, bool kTimed = false>
@@ -1537,9 +1534,7 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
   extern __shared__ float4 lds[];
   __shared__ uint32_t s_cnt;
   __shared__ uint32_t s_hist[kCount ? kHistBins : 1];
-#if SPTR_WP_LDS_FOLD
-  __shared__ float4 s_fold[kBlock];
-#endif
+  __shared__ float4 s_fold[kBlock];  // the round's values of the wave's pixel groups (the fold below)
   if (threadIdx.x == 0) s_cnt = 0u;
   if (kCount) hist_init(s_hist);
   const Staged sc = stage_scene<kLds>(sv, lds);
@@ -1594,9 +1589,10 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
       const uint32_t hm = (uint32_t)(__ballot(hit) >> g0) & ((1u << kFoldLanes) - 1u);
       const uint32_t nact = f.k - r * kFoldLanes < kFoldLanes ? f.k - r * kFoldLanes : kFoldLanes;
       const uint32_t nfold = fold ? (hm ? (uint32_t)__builtin_ctz(hm) : nact) : 0u;
-#if SPTR_WP_LDS_FOLD
       // the group's values through LDS: one write per lane, and the group's first lane (the one that
-      // stores the sum) reads and adds them in sample order; the wave's own LDS accesses are in order
+      // stores the sum) reads and adds them in sample order; the wave's own LDS accesses are in order.
+      // (r06: 24 shuffles per round before, with every lane of the group adding: C2 2.373-2.38 -> 2.321-2.331
+      // ms/step, the 8-way shard 0.481-0.504 -> 0.476-0.478, gpurun_out/r06s)
       s_fold[threadIdx.x] = make_float4(rv.x, rv.y, rv.z, 0.0f);
       __builtin_amdgcn_wave_barrier();
       if (q == 0u) {
@@ -1609,13 +1605,6 @@ __global__ void __launch_bounds__(kBlock, kW4 ? SPTR_TRACE4_WAVES : (kHiOcc ? 8 
         }
       }
       __builtin_amdgcn_wave_barrier();
-#else
-#pragma unroll
-      for (uint32_t j = 0; j < kFoldLanes; ++j) {
-        const float vx = __shfl(rv.x, (int)(g0 + j)), vy = __shfl(rv.y, (int)(g0 + j)), vz = __shfl(rv.z, (int)(g0 + j));
-        if (j < nfold) a = v3(a.x + vx, a.y + vy, a.z + vz);
-      }
-#endif
       if (fold && hm) {
         fold = false;
         resume = r * kFoldLanes + nfold;
@@ -2044,7 +2033,7 @@ __device__ __forceinline__ Surface surface_at(const SceneView& sv, const ShadeVi
   } else {
     const float4 c = sv.tris[3 * idx + 2];
     ng = v3(c.y, c.z, c.w);
-    mid = sh.geom_mat[sv.tri_geom[idx]];
+    mid = sh.tri_mat ? sh.tri_mat[idx] : sh.geom_mat[sv.tri_geom[idx]];
   }
   s.n = safe_normalize(ng);
   if (dot(s.n, rd) > 0.0f) s.n = -s.n;
@@ -4157,6 +4146,14 @@ void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uin
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,
                     hipStream_t s) {
   hipLaunchKernelGGL(k_resolve, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, accum, n, tiles, image);
+}
+
+__global__ void __launch_bounds__(kBlock) k_tri_materials(const uint32_t* tri_geom, const uint32_t* geom_mat, uint32_t n,
+                                                          uint32_t* tri_mat) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += grid_threads()) tri_mat[i] = geom_mat[tri_geom[i]];
+}
+void launch_tri_materials(const uint32_t* tri_geom, const uint32_t* geom_mat, uint32_t n, uint32_t* tri_mat, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_tri_materials, dim3(grid_for(n)), dim3(kBlock), 0, s, tri_geom, geom_mat, n, tri_mat);
 }
 
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,

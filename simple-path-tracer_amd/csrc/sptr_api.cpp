@@ -130,6 +130,19 @@ int resolve_geom_materials(Context& c) {
   }
   API_HIP(ensure_buf(c.geom_mat, t.size() * 4));
   API_HIP(hipMemcpy(c.geom_mat.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  // scenes traversed from L2/HBM: the material of every triangle slot, so that shading a hit loads it
+  // directly instead of the slot's geomID and then its material
+#ifndef SPTR_TRI_MAT
+#define SPTR_TRI_MAT 1
+#endif
+  free_buf(c.tri_mat);
+  if (SPTR_TRI_MAT && scene_view(c).lds_bytes == 0u && c.num_tri_refs) {
+    API_HIP(ensure_buf(c.tri_mat, (size_t)c.num_tri_refs * 4));
+    launch_tri_materials(static_cast<const uint32_t*>(c.tri_geom.p), static_cast<const uint32_t*>(c.geom_mat.p),
+                         c.num_tri_refs, static_cast<uint32_t*>(c.tri_mat.p), c.stream);
+    API_HIP(hipGetLastError());
+    API_HIP(hipStreamSynchronize(c.stream));
+  }
   return SPTR_OK;
 }
 
@@ -279,6 +292,7 @@ ShadeView shade_view(const Context& cc) {
   s.mats = static_cast<const DevMaterial*>(c.mats.p);
   s.num_mats = (uint32_t)c.mats_host.size();
   s.geom_mat = static_cast<const uint32_t*>(c.geom_mat.p);
+  s.tri_mat = cc.parent ? nullptr : static_cast<const uint32_t*>(c.tri_mat.p);  // (slots are the owner's)
   s.num_lights = (uint32_t)c.lights_host.size();
   for (uint32_t i = 0; i < s.num_lights; ++i) s.lights[i] = c.lights_host[i];
   s.env.env = static_cast<const float4*>(c.env.p);
@@ -652,10 +666,6 @@ uint32_t enqueue_path_per_thread(Context& c, const sptr_frame& f, hipStream_t s,
   return launches;
 }
 
-#ifndef SPTR_FUSE_BOUNCE_LOG2
-#define SPTR_FUSE_BOUNCE_LOG2 26
-#endif
-constexpr uint64_t kFuseBouncePaths = 1ull << SPTR_FUSE_BOUNCE_LOG2;
 
 // launches overlapped on the side streams (launch mode 2: everything on one stream)
 bool overlap_enabled(const Context& c) {
@@ -762,10 +772,11 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     // (r04s: handing them to k_sky beside the thread-per-pixel bounce 0 too: C2 3.09-3.20 -> 3.54-3.57 ms)
     fv.sky_fold = (fv.cull != nullptr && fv.pixel_major == kFoldNone) ? 1u : 0u;
     fv.plist = fv.sky_fold ? static_cast<const uint32_t*>(c.plist.p) : nullptr;
-    // fused bounces (k_bounce) pay off where launches are short: measured on C2 (r02 bounce_ab),
-    // 8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822 (66 M paths), but 1 GPU (133 M paths)
-    // 3.39 -> 3.46 ms: the fused kernel runs the traversal at the shading kernel's occupancy
-    const bool fuse_bounce = fuse && !no_bounce && (uint64_t)fv.P * kk <= kFuseBouncePaths;
+    // fused bounces (k_bounce), in batches of every size since r06: r02 measured them on C2 only where
+    // launches are short (8-way shard 0.627 -> 0.590 ms, 2-way 1.887 -> 1.822, but 1 GPU (133 M paths) 3.39
+    // -> 3.46 ms: the traversal at the shading kernel's occupancy); after k_bounce01 they gain on the large
+    // batches too (r06s: C4, 535 M-path batches, 122.2-122.6 -> 119.2-119.4 ms/step; C2 unchanged)
+    const bool fuse_bounce = fuse && !no_bounce;
     // larger batches could fuse only their late bounces, whose queues are short: no gain measured
     // (r03zx, SPTR_FUSE_FROM 2/3/4 on C2: 3.16-3.25 vs 3.17 ms/step)
     const int fuse_from = fuse_bounce ? 1 : ((fuse && !no_bounce && fuse_from_env > 0) ? fuse_from_env : D + 1);
@@ -1368,7 +1379,7 @@ int sptr_destroy(sptr_ctx* x) {
   if (c.pending) (void)hipStreamSynchronize(c.pending_stream);
   if (c.stream) (void)hipStreamSynchronize(c.stream);
   DevBuf* bufs[] = {&c.nodes,  &c.prim_ref, &c.tris,  &c.sph,   &c.tri_geom, &c.sph_geom, &c.tri_orig,
-                    &c.sph_orig, &c.geom_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
+                    &c.sph_orig, &c.geom_mat, &c.tri_mat, &c.mats, &c.env, &c.w_tot,  &c.accum,   &c.tiles,
                     &c.image,    &c.qbuf,     &c.nodes4, &c.cull, &c.plist, &c.tslots};
   for (DevBuf* b : bufs) free_buf(*b);
   for (DevBuf* b : {&c.wb.hrec, &c.wb.rad, &c.wb.stask, &c.wb.seg, &c.wb.strag}) free_buf(*b);

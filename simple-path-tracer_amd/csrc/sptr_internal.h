@@ -134,6 +134,9 @@ struct ShadeView {
   const DevMaterial* mats;
   uint32_t num_mats;
   const uint32_t* geom_mat;  // geomID -> material index, resolved as MaterialManager::getMaterialFromHit
+  // triangle slot -> material index (geom_mat[tri_geom[slot]], precomputed): scenes traversed from L2/HBM,
+  // where the shading of a hit saves a dependent load; null elsewhere
+  const uint32_t* tri_mat;
   uint32_t num_lights;
   DevLight lights[kMaxLights];
   EnvView env;
@@ -396,6 +399,7 @@ struct Context {
   uint32_t tail_depth = 0;  // first bounce traced path-per-thread by k_tail (0 = automatic)
   // scene
   DevBuf nodes, prim_ref, tris, sph, tri_geom, sph_geom, tri_orig, sph_orig, geom_mat;
+  DevBuf tri_mat;  // ShadeView::tri_mat (resolve_geom_materials)
   uint32_t leaf_size = 0;  // max primitives per BVH leaf range (1..16); 0 = automatic
   uint32_t bvh_width = 0;  // traversal width: 2 (LBVH as built), 4 (collapsed), 0 = automatic
   uint32_t leaf_used = 0;  // leaf size the current BVH was built with
@@ -511,6 +515,8 @@ void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView
 void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
 void launch_unpack(const uint32_t* gathered, int G, uint32_t tiles_per_rank, int W, int H, uint8_t* rgb,
                    hipStream_t s);
+// tri_mat[i] = geom_mat[tri_geom[i]], i < n
+void launch_tri_materials(const uint32_t* tri_geom, const uint32_t* geom_mat, uint32_t n, uint32_t* tri_mat, hipStream_t s);
 void launch_query(const SceneView& sv, const uint32_t* tri_orig, const uint32_t* sph_orig, const float* rays, uint32_t n,
                   bool anyhit, uint32_t* ref, float* t, float* ng, uint8_t* occ, uint32_t* stack_overflow, hipStream_t s);
 void launch_primary(const FrameView& f, float* dirs, uint32_t* rng, hipStream_t s);
