@@ -22,7 +22,7 @@ import sys
 
 # position of the kCount template argument per kernel
 COUNT_ARG = {"k_trace_pm": 0, "k_trace": 1, "k_trace_wp": 1, "k_trace_dyn": 1, "k_shadow": 1, "k_shadow_dyn": 0,
-             "k_bounce": None}  # (k_bounce: no count instantiation; the visit-count pass runs no fused bounce)
+             "k_bounce": None, "k_bounce01": None}  # (no count instantiations: the visit-count pass fuses nothing)
 FAMILY = {"k_trace": ("k_trace", "k_bounce"), "k_shadow": ("k_shadow",)}
 
 
