@@ -61,11 +61,11 @@
 #endif
 #define SPTR_STR2(x) #x
 #define SPTR_STR(x) SPTR_STR2(x)  // a register name for an occupancy cap's clobber list
-// A launch timed by the stage timer (g_launch_timing set: the dispatch records its start and end into
-// the two events), else a plain launch.
+// A launch timed by the stage timer (g_launch_timing set: the dispatch records its start and/or end into
+// the events), else a plain launch.
 #define SPTR_TIMED_LAUNCH(kern, grid, block, lds, stream, ...)                                              \
   do {                                                                                                   \
-    if (g_launch_timing.start) {                                                                         \
+    if (g_launch_timing.start || g_launch_timing.stop) {                                                 \
       const LaunchTiming lt_ = g_launch_timing;                                                          \
       g_launch_timing = LaunchTiming{};                                                                  \
       hipExtLaunchKernelGGL(kern, grid, block, lds, stream, lt_.start, lt_.stop, 0u, __VA_ARGS__);         \
@@ -4092,7 +4092,7 @@ void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
 
 void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
                       hipStream_t s) {
-  hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total, clear);
+  SPTR_TIMED_LAUNCH(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total, clear);
 }
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 
@@ -4139,8 +4139,8 @@ void launch_interleave_tiles(const uint32_t* a, uint32_t na, const uint32_t* b, 
 
 void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,
                        bool resolve, hipStream_t s) {
-  if (resolve) hipLaunchKernelGGL(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
-  else hipLaunchKernelGGL(k_accum<false>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
+  if (resolve) SPTR_TIMED_LAUNCH(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
+  else SPTR_TIMED_LAUNCH(k_accum<false>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
 }
 
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,

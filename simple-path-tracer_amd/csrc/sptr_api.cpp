@@ -310,6 +310,9 @@ ShadeView shade_view(const Context& cc) {
 // shading of a bounce in one launch, counted with the trace launches); 0-9 with SPTR_FRAME_TIMING,
 // 1, 3, 5 and 9 with SPTR_FRAME_TIMING_TRACE.
 constexpr int kStages = 10;
+#ifndef SPTR_CALL_SPAN
+#define SPTR_CALL_SPAN 1  // untimed direct calls' span: 0 = event records, 1 = dispatch events, 2 = none (A/B)
+#endif
 struct StageTimer {
   Context& c;
   bool on;                  // SPTR_FRAME_TIMING or SPTR_FRAME_TIMING_TRACE
@@ -401,13 +404,37 @@ struct StageTimer {
     c.marks[open].e = next();
     open = SIZE_MAX;
   }
+  // The call span of an untimed direct call: the dispatch events of its first launch (k_frame_dyn, start)
+  // and its last (k_accum, end) instead of two event records between launches.
+  size_t call_b = SIZE_MAX, call_e = SIZE_MAX;
+  bool span_by_launch = false, stop_set = false;
+  void pre_call() {  // right before the call's first launch
+    if (SPTR_CALL_SPAN != 1 || on || capturing) return;
+    call_b = alloc();
+    call_e = alloc();
+    if (call_b == SIZE_MAX || call_e == SIZE_MAX) return;
+    span_by_launch = true;
+    g_launch_timing = LaunchTiming{c.events[call_b], nullptr};
+  }
   void begin_call() {  // (a replayed graph's call span is recorded around its launch: run_call)
     if (capturing || (on && trace_only)) return;  // SPTR_FRAME_TIMING_TRACE: the trace spans only
+    if (SPTR_CALL_SPAN == 2 && !on) return;
     call = c.marks.size();
-    c.marks.push_back(StageMark{0, next(), SIZE_MAX});
+    c.marks.push_back(StageMark{0, span_by_launch ? call_b : next(), SIZE_MAX});
+  }
+  void last_launch() {  // right before the call's last launch on s
+    if (!span_by_launch || call == SIZE_MAX) return;
+    g_launch_timing.stop = c.events[call_e];
+    stop_set = true;
   }
   void end_call() {
-    if (call != SIZE_MAX) c.marks[call].e = next();
+    if (call == SIZE_MAX) return;
+    if (stop_set && g_launch_timing.stop != c.events[call_e]) {  // taken by the last launch
+      c.marks[call].e = call_e;
+      return;
+    }
+    if (stop_set) g_launch_timing = LaunchTiming{};
+    c.marks[call].e = next();
   }
 };
 
@@ -896,6 +923,7 @@ uint32_t enqueue_wavefront(Context& c, const sptr_frame& f, uint32_t k, int T, h
     if (join_sky) check(hipStreamWaitEvent(s, ev.sky, 0), "sky join wait");
     join_sky = false;
     tm.begin(4);
+    if (done + kk >= f.spp) tm.last_launch();
     launch_accumulate(fv, w, static_cast<float4*>(c.accum.p), static_cast<uint32_t*>(c.tiles.p),
                       c.image_out ? c.image_out : static_cast<uint8_t*>(c.image.p), resolve, s);
     tm.end();
@@ -1056,6 +1084,7 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     // (two events reused by every such launch, never read): r06l, C2 2.512-2.531 vs 2.548-2.565 ms per step
     // with plain launches, on one box
     tm.quiet = !timing && c.time_by_events && c.quiet_ev[1] != nullptr;
+    tm.pre_call();
     launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
