@@ -248,12 +248,15 @@ __device__ __forceinline__ FrameView frame_dyn(FrameView f) {
   return f;
 }
 // clear (may be null): the two words after an in-sequence k_cull's list (its unculled pixel count and a
-// spare), zeroed here instead of by a memset node of their own.
-__global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear) {
+// spare), zeroed here instead of by a memset node of their own.  t0 (may be null): the start word of the
+// call span's timing slot (the call's last k_accum takes its end, ktime_end).
+__global__ void k_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
+                            unsigned long long* t0) {
   if (threadIdx.x == 0) {
     dyn[0] = frame_begin;
     dyn[1] = reset;
     dyn[2] = total;
+    if (t0) t0[0] = (unsigned long long)wall_clock64();
   }
   if (threadIdx.x == 0) {
     if (clear) {
@@ -3168,6 +3171,7 @@ __global__ void __launch_bounds__(kBlock) k_accum(FrameView fin, WaveView w, flo
       atomicAdd(&w.tot[kTotTail], c);
     }
   }
+  ktime_end(w);  // (w.tslot: the end of an untimed call's span, whose start k_frame_dyn stored)
 }
 
 __global__ void __launch_bounds__(kBlock) k_resolve(FrameView f, const float4* accum, uint32_t n_arg, uint32_t* tiles,
@@ -4091,8 +4095,8 @@ void launch_optix(const SceneView& sv, const ShadeView& sh, const FrameView& f, 
 }
 
 void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
-                      hipStream_t s) {
-  SPTR_TIMED_LAUNCH(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total, clear);
+                      unsigned long long* t0, hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_dyn, dim3(1), dim3(64), 0, s, dyn, frame_begin, reset, total, clear, t0);
 }
 const void* frame_dyn_kernel() { return (const void*)&k_frame_dyn; }
 
@@ -4137,10 +4141,11 @@ void launch_interleave_tiles(const uint32_t* a, uint32_t na, const uint32_t* b, 
                      reinterpret_cast<uint4*>(dst), n);
 }
 
-void launch_accumulate(const FrameView& f, const WaveView& w, float4* accum, uint32_t* tiles, uint8_t* image,
+void launch_accumulate(const FrameView& f, const WaveView& w_in, float4* accum, uint32_t* tiles, uint8_t* image,
                        bool resolve, hipStream_t s) {
-  if (resolve) SPTR_TIMED_LAUNCH(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
-  else SPTR_TIMED_LAUNCH(k_accum<false>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
+  const WaveView w = with_tslot(w_in);  // (the call span's end: the call's last k_accum)
+  if (resolve) hipLaunchKernelGGL(k_accum<true>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
+  else hipLaunchKernelGGL(k_accum<false>, dim3(grid_for(f.P)), dim3(kBlock), 0, s, f, w, accum, tiles, image);
 }
 
 void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_t* tiles, uint8_t* image,

@@ -404,36 +404,39 @@ struct StageTimer {
     c.marks[open].e = next();
     open = SIZE_MAX;
   }
-  // The call span of an untimed direct call: the dispatch events of its first launch (k_frame_dyn, start)
-  // and its last (k_accum, end) instead of two event records between launches.
-  size_t call_b = SIZE_MAX, call_e = SIZE_MAX;
-  bool span_by_launch = false, stop_set = false;
-  void pre_call() {  // right before the call's first launch
-    if (SPTR_CALL_SPAN != 1 || on || capturing) return;
-    call_b = alloc();
-    call_e = alloc();
-    if (call_b == SIZE_MAX || call_e == SIZE_MAX) return;
-    span_by_launch = true;
-    g_launch_timing = LaunchTiming{c.events[call_b], nullptr};
+  // The call span of an untimed direct wavefront call: a timing slot whose start the call's first launch
+  // (k_frame_dyn) stores and whose end its last (k_accum) takes, like a slot-timed launch's, instead of
+  // two event records, each of which idled the GPU for ~5 us (r06, kernel trace of the 8-way C2 shard:
+  // 475 us per step with them, 463 without; dispatch events on those two launches left the same gaps).
+  uint32_t call_slot = UINT32_MAX;
+  bool stop_set = false;
+  unsigned long long* slot_ptr(uint32_t i) const {
+    return static_cast<unsigned long long*>(c.tslots.p) + (size_t)kTimeSlotWords * i;
+  }
+  unsigned long long* pre_call(bool wavefront) {  // right before the call's first launch: its t0 word
+    if (SPTR_CALL_SPAN != 1 || !wavefront || on || capturing || !c.tslots.p || c.tslots_used >= kTimeSlots)
+      return nullptr;
+    call_slot = c.tslots_used++;
+    return slot_ptr(call_slot);
   }
   void begin_call() {  // (a replayed graph's call span is recorded around its launch: run_call)
     if (capturing || (on && trace_only)) return;  // SPTR_FRAME_TIMING_TRACE: the trace spans only
     if (SPTR_CALL_SPAN == 2 && !on) return;
     call = c.marks.size();
-    c.marks.push_back(StageMark{0, span_by_launch ? call_b : next(), SIZE_MAX});
+    if (call_slot != UINT32_MAX) c.marks.push_back(StageMark{0, SIZE_MAX, SIZE_MAX, call_slot});
+    else c.marks.push_back(StageMark{0, next(), SIZE_MAX});
   }
-  void last_launch() {  // right before the call's last launch on s
-    if (!span_by_launch || call == SIZE_MAX) return;
-    g_launch_timing.stop = c.events[call_e];
+  void last_launch() {  // right before the call's last launch on s (k_accum)
+    if (call_slot == UINT32_MAX || call == SIZE_MAX) return;
+    g_tslot = slot_ptr(call_slot);
     stop_set = true;
   }
   void end_call() {
     if (call == SIZE_MAX) return;
-    if (stop_set && g_launch_timing.stop != c.events[call_e]) {  // taken by the last launch
-      c.marks[call].e = call_e;
+    if (call_slot != UINT32_MAX) {  // (a slot whose end was not taken reads as 0 ms)
+      if (stop_set) g_tslot = nullptr;
       return;
     }
-    if (stop_set) g_launch_timing = LaunchTiming{};
     c.marks[call].e = next();
   }
 };
@@ -1084,8 +1087,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     // (two events reused by every such launch, never read): r06l, C2 2.512-2.531 vs 2.548-2.565 ms per step
     // with plain launches, on one box
     tm.quiet = !timing && c.time_by_events && c.quiet_ev[1] != nullptr;
-    tm.pre_call();
-    launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, s);
+    unsigned long long* t0 = tm.pre_call(key.frame.integrator == SPTR_INTEGRATOR_WAVEFRONT);
+    launch_frame_dyn(static_cast<uint32_t*>(c.dyn.p), frame_begin, reset, total, clear, t0, s);
     waves = enqueue(s, tm);
     API_HIP(hipGetLastError());
     if (tm.err != hipSuccess) return fail(c, SPTR_ERR_HIP, "render: " + tm.what + ": " + hipGetErrorString(tm.err));
@@ -1168,7 +1171,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
     void* dyn_ptr = c.dyn.p;
     uint32_t a0 = frame_begin, a1 = reset, a2 = total;
     uint32_t* a3 = clear;
-    void* args[5] = {&dyn_ptr, &a0, &a1, &a2, &a3};
+    unsigned long long* a4 = nullptr;  // (a replay's call span: event records around its launch)
+    void* args[6] = {&dyn_ptr, &a0, &a1, &a2, &a3, &a4};
     hipKernelNodeParams kp{};
     kp.func = const_cast<void*>(frame_dyn_kernel());
     kp.gridDim = dim3(1);
@@ -1194,7 +1198,8 @@ int run_call(Context& c, const GraphKey& key, uint32_t frame_begin, uint32_t res
   void* dyn_ptr = c.dyn.p;
   uint32_t a0 = frame_begin, a1 = reset, a2 = total;
   uint32_t* a3 = clear;
-  void* args[5] = {&dyn_ptr, &a0, &a1, &a2, &a3};
+  unsigned long long* a4 = nullptr;
+  void* args[6] = {&dyn_ptr, &a0, &a1, &a2, &a3, &a4};
   hipKernelNodeParams p = gc.dyn_params;
   p.kernelParams = args;
   p.extra = nullptr;

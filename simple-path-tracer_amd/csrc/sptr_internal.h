@@ -506,7 +506,7 @@ void launch_resolve(const FrameView& f, const float4* accum, uint32_t n, uint32_
                     hipStream_t s);
 // Head of every render call: the per-call values kernels read through FrameView::dyn.
 void launch_frame_dyn(uint32_t* dyn, uint32_t frame_begin, uint32_t reset, uint32_t total, uint32_t* clear,
-                      hipStream_t s);
+                      unsigned long long* t0, hipStream_t s);
 const void* frame_dyn_kernel();
 // PathTracer-mode frames (the k frames of f from f.acc0), one launch: accum += tonemapped frames.
 void launch_pathtracer(const SceneView& sv, const ShadeView& sh, const FrameView& f, const WaveView& w, hipStream_t s);
