@@ -471,6 +471,9 @@ def test_launch_graph_replay_equals_direct(renderer, integrator):
         assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
         assert (a[1], a[2]) == (b[1], b[2])
         assert b[5] > 0.0  # the call span's events were re-pointed and recorded on replay
+        # direct calls: the span of a wavefront call is its device wall-clock slot (k_frame_dyn's start, the last
+        # k_accum's end), of a path-per-thread call two event records
+        assert a[5] > 0.0
 
 
 @pytest.mark.parametrize("scene", ["default", "default_emitter"])
