@@ -540,6 +540,47 @@ def test_overlapped_launches_equal_serial(renderer, scene, p0, p1, spp):
             assert a[1:] == ref[1:], mode
 
 
+@pytest.mark.parametrize("nlights,depth", [(1, 6), (1, 32), (8, 32)])
+def test_many_lights_deep_paths_overlapped_equal_serial(renderer, nlights, depth):
+    """Scenes beyond an XCD's L2 with up to 8 lights (directional and point: 3-slot shadow tasks) and paths
+    up to the maximum depth (32, so the tail carries 29 bounces): the overlapped launch sequence (shadow
+    launches beside the next bounce trace, k_strag and k_sky beside the chain) in direct launches (modes 1
+    and 0) and a replayed graph (mode 3) gives the one-stream sequence's (mode 2) image and query counts bit
+    for bit.  (r06: this also covered a deferred tail, started beside the last shadow launch, measured
+    no faster and not kept)"""
+    W, H, S = 128, 96, 8
+    sptr.setup_default(renderer, "sphere_mesh", 300, 600)
+    lights = sptr.default_lights()
+    extra = []
+    for i in range(nlights - len(lights)):
+        l = sptr.Light()
+        l.type = 1 if i % 2 == 0 else 0
+        l.v[0], l.v[1], l.v[2] = (1.5 - 0.4 * i, 2.0 + 0.1 * i, 1.0) if l.type == 1 else (0.3, 0.8 + 0.05 * i, 0.4)
+        l.color[0], l.color[1], l.color[2] = 1.0, 0.9 - 0.05 * i, 0.8
+        l.intensity = 2.0 if l.type == 1 else 0.5
+        extra.append(l)
+    cam = sptr.camera_lookat(aspect=W / H)
+    out = {}
+    try:
+        renderer.set_lights((lights + extra)[:nlights])
+        for mode in (2, 1, 0, 3):
+            renderer.set_launch_mode(mode)
+            runs = []
+            for _ in range(2 if mode != 3 else 3):
+                st = renderer.render(cam, W, H, spp=S, max_depth=depth)
+                runs.append((renderer.read_accum().copy(), st.rays_closest, st.rays_shadow))
+            out[mode] = runs
+    finally:
+        renderer.set_launch_mode(0)
+        renderer.set_lights(lights)
+    ref = out[2][0]
+    assert ref[2] > 0
+    for mode in (2, 1, 0, 3):
+        for a in out[mode]:
+            assert np.array_equal(a[0].view(np.uint32), ref[0].view(np.uint32)), mode
+            assert a[1:] == ref[1:], mode
+
+
 @pytest.mark.parametrize("mode", [1, 3])
 def test_many_calls_without_collect(renderer, mode):
     """1500 asynchronous calls of an L2-scene frame with no collection in between, each forking k_sky
